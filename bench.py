@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark of the north-star path: CRC32C over device-resident buffers on
+MI355X through the C-ABI engine (libphoton_checksum.so).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+One "step" = one pass of the hot path over one batch (BASELINE.json configs):
+  c2 (default, configs[1]): 65,536 x 64 KiB random buffers, device-resident
+  c3: 1,048,576 x 4 KiB                c4: 32,768 x 1 MiB per GPU (the 8-GPU config's shard)
+  c5: 65,536 messages x 8 non-contiguous 8 KiB segments (per-segment CRC + combine)
+Multi-GPU: one process per GPU (torchrun); every rank checksums its own
+independent batch (weak scaling, no data-path collective; gloo is used only
+for the timing barrier and the max-over-ranks). Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from photonlibos_amd import checksum as ck  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
+GIB = float(1 << 30)
+
+CONFIGS = {
+    "c2": dict(kind="strided", nbytes=65536, count=65536,
+               workload="C2: 65536 x 64 KiB random buffers, device-resident, per GPU"),
+    "c3": dict(kind="strided", nbytes=4096, count=1 << 20,
+               workload="C3: 1048576 x 4 KiB RPC-payload buffers, device-resident, per GPU"),
+    "c4": dict(kind="strided", nbytes=1 << 20, count=32768,
+               workload="C4 shard: 32768 x 1 MiB buffers per GPU (256K x 1 MiB over 8 GPUs)"),
+    "c5": dict(kind="msg", nbytes=8192, count=65536, nseg=8,
+               workload="C5: 65536 messages x 8 non-contiguous 8 KiB segments, per-segment CRC + combine"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (profiles/*.json) giving HBM bytes per launch")
+    return ap.parse_args()
+
+
+class Workload:
+    """Device-resident synthetic batch for one config on the current device."""
+
+    def __init__(self, cfg, rank, stream):
+        self.cfg = cfg
+        self.stream = stream
+        n, cnt = cfg["nbytes"], cfg["count"]
+        seed_base = 0x5EED0001 + rank * cnt
+        self.payload = torch.empty(n * cnt, dtype=torch.uint8, device="cuda")
+        ck.fill_splitmix(self.payload, n, n, cnt, seed_base, stream=stream)
+        self.bytes_per_step = n * cnt
+        if cfg["kind"] == "strided":
+            self.out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+        else:
+            nmsg, nseg = cnt, cfg["nseg"]
+            slots = nmsg * nseg
+            # the payload above is a pool of `count` slots; re-make it with nmsg*nseg slots
+            self.payload = torch.empty(n * slots, dtype=torch.uint8, device="cuda")
+            ck.fill_splitmix(self.payload, n, n, slots, seed_base, stream=stream)
+            rng = np.random.default_rng(0x5EED0005 + rank)
+            perm = rng.permutation(slots).astype(np.uint64)
+            iov = np.empty((slots, 2), np.uint64)
+            iov[:, 0] = np.uint64(self.payload.data_ptr()) + perm * np.uint64(n)
+            iov[:, 1] = n
+            self.iov = torch.from_numpy(iov.view(np.int64)).cuda()
+            self.start = torch.from_numpy(np.arange(0, slots + 1, nseg, dtype=np.uint64).view(np.int64)).cuda()
+            self.seg_out = torch.zeros(slots, dtype=torch.int32, device="cuda")
+            self.out = torch.zeros(nmsg, dtype=torch.int32, device="cuda")
+            self.bytes_per_step = n * slots
+        torch.cuda.synchronize()
+
+    def step(self):
+        c = self.cfg
+        if c["kind"] == "strided":
+            ck.batch_strided(self.payload, c["nbytes"], c["nbytes"], c["count"], self.out, stream=self.stream)
+        else:
+            ck.batch_msg(self.iov, self.start, c["count"], self.seg_out, self.out, stream=self.stream)
+
+    def self_check(self):
+        """Spot-check 4 results against the product's own host engine (crc32c_hw)."""
+        c = self.cfg
+        n = c["nbytes"]
+        if c["kind"] != "strided":
+            return None
+        out = self.out.cpu().numpy().view(np.uint32)
+        for i in (0, 1, c["count"] // 2, c["count"] - 1):
+            host = self.payload[i * n:(i + 1) * n].cpu().numpy().tobytes()
+            if ck.crc32c_hw(host) != out[i]:
+                return False
+        return True
+
+
+def cpu_baseline(cfg, seconds):
+    """Photon's own CPU checksum (reference crc.cpp, oracle/_ref/ref_harness),
+    timed on this host; the oracle's C port as fallback."""
+    n = cfg["nbytes"]
+    nbuf = max(1, (256 << 20) // n)  # bounded 256 MiB sample of the same workload
+    threads = max(1, min(16, os.cpu_count() or 1))
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    sample = f"{nbuf} x {n} B random host buffers (256 MiB, stream 0x5EED0001+i), best pass over >= {seconds:.0f} s"
+    if os.path.exists(harness):
+        out = subprocess.run([harness, "bench", str(nbuf), str(n), str(threads), str(seconds)],
+                             capture_output=True, text=True, timeout=seconds * 4 + 120)
+        if out.returncode == 0:
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            cpu = ""
+            try:
+                cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+            except Exception:
+                pass
+            return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                    "sample": sample + f"; Photon crc32c() auto-dispatch (crc.cpp:339-358) on {threads} threads"
+                    + (f" of {cpu}" if cpu else "")}
+    # Fallback: the oracle's C restatement (slicing-by-8), one thread.
+    from tests import _oracle
+    from photonlibos_amd import datagen
+    bufs = [datagen.stream_bytes(0x5EED0001 + i, n).tobytes() for i in range(min(nbuf, 256))]
+    t0, done = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        for b in bufs:
+            _oracle.crc32c(b)
+        done += len(bufs) * n
+    return {"value": round(done / (time.perf_counter() - t0) / GIB, 3), "unit": "GiB/s", "cores": 1,
+            "kind": "port", "sample": f"{len(bufs)} x {n} B, oracle slicing-by-8, 1 thread"}
+
+
+def load_traffic(path, config):
+    if path is None:
+        path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    ck.set_lanes_per_buffer(args.lanes)
+    cfg = CONFIGS[args.config]
+    stream = torch.cuda.current_stream()
+    wl = Workload(cfg, rank, stream)
+
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize()
+    ok = wl.self_check()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        wl.step()
+        ev[s][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    total_bytes = wl.bytes_per_step * args.steps * world
+    value = total_bytes / elapsed / GIB
+    per_launch_gbps = wl.bytes_per_step / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic_json, args.config)
+
+    if rank == 0:
+        res = {
+            "metric": "GiB/s CRC32C over device-resident buffers; % of HBM-read roofline",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 random bytes generated on device)",
+            "config": {"workload": cfg["workload"], "buffers": cfg["count"], "buffer_bytes": cfg["nbytes"],
+                       "bytes_per_gpu_per_step": wl.bytes_per_step, "parallelism": f"shard-per-gpu x{world}",
+                       "lanes_per_buffer": args.lanes or "auto"},
+            "roofline": {"bound": "hbm", "achieved": round(per_launch_gbps, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(per_launch_gbps / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic},
+            "self_check": ok,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

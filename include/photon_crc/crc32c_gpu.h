@@ -1,0 +1,101 @@
+/*
+ * crc32c_gpu.h -- C-ABI of the MI355X CRC32C engine (libphoton_checksum.so).
+ *
+ * Plain pointers and sizes only; no HIP or torch types in the signatures
+ * (`stream` is a hipStream_t passed as void*, NULL = the default stream).
+ *
+ * Semantics are PhotonLibOS's raw CRC-32C (common/checksum/crc32c.h:30-45):
+ * reflected polynomial 0x82F63B78, init = caller's seed, no final xor.
+ *   out[i] = crc32c_extend(buffer_i, nbytes_i, seed_i)
+ * Every entry point below replaces a host loop over that reference call:
+ *   photon_crc32c_batch_strided  <- loop of crc32c_extend (crc32c.h:30-33) over
+ *                                   base + i*stride; with stride == nbytes and
+ *                                   seeds == 0 it is crc32c_series
+ *                                   (crc32c.h:52-57, crc.cpp:474-509)
+ *   photon_crc32c_batch_iov      <- loop of crc32c_extend over struct iovec[]
+ *                                   (common/iovector.h:56-230)
+ *   photon_crc32c_batch_msg      <- Crc32Hasher::extend_hash over each
+ *                                   message's iovector (rpc/serialize.h:239-252):
+ *                                   per-segment CRC + crc32c_combine fold
+ *                                   (crc.cpp:393-430)
+ *   photon_crc32c_combine_batch  <- loop of crc32c_combine (crc32c.h:61-66)
+ *
+ * All batch calls are asynchronous on `stream`: inputs must stay valid and
+ * outputs are ready only after the stream is synchronised. Buffers and
+ * descriptor arrays must be device-accessible (hipMalloc'd or registered /
+ * pinned host memory).
+ *
+ * Return value: 0 on success, a negative errno-style code otherwise
+ * (-ENODEV no usable gfx950 device, -EINVAL bad arguments, -EIO HIP runtime
+ * error; photon_crc_last_error() has the text). There is NO silent CPU
+ * fallback: on error nothing is computed.
+ */
+#ifndef PHOTON_CRC32C_GPU_H
+#define PHOTON_CRC32C_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same layout as struct iovec {void *iov_base; size_t iov_len;}
+ * (common/iovector.h:56-230 uses struct iovec); a struct iovec array may be
+ * passed directly. */
+typedef struct photon_crc_iovec {
+    const void* base;
+    uint64_t len;
+} photon_crc_iovec;
+
+/* Number of usable gfx950 devices (>0), or a negative error code. */
+int photon_crc_device_count(void);
+
+/* Text of the last error on this thread ("" if none). */
+const char* photon_crc_last_error(void);
+
+/* (i) Equal-length buffers: buffer i = d_base + i*stride, nbytes each.
+ * seed_i = d_seeds ? d_seeds[i] : seed0. d_out[count] receives the CRCs. */
+int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+
+/* (ii) Arbitrary buffers: d_iov[count] (device-resident descriptors); any
+ * alignment, any length (0 returns the seed). */
+int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint32_t seed0,
+                            const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+
+/* (iii) Scatter-gather messages: message m is segments
+ * [d_msg_start[m], d_msg_start[m+1]) of d_iov (d_msg_start has nmsg+1
+ * entries, d_msg_start[nmsg] = total segments). d_out[m] = the chained
+ * crc32c_extend over the message's segments starting from seed_m.
+ * d_seg_out (total segments entries) receives each segment's own CRC32C
+ * (seed 0); it is required (it is the combine kernel's input). */
+int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                            uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
+                            void* stream);
+
+/* d_out[i] = crc32c_combine(d_crc1[i], d_crc2[i], d_len2[i]) with the
+ * reference's shortcuts (crc1 == 0 -> crc2, len2 == 0 -> crc1). */
+int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,
+                                uint64_t count, uint32_t* d_out, void* stream);
+
+/* Synchronous convenience: photon_crc32c_batch_strided + stream sync. */
+int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                     uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
+
+/* Engine selection for photon_crc32c_batch_* (testing / tuning):
+ * lanes per buffer G in {4,8,16,32,64}; 0 = automatic (default). */
+int photon_crc_set_lanes_per_buffer(int g);
+
+/* Test/bench utility (not on the checksum path): fill count buffers of
+ * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
+ * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),
+ * little-endian; identical to photonlibos_amd.datagen. */
+int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                  uint64_t seed_base, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PHOTON_CRC32C_GPU_H */

@@ -1,0 +1,249 @@
+// ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (oracle side). Not product code.
+//
+// Drives the REFERENCE's own common/checksum/crc.cpp + crc_tables.cpp,
+// compiled unmodified from /root/reference by oracle/ref/Makefile, to
+//   (1) emit golden vectors (`vectors` mode) -> tests/golden/ref_vectors.json
+//       via tests/golden/gen_ref_vectors.py, and
+//   (2) time Photon's own CPU checksum (`bench` mode) for bench.py's
+//       cpu_baseline leg ("kind": "reference").
+// The only symbols the reference objects need beyond libc are alog's logger
+// (used solely by crc32c_trim's EINVAL branch, crc.cpp:444-445); they are left
+// unresolved at link time and that branch is never taken here.
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+// Declarations as in the reference's public headers (crc32c.h:20-92,
+// crc64ecma.h:20-87) and the test's extra entry points (test_checksum.cpp:86-87).
+uint32_t crc32c_sw(const uint8_t*, size_t, uint32_t);
+uint32_t crc32c_hw(const uint8_t*, size_t, uint32_t);
+uint32_t crc32c_hw_simple(const uint8_t*, size_t, uint32_t);
+uint32_t crc32c_hw_portable(const uint8_t*, size_t, uint32_t);
+void crc32c_series_sw(const uint8_t*, uint32_t, uint32_t, uint32_t*);
+void crc32c_series_hw(const uint8_t*, uint32_t, uint32_t, uint32_t*);
+uint32_t crc32c_combine_sw(uint32_t, uint32_t, uint32_t);
+uint32_t crc32c_combine_hw(uint32_t, uint32_t, uint32_t);
+uint32_t crc32c_combine_series_sw(uint32_t*, uint32_t, uint32_t);
+uint32_t crc32c_combine_series_hw(uint32_t*, uint32_t, uint32_t);
+struct CRC32C_Component { uint32_t crc; uint32_t size; };
+uint32_t crc32c_trim_sw(CRC32C_Component, CRC32C_Component, CRC32C_Component);
+uint32_t crc32c_trim_hw(CRC32C_Component, CRC32C_Component, CRC32C_Component);
+extern uint32_t (*crc32c_auto)(const uint8_t*, size_t, uint32_t);
+uint64_t crc64ecma_sw(const uint8_t*, size_t, uint64_t);
+uint64_t crc64ecma_hw_sse128(const uint8_t*, size_t, uint64_t);
+uint64_t crc64ecma_combine_sw(uint64_t, uint64_t, uint32_t);
+uint64_t crc64ecma_combine_hw(uint64_t, uint64_t, uint32_t);
+struct CRC64ECMA_Component { uint64_t crc; uint64_t size; };
+uint64_t crc64ecma_trim_sw(CRC64ECMA_Component, CRC64ECMA_Component, CRC64ECMA_Component);
+extern const uint32_t (&crc32c_lshift_table_hw)[28];
+extern const uint32_t (&crc32c_rshift_table_hw)[32];
+extern const uint32_t (&crc32c_lshift_table_sw)[32];
+extern const uint32_t (&crc32c_rshift_table_sw)[32];
+
+// splitmix64 byte stream; identical to photonlibos_amd.datagen and the
+// device generator: word k of stream `seed` = mix(seed + (k+1)*GOLDEN).
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static void fill(uint8_t* p, size_t n, uint64_t seed) {
+    for (size_t k = 0; k * 8 < n; ++k) {
+        uint64_t w = mix64(seed + (k + 1) * 0x9E3779B97F4A7C15ull);
+        size_t m = n - k * 8 < 8 ? n - k * 8 : 8;
+        memcpy(p + k * 8, &w, m);
+    }
+}
+
+struct Out {
+    std::string s;
+    bool first = true;
+    void key(const char* k) { s += first ? "\n" : ",\n"; first = false; s += "\""; s += k; s += "\": "; }
+    void arr(const char* k, const std::vector<uint64_t>& v) {
+        key(k); s += "[";
+        for (size_t i = 0; i < v.size(); ++i) { if (i) s += ","; s += std::to_string(v[i]); }
+        s += "]";
+    }
+};
+
+static int vectors() {
+    Out o;
+    std::vector<uint64_t> v;
+    for (auto x : crc32c_lshift_table_hw) v.push_back(x);
+    o.arr("lshift_table_hw", v); v.clear();
+    for (auto x : crc32c_rshift_table_hw) v.push_back(x);
+    o.arr("rshift_table_hw", v); v.clear();
+    for (auto x : crc32c_lshift_table_sw) v.push_back(x);
+    o.arr("lshift_table_sw", v); v.clear();
+    for (auto x : crc32c_rshift_table_sw) v.push_back(x);
+    o.arr("rshift_table_sw", v); v.clear();
+
+    // Alphabet pattern, lengths 0..4096 (test_checksum.cpp:70-84 pattern),
+    // checked sw == hw == hw_simple == auto; the agreed value is recorded.
+    {
+        std::vector<uint8_t> buf(4097);
+        for (size_t i = 0; i < buf.size(); ++i) buf[i] = 'a' + i % 26;
+        for (size_t n = 0; n <= 4096; ++n) {
+            uint32_t a = crc32c_sw(buf.data(), n, 0), b = crc32c_hw(buf.data(), n, 0),
+                     c = crc32c_hw_simple(buf.data(), n, 0), d = crc32c_auto(buf.data(), n, 0);
+            if (a != b || a != c || a != d) { fprintf(stderr, "sw/hw disagree at %zu\n", n); return 1; }
+            v.push_back(a);
+        }
+        o.arr("alphabet_crc32c", v); v.clear();
+    }
+    // Seeded random buffers: lengths x misalignments x seeds.
+    {
+        const size_t lens[] = {1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 127, 128,
+                               129, 255, 256, 257, 511, 512, 513, 1000, 1023, 1024, 1025, 1536, 2047,
+                               2048, 4095, 4096, 4097, 8191, 8192, 8193, 65535, 65536, 65537, 1048576};
+        const size_t offs[] = {0, 1, 3, 7, 8, 13, 15};
+        const uint32_t seeds[] = {0u, 0xFFFFFFFFu, 0x12345678u};
+        std::vector<uint8_t> buf(1048576 + 64);
+        std::vector<uint64_t> L, O, S, R, C;
+        uint64_t rs = 0x5EED0000ull;
+        for (size_t n : lens)
+            for (size_t off : offs)
+                for (uint32_t sd : seeds) {
+                    ++rs;
+                    fill(buf.data() + off, n, rs);
+                    uint32_t a = crc32c_sw(buf.data() + off, n, sd);
+                    uint32_t b = crc32c_hw(buf.data() + off, n, sd);
+                    if (a != b) { fprintf(stderr, "sw/hw disagree n=%zu off=%zu\n", n, off); return 1; }
+                    L.push_back(n); O.push_back(off); S.push_back(sd); R.push_back(rs); C.push_back(a);
+                }
+        o.arr("rand_len", L); o.arr("rand_off", O); o.arr("rand_seed", S);
+        o.arr("rand_stream", R); o.arr("rand_crc32c", C);
+    }
+    // combine: random triples + shortcut cases (crc.cpp:394-395, 425-426).
+    {
+        std::vector<uint64_t> A, B, N, Rs, Rh;
+        uint64_t st = 0xC0FFEEull;
+        for (int i = 0; i < 2000; ++i) {
+            uint64_t r = mix64(st += 0x9E3779B97F4A7C15ull);
+            uint32_t c1 = (uint32_t)r, c2 = (uint32_t)(r >> 32);
+            uint32_t l2 = (uint32_t)mix64(st += 0x9E3779B97F4A7C15ull);
+            if (i % 4 == 1) l2 &= 0xffff;
+            if (i % 4 == 2) l2 &= 0xff;
+            if (i == 3) c1 = 0;
+            if (i == 5) l2 = 0;
+            if (i == 7) { c1 = 0; l2 = 0; }
+            uint32_t s = crc32c_combine_sw(c1, c2, l2), h = crc32c_combine_hw(c1, c2, l2);
+            A.push_back(c1); B.push_back(c2); N.push_back(l2); Rs.push_back(s); Rh.push_back(h);
+        }
+        o.arr("comb_crc1", A); o.arr("comb_crc2", B); o.arr("comb_len2", N);
+        o.arr("comb_sw", Rs); o.arr("comb_hw", Rh);
+    }
+    // series (incl. part_size < 8 quirk of _hw) + combine_series over stream 0x5EEDA000.
+    {
+        std::vector<uint64_t> P, NP, Ssw, Shw, CSs, CSh;
+        const uint32_t parts[][2] = {{1, 10}, {3, 7}, {7, 5}, {8, 9}, {9, 4}, {15, 6}, {16, 16}, {17, 5},
+                                     {510, 10}, {4096, 8}, {8192, 8}, {65536, 2}};
+        std::vector<uint8_t> buf(1 << 20);
+        fill(buf.data(), buf.size(), 0x5EEDA000ull);
+        for (auto& ps : parts) {
+            std::vector<uint32_t> a(ps[1]), b(ps[1]);
+            crc32c_series_sw(buf.data(), ps[0], ps[1], a.data());
+            crc32c_series_hw(buf.data(), ps[0], ps[1], b.data());
+            P.push_back(ps[0]); NP.push_back(ps[1]);
+            for (auto x : a) Ssw.push_back(x);
+            for (auto x : b) Shw.push_back(x);
+            CSs.push_back(crc32c_combine_series_sw(a.data(), ps[0], ps[1]));
+            CSh.push_back(crc32c_combine_series_hw(a.data(), ps[0], ps[1]));
+        }
+        o.arr("series_part", P); o.arr("series_n", NP); o.arr("series_sw", Ssw);
+        o.arr("series_hw", Shw); o.arr("cseries_sw", CSs); o.arr("cseries_hw", CSh);
+    }
+    // trim (test_checksum.cpp:257-265 style) over stream 0x5EEDB000, valid sizes only.
+    {
+        std::vector<uint8_t> buf(5100);
+        fill(buf.data(), buf.size(), 0x5EEDB000ull);
+        uint32_t x = crc32c_sw(buf.data(), buf.size(), 0);
+        std::vector<uint64_t> L1, L3, Ts, Th;
+        uint64_t st = 0x7717ull;
+        for (int i = 0; i < 500; ++i) {
+            uint32_t l1 = (uint32_t)(mix64(st += 0x9E3779B97F4A7C15ull) % 2600);
+            uint32_t l3 = (uint32_t)(mix64(st += 0x9E3779B97F4A7C15ull) % (5100 - l1 + 1));
+            if (i == 0) { l1 = 0; l3 = 0; }
+            if (i == 1) { l1 = 0; l3 = 100; }
+            if (i == 2) { l1 = 100; l3 = 0; }
+            uint32_t c1 = crc32c_sw(buf.data(), l1, 0);
+            uint32_t c3 = crc32c_sw(buf.data() + 5100 - l3, l3, 0);
+            Ts.push_back(crc32c_trim_sw({x, 5100}, {c1, l1}, {c3, l3}));
+            Th.push_back(crc32c_trim_hw({x, 5100}, {c1, l1}, {c3, l3}));
+            L1.push_back(l1); L3.push_back(l3);
+        }
+        o.arr("trim_l1", L1); o.arr("trim_l3", L3); o.arr("trim_sw", Ts); o.arr("trim_hw", Th);
+        v.push_back(x); o.arr("trim_all", v); v.clear();
+    }
+    // Known answers quoted in SURVEY.md.
+    {
+        std::vector<uint8_t> ff(65536, 0xFF), z(4096, 0);
+        v.push_back(crc32c_auto((const uint8_t*)"123456789", 9, 0));
+        v.push_back(crc32c_auto(ff.data(), ff.size(), 0));
+        v.push_back(crc32c_auto(z.data(), z.size(), 0));
+        o.arr("known_answers", v); v.clear();
+    }
+    // CRC64ECMA (next row): sw over random buffers (sse128 cross-checked).
+    {
+        const size_t lens[] = {0, 1, 7, 8, 15, 16, 17, 100, 255, 256, 257, 1000, 4096, 4097, 65536};
+        std::vector<uint8_t> buf(65536 + 16);
+        std::vector<uint64_t> L, C;
+        uint64_t rs = 0x5EED6400ull;
+        for (size_t n : lens) {
+            fill(buf.data(), n, ++rs);
+            uint64_t a = crc64ecma_sw(buf.data(), n, 0), b = crc64ecma_hw_sse128(buf.data(), n, 0);
+            if (a != b) { fprintf(stderr, "crc64 sw/sse disagree n=%zu\n", n); return 1; }
+            L.push_back(n); C.push_back(a);
+        }
+        o.arr("crc64_len", L); o.arr("crc64_sw", C);
+    }
+    printf("{%s\n}\n", o.s.c_str());
+    return 0;
+}
+
+// `bench <nbuf> <len> <threads> <min_seconds>`: Photon's crc32c() (auto
+// dispatch, crc.cpp:339-358 on SSE4.2 hosts) over nbuf random buffers of len
+// bytes (stream 0x5EED0001 + i), split across threads; best pass of several.
+static int bench(size_t nbuf, size_t len, int threads, double min_s) {
+    std::vector<uint8_t> buf(nbuf * len);
+    for (size_t i = 0; i < nbuf; ++i) fill(buf.data() + i * len, len, 0x5EED0001ull + i);
+    std::vector<uint32_t> out(nbuf);
+    auto pass = [&]() {
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t]() {
+                size_t b = nbuf * t / threads, e = nbuf * (t + 1) / threads;
+                for (size_t i = b; i < e; ++i) out[i] = crc32c_auto(buf.data() + i * len, len, 0);
+            });
+        for (auto& x : th) x.join();
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    };
+    double best = 1e30, total = 0;
+    int passes = 0;
+    while (total < min_s || passes < 3) {
+        double t = pass();
+        best = t < best ? t : best;
+        total += t;
+        ++passes;
+    }
+    uint32_t x = 0;
+    for (auto c : out) x ^= c;
+    printf("{\"gib_per_s\": %.4f, \"best_s\": %.6f, \"passes\": %d, \"threads\": %d, \"nbuf\": %zu, "
+           "\"len\": %zu, \"xor_of_crcs\": %u}\n",
+           (double)nbuf * len / best / (1u << 30), best, passes, threads, nbuf, len, x);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc >= 2 && !strcmp(argv[1], "vectors")) return vectors();
+    if (argc >= 6 && !strcmp(argv[1], "bench"))
+        return bench(strtoull(argv[2], 0, 0), strtoull(argv[3], 0, 0), atoi(argv[4]), atof(argv[5]));
+    fprintf(stderr, "usage: %s vectors | bench <nbuf> <len> <threads> <min_seconds>\n", argv[0]);
+    return 2;
+}

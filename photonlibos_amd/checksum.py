@@ -1,0 +1,240 @@
+"""Host-side mirror of PhotonLibOS common/checksum (CRC32C) over the C-ABI
+library libphoton_checksum.so.
+
+Two layers, both thin bindings (no arithmetic in Python):
+
+* Drop-in entry points with the reference's names and meaning
+  (common/checksum/crc32c.h:20-92): crc32c, crc32c_extend, crc32c_series,
+  crc32c_combine, crc32c_combine_series, crc32c_trim (+ the _sw/_hw engines),
+  bound to the library's exported C++ symbols and dispatch pointers.
+* The batched device engine (include/photon_crc/crc32c_gpu.h):
+  batch_strided / batch_iov / batch_msg / combine_batch. Arguments are device
+  pointers (ints) or objects exposing .data_ptr() (e.g. torch tensors);
+  `stream` is a hipStream_t handle (int) or an object with .cuda_stream.
+  Errors raise CrcError; nothing falls back to the CPU.
+"""
+import ctypes
+
+from ._native import lib
+
+__all__ = [
+    "CrcError",
+    "crc32c", "crc32c_extend", "crc32c_sw", "crc32c_hw", "crc32c_hw_simple", "crc32c_hw_portable",
+    "crc32c_series", "crc32c_series_sw", "crc32c_series_hw",
+    "crc32c_combine", "crc32c_combine_sw", "crc32c_combine_hw",
+    "crc32c_combine_series", "crc32c_combine_series_sw", "crc32c_combine_series_hw",
+    "crc32c_trim", "crc32c_trim_sw", "crc32c_trim_hw", "is_crc32c_hw_available",
+    "device_count", "set_lanes_per_buffer", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
+    "combine_batch", "fill_splitmix", "IOVEC_DTYPE",
+]
+
+_CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
+_SERIES_FN = ctypes.CFUNCTYPE(None, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                              ctypes.POINTER(ctypes.c_uint32))
+_COMB_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32)
+_CSER_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_uint32)
+_TRIM_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64)
+
+
+class CrcError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"photon_crc error {code}: {what}")
+        self.code = code
+
+
+def _auto(name, proto):
+    return proto(lib().auto[name].value)
+
+
+def _buf(data):
+    if isinstance(data, str):
+        data = data.encode()
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        return bytes(mv), len(mv)
+    return (ctypes.c_char * len(mv)).from_buffer(mv), len(mv)
+
+
+# ---------------------------------------------------------------- drop-in API
+
+def crc32c_extend(data, crc):
+    """crc32c_extend(data, nbytes, crc) (crc32c.h:30-33, 39-41)."""
+    b, n = _buf(data)
+    return _auto("crc32c_auto", _CRC_FN)(ctypes.cast(b, ctypes.c_char_p) if not isinstance(b, bytes) else b,
+                                         n, crc & 0xFFFFFFFF)
+
+
+def crc32c(data):
+    """crc32c(data, nbytes) == crc32c_extend(data, nbytes, 0) (crc32c.h:35-45)."""
+    return crc32c_extend(data, 0)
+
+
+def _engine(name):
+    def f(data, crc=0):
+        b, n = _buf(data)
+        return lib().cpp[name](ctypes.cast(b, ctypes.c_char_p) if not isinstance(b, bytes) else b, n,
+                               crc & 0xFFFFFFFF)
+    f.__name__ = name
+    f.__doc__ = f"{name}(buffer, nbytes, crc) (crc32c.h:20-22)."
+    return f
+
+
+crc32c_sw = _engine("crc32c_sw")
+crc32c_hw = _engine("crc32c_hw")
+crc32c_hw_simple = _engine("crc32c_hw_simple")
+crc32c_hw_portable = _engine("crc32c_hw_portable")
+
+
+def _series(fn, buffer, part_size, n_parts):
+    b, n = _buf(buffer)
+    out = (ctypes.c_uint32 * max(n_parts, 1))()
+    fn(ctypes.cast(b, ctypes.c_char_p) if not isinstance(b, bytes) else b, part_size, n_parts, out)
+    return list(out)[:n_parts]
+
+
+def crc32c_series(buffer, part_size, n_parts):
+    """crc32c_series (crc32c.h:47-57): CRCs of n_parts consecutive parts."""
+    return _series(_auto("crc32c_series_auto", _SERIES_FN), buffer, part_size, n_parts)
+
+
+def crc32c_series_sw(buffer, part_size, n_parts):
+    return _series(lib().cpp["crc32c_series_sw"], buffer, part_size, n_parts)
+
+
+def crc32c_series_hw(buffer, part_size, n_parts):
+    return _series(lib().cpp["crc32c_series_hw"], buffer, part_size, n_parts)
+
+
+def crc32c_combine(crc1, crc2, len2):
+    """crc32c_combine (crc32c.h:59-66): crc(A||B) from crc(A), crc(B), |B|."""
+    return _auto("crc32c_combine_auto", _COMB_FN)(crc1, crc2, len2)
+
+
+def crc32c_combine_sw(crc1, crc2, len2):
+    return lib().cpp["crc32c_combine_sw"](crc1, crc2, len2)
+
+
+def crc32c_combine_hw(crc1, crc2, len2):
+    return lib().cpp["crc32c_combine_hw"](crc1, crc2, len2)
+
+
+def _cseries(fn, crcs, part_size):
+    arr = (ctypes.c_uint32 * max(len(crcs), 1))(*crcs)
+    return fn(arr, part_size, len(crcs))
+
+
+def crc32c_combine_series(crcs, part_size):
+    """crc32c_combine_series (crc32c.h:68-74); 0 for an empty list."""
+    return _cseries(_auto("crc32c_combine_series_auto", _CSER_FN), crcs, part_size)
+
+
+def crc32c_combine_series_sw(crcs, part_size):
+    return _cseries(lib().cpp["crc32c_combine_series_sw"], crcs, part_size)
+
+
+def crc32c_combine_series_hw(crcs, part_size):
+    return _cseries(lib().cpp["crc32c_combine_series_hw"], crcs, part_size)
+
+
+def _comp(c):
+    crc, size = c
+    return (crc & 0xFFFFFFFF) | ((size & 0xFFFFFFFF) << 32)
+
+
+def _trim(fn, all_, prefix, suffix):
+    return fn(_comp(all_), _comp(prefix), _comp(suffix))
+
+
+def crc32c_trim(all_, prefix, suffix):
+    """crc32c_trim (crc32c.h:76-87); components are (crc, size) pairs.
+    Inconsistent sizes: returns 0 with errno = EINVAL, like the reference."""
+    return _trim(_auto("crc32c_trim_auto", _TRIM_FN), all_, prefix, suffix)
+
+
+def crc32c_trim_sw(all_, prefix, suffix):
+    return _trim(lib().cpp["crc32c_trim_sw"], all_, prefix, suffix)
+
+
+def crc32c_trim_hw(all_, prefix, suffix):
+    return _trim(lib().cpp["crc32c_trim_hw"], all_, prefix, suffix)
+
+
+def is_crc32c_hw_available():
+    """crc32c.h:89-92."""
+    L = lib()
+    return L.auto["crc32c_auto"].value != ctypes.cast(L.cpp["crc32c_sw"], ctypes.c_void_p).value
+
+
+# ---------------------------------------------------------- batched device API
+
+IOVEC_DTYPE = [("base", "<u8"), ("len", "<u8")]  # == struct iovec / photon_crc_iovec
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    raise TypeError(f"expected a device pointer (int) or an object with data_ptr(), got {type(x)!r}")
+
+
+def _stream(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    return s.cuda_stream
+
+
+def _check(rc):
+    if rc != 0:
+        raise CrcError(rc, lib().photon_crc_last_error().decode(errors="replace"))
+
+
+def device_count():
+    """Number of usable gfx950 devices; raises CrcError if there is none."""
+    n = lib().photon_crc_device_count()
+    if n < 0:
+        _check(n)
+    return n
+
+
+def set_lanes_per_buffer(g):
+    """Lanes per buffer for the batch kernels (0 = automatic, else 4..64)."""
+    _check(lib().photon_crc_set_lanes_per_buffer(g))
+
+
+def batch_strided(base, stride, nbytes, count, out, seed=0, seeds=None, stream=None):
+    """out[i] = crc32c_extend(base + i*stride, nbytes, seeds[i] or seed). Async."""
+    _check(lib().photon_crc32c_batch_strided(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFF, _ptr(seeds),
+                                             _ptr(out), _stream(stream)))
+
+
+def batch_strided_sync(base, stride, nbytes, count, out, seed=0, seeds=None, stream=None):
+    _check(lib().photon_crc32c_batch_strided_sync(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFF,
+                                                  _ptr(seeds), _ptr(out), _stream(stream)))
+
+
+def batch_iov(iov, count, out, seed=0, seeds=None, stream=None):
+    """out[i] = crc32c_extend(iov[i].base, iov[i].len, seed_i). Async."""
+    _check(lib().photon_crc32c_batch_iov(_ptr(iov), count, seed & 0xFFFFFFFF, _ptr(seeds), _ptr(out),
+                                         _stream(stream)))
+
+
+def batch_msg(iov, msg_start, nmsg, seg_out, out, seed=0, seeds=None, stream=None):
+    """out[m] = chained crc32c_extend over message m's segments. Async."""
+    _check(lib().photon_crc32c_batch_msg(_ptr(iov), _ptr(msg_start), nmsg, seed & 0xFFFFFFFF, _ptr(seeds),
+                                         _ptr(seg_out), _ptr(out), _stream(stream)))
+
+
+def combine_batch(crc1, crc2, len2, count, out, stream=None):
+    """out[i] = crc32c_combine(crc1[i], crc2[i], len2[i]). Async."""
+    _check(lib().photon_crc32c_combine_batch(_ptr(crc1), _ptr(crc2), _ptr(len2), count, _ptr(out),
+                                             _stream(stream)))
+
+
+def fill_splitmix(base, stride, nbytes, count, seed_base, stream=None):
+    """Test/bench utility: device buffers = photonlibos_amd.datagen streams."""
+    _check(lib().photon_crc_util_fill_splitmix(_ptr(base), stride, nbytes, count, seed_base, _stream(stream)))

@@ -1,0 +1,558 @@
+// crc32c_device.hip -- MI355X (gfx950) CRC32C engine behind the C-ABI of
+// include/photon_crc/crc32c_gpu.h.
+//
+// What it computes: PhotonLibOS's raw CRC-32C, crc32c_extend(data, n, seed)
+// (reference common/checksum/crc32c.h:30-33; engines crc.cpp:114-117,
+// 339-368), for batches of independent device-resident buffers.
+//
+// How (DESIGN.md "Kernel"): a group of G lanes (G = 64: one wavefront per
+// buffer; G < 64 packs 64/G small buffers per wavefront) walks the buffer in
+// rows of G 16-byte blocks: lane l of the group loads block (row*G + l) with
+// one coalesced global_load_dwordx4, so a row is one contiguous 16*G-byte
+// sweep. Each lane keeps a partial CRC over "its" blocks as if the other
+// lanes' bytes were zeros, so between two of its blocks it must skip
+// gap = 16*(G-1) zero bytes: P <- P * x^(8*gap) mod P, folded into the first
+// word's table step. All GF(2) products by constants are byte-sliced LDS
+// table lookups (no carry-less multiply on CDNA4, no MFMA: this is GF(2)):
+//   D tables: x -> x * x^32 mod P, 4 byte slices, replicated 32x so that lane
+//             l always hits bank l%32 (conflict-free random lookups), 128 KiB;
+//   S tables: P -> P * x^(8*gap+32) mod P, 4 slices, 4 replicas, 16 KiB.
+// At the end lane l multiplies its partial by x^(128*d_l), d_l = number of
+// 16-byte blocks between its last block and the end (6 constant-basis GF(2)
+// multiplies, bits of d_l), and the group XOR-reduces with __shfl_xor.
+// Unaligned heads use zero-prefix invariance (crc.md:24-32): the leading
+// bytes of the first aligned block are masked to 0 and the seed is XORed into
+// the first four data bytes (init-value linearity), so every load is an
+// aligned 16-byte load. Ragged tails (<16 B) are finished byte-serially.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/photon_crc/crc32c_gpu.h"
+#include "gf2.h"
+
+namespace pcrc {
+
+// ------------------------------------------------------------------ LDS map
+constexpr uint32_t kDataBytes = 2u * 65536u;   // 4 slices x 256 idx x 32 replicas x 4 B
+constexpr uint32_t kShiftBase = kDataBytes;    // S tables follow
+constexpr uint32_t kShiftBytes = 4u * 4096u;   // 4 slices x 256 idx x 4 replicas x 4 B
+constexpr uint32_t kLdsBytes = kShiftBase + kShiftBytes;  // 147456 B of the 160 KiB
+constexpr int kBlock = 1024;                   // 16 waves, one workgroup per CU
+constexpr int kWaves = kBlock / 64;
+
+// Kernel constants computed on the host (gf2.h) per lanes-per-buffer G.
+struct LaneConsts {
+    uint32_t kshift;           // x^(8*16*(G-1) + 32) mod P
+    uint32_t basis[6][32];     // basis of x^(128 * 2^k) mod P, k = 0..5
+};
+
+struct BatchArgs {
+    const uint8_t* base;       // strided mode
+    uint64_t stride;
+    uint64_t nbytes;
+    const photon_crc_iovec* iov;  // iov mode when non-null
+    uint64_t count;
+    const uint32_t* seeds;     // optional
+    uint32_t* out;
+    uint32_t seed0;
+};
+
+__device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+
+// Per-lane LDS base addresses: D slice t lives at ((t>>1)<<16) + idx*256 +
+// ((t&1)<<7) + (lane&31)*4, so its address is (idx << 8) | d[t].
+struct LaneAddr {
+    uint32_t d0, d1, d2, d3, s;
+};
+
+// x * x^32 mod P = CRC register after absorbing the 32-bit word x.
+__device__ __forceinline__ uint32_t dstep(const uint32_t* lds, uint32_t x, const LaneAddr& a) {
+    const uint32_t t0 = lds_word(lds, ((x << 8) & 0xff00u) | a.d0);
+    const uint32_t t1 = lds_word(lds, (x & 0xff00u) | a.d1);
+    const uint32_t t2 = lds_word(lds, ((x >> 8) & 0xff00u) | a.d2);
+    const uint32_t t3 = lds_word(lds, ((x >> 16) & 0xff00u) | a.d3);
+    return t0 ^ t1 ^ t2 ^ t3;
+}
+
+// P * x^(8*gap+32) mod P through the S tables (slice t at s + t*4096 + idx*16).
+__device__ __forceinline__ uint32_t sstep(const uint32_t* lds, uint32_t p, uint32_t s) {
+    const uint32_t t0 = lds_word(lds, s + ((p << 4) & 0xff0u));
+    const uint32_t t1 = lds_word(lds, s + 4096u + ((p >> 4) & 0xff0u));
+    const uint32_t t2 = lds_word(lds, s + 8192u + ((p >> 12) & 0xff0u));
+    const uint32_t t3 = lds_word(lds, s + 12288u + ((p >> 20) & 0xff0u));
+    return t0 ^ t1 ^ t2 ^ t3;
+}
+
+// Byte-serial step with the D3 slice (D3[b] = b<<24 * x^32 = b * x^8, the
+// classic byte table).
+__device__ __forceinline__ uint32_t bytestep(const uint32_t* lds, uint32_t c, uint8_t b, const LaneAddr& a) {
+    const uint32_t x = c ^ b;
+    return lds_word(lds, ((x << 8) & 0xff00u) | a.d3) ^ (c >> 8);
+}
+
+// One 16-byte block of this lane's stream, `gap` zero bytes after the previous one.
+__device__ __forceinline__ uint32_t block_step(const uint32_t* lds, uint32_t p, uint4 w, const LaneAddr& a) {
+    uint32_t c = sstep(lds, p, a.s) ^ dstep(lds, w.x, a);
+    c = dstep(lds, c ^ w.y, a);
+    c = dstep(lds, c ^ w.z, a);
+    return dstep(lds, c ^ w.w, a);
+}
+
+// Word at byte offset `off` (relative to the aligned start A0) of the first
+// two blocks: zero the bytes before the data start s0 and XOR the seed into
+// data bytes s0..s0+3 (CRC with init s == CRC with init 0 of the data whose
+// first 4 bytes are XORed with s; leading zeros do not change a CRC).
+__device__ __forceinline__ uint32_t head_word(uint32_t w, int off, int s0, uint32_t seed) {
+    const int k = s0 - off;
+    if (k >= 4) return 0u;
+    if (k > 0) w &= 0xffffffffu << (8 * k);
+    if (k >= 0) w ^= seed << (8 * k);
+    else if (k > -4) w ^= seed >> (8 * -k);
+    return w;
+}
+
+__device__ __forceinline__ uint32_t mul_basis_dev(uint32_t p, const uint32_t* basis) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) r ^= (0u - ((p >> i) & 1u)) & basis[i];
+    return r;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+// Streaming 16-byte global load (every payload byte is read exactly once).
+// The explicit global address space keeps it a global_load_dwordx4: a flat
+// load would also count on lgkmcnt and serialise against the LDS lookups.
+__device__ __forceinline__ uint4 load16(const uint8_t* p) {
+    const u32x4 v = __builtin_nontemporal_load((g_u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint8_t load8(const uint8_t* p) { return *(g_u8*)p; }
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+
+    // ---- build the tables (every workgroup; 1024 threads = 1024 entries)
+    {
+        const uint32_t tid = threadIdx.x;
+        const uint32_t t = tid >> 8, b = tid & 255u;
+        const uint32_t v = b << (8 * t);
+        const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
+        const uint32_t dbase = (((t >> 1) << 16) + (b << 8) + ((t & 1) << 7)) >> 2;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) lds[dbase + r] = dv;
+        const uint32_t sv = mulmod(v, kc.kshift);
+        const uint32_t sbase = (kShiftBase + t * 4096u + b * 16u) >> 2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds[sbase + r] = sv;
+    }
+    __syncthreads();
+
+    constexpr int GPW = 64 / G;  // buffers per wavefront
+    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
+    constexpr int U = 4;         // rows in flight per lane
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+
+    LaneAddr la;
+    la.d0 = ((lane & 31u) << 2);
+    la.d1 = (1u << 7) | ((lane & 31u) << 2);
+    la.d2 = (1u << 16) | ((lane & 31u) << 2);
+    la.d3 = (1u << 16) | (1u << 7) | ((lane & 31u) << 2);
+    la.s = kShiftBase + ((lane & 3u) << 2);
+
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.count; wv += nwaves) {
+        const uint64_t bi = wv * GPW + grp;
+        const bool active = bi < args.count;
+        const uint8_t* p = nullptr;
+        uint64_t n = 0;
+        uint32_t seed = args.seed0;
+        if (active) {
+            if (args.iov) {
+                p = static_cast<const uint8_t*>(args.iov[bi].base);
+                n = args.iov[bi].len;
+            } else {
+                p = args.base + bi * args.stride;
+                n = args.nbytes;
+            }
+            if (args.seeds) seed = args.seeds[bi];
+        }
+
+        uint32_t crc;
+        if (n < 64) {
+            // Tiny buffer: byte-serial on the group's first lane.
+            crc = seed;
+            if (gl == 0)
+                for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
+        } else {
+            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+            const uint8_t* e = p + n;
+            const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
+            const int s0 = (int)(p - a0);
+            const uint64_t nb = (uint64_t)(eb - a0) >> 4;  // >= 3 blocks since n >= 64
+            const uint64_t full = nb / G;                   // rows where every lane has a block
+            const uint64_t rows = (nb + G - 1) / G;
+            const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);  // blocks in the last row, 1..G
+            const uint8_t* lp = a0 + 16 * gl;               // this lane's block in row 0
+
+            // Row 0 (holds the head: masked leading bytes + seed).
+            uint32_t pc = 0;
+            if (gl < nb) {
+                uint4 w = load16(lp);
+                if (gl < 2) {
+                    const int off = (int)gl * 16;
+                    w.x = head_word(w.x, off, s0, seed);
+                    w.y = head_word(w.y, off + 4, s0, seed);
+                    w.z = head_word(w.z, off + 8, s0, seed);
+                    w.w = head_word(w.w, off + 12, s0, seed);
+                }
+                pc = block_step(lds, 0u, w, la);
+            }
+            // Full rows 1..full-1: branch-free, U rows in flight while U are processed.
+            uint64_t row = 1;
+            if (row + U <= full) {
+                uint4 cur[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
+                for (; row + 2 * U <= full; row += U) {
+                    uint4 nxt[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+#pragma unroll
+                    for (int u = 0; u < U; ++u) pc = block_step(lds, pc, cur[u], la);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) pc = block_step(lds, pc, cur[u], la);
+                row += U;
+            }
+            for (; row < full; ++row) pc = block_step(lds, pc, load16(lp + row * (16 * G)), la);
+            // Partial last row.
+            if (full >= 1 && full < rows && full * G + gl < nb) pc = block_step(lds, pc, load16(lp + full * (16 * G)), la);
+
+            // Shift each partial to the end of the body: d = (rlast-1-gl) mod G blocks.
+            const uint32_t d = (rlast + G - 1 - gl) & (G - 1);
+#pragma unroll
+            for (int k = 0; k < LOG2G; ++k)
+                if ((d >> k) & 1u) pc = mul_basis_dev(pc, kc.basis[k]);
+#pragma unroll
+            for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
+            crc = pc;
+            // Ragged tail (< 16 bytes) after the last aligned block.
+            if (gl == 0)
+                for (const uint8_t* q = eb; q < e; ++q) crc = bytestep(lds, crc, load8(q), la);
+        }
+        if (active && gl == 0) args.out[bi] = crc;
+    }
+}
+
+// Per-message fold of per-segment CRCs: acc = seed; acc = acc*x^(8 len)+crc.
+// (Crc32Hasher::extend_hash, rpc/serialize.h:244-252, equals this fold.)
+struct PowTable {
+    uint32_t x8pow2[64];  // x^(8 * 2^i) mod P
+};
+
+__device__ __forceinline__ uint32_t shift_bytes_tab(uint32_t crc, uint64_t n, const PowTable& t) {
+    for (int i = 0; n; ++i, n >>= 1)
+        if (n & 1) crc = mulmod(crc, t.x8pow2[i]);
+    return crc;
+}
+
+__global__ void crc32c_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_t* msg_start, uint64_t nmsg,
+                                       const uint32_t* seg_crc, uint32_t seed0, const uint32_t* seeds,
+                                       uint32_t* out, PowTable pt) {
+    const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= nmsg) return;
+    uint32_t acc = seeds ? seeds[m] : seed0;
+    for (uint64_t s = msg_start[m]; s < msg_start[m + 1]; ++s)
+        acc = shift_bytes_tab(acc, iov[s].len, pt) ^ seg_crc[s];
+    out[m] = acc;
+}
+
+__global__ void crc32c_combine_kernel(const uint32_t* c1, const uint32_t* c2, const uint32_t* l2, uint64_t n,
+                                      uint32_t* out, PowTable pt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t a = c1[i], b = c2[i], len = l2[i];
+    // crc.cpp:394-395 / 425-426 shortcuts, then crc1 * x^(8 len2) ^ crc2.
+    out[i] = !a ? b : !len ? a : (shift_bytes_tab(a, len, pt) ^ b);
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_splitmix_kernel(uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                     uint64_t seed_base) {
+    const uint64_t wpb = (nbytes + 7) / 8;
+    const uint64_t total = wpb * count;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = g / wpb, k = g - b * wpb;
+        const uint64_t w = mix64(seed_base + b + (k + 1) * 0x9E3779B97F4A7C15ull);
+        uint8_t* dst = base + b * stride + k * 8;
+        const uint64_t m = nbytes - k * 8 < 8 ? nbytes - k * 8 : 8;
+        if (m == 8 && (reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+            *reinterpret_cast<uint64_t*>(dst) = w;
+        } else {
+            for (uint64_t j = 0; j < m; ++j) dst[j] = (uint8_t)(w >> (8 * j));
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+
+thread_local std::string g_err;
+int g_lanes_override = 0;
+
+int fail(int code, const std::string& what) {
+    g_err = what;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(-EIO, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceInfo {
+    bool probed = false;
+    bool ok = false;
+    int cus = 0;
+};
+
+std::mutex g_mu;
+std::vector<DeviceInfo> g_dev;
+
+// Resolve the current device; only gfx950 is supported (no other code path).
+int current_device(int* cus) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
+    DeviceInfo& di = g_dev[dev];
+    if (!di.probed) {
+        hipDeviceProp_t prop;
+        e = hipGetDeviceProperties(&prop, dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        di.ok = strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+        di.cus = prop.multiProcessorCount;
+        di.probed = true;
+        if (!di.ok) g_err = std::string("device is ") + prop.gcnArchName + ", need gfx950";
+    }
+    if (!di.ok) return fail(-ENODEV, "photon_crc: no gfx950 device (got other arch)");
+    *cus = di.cus;
+    return dev;
+}
+
+LaneConsts make_lane_consts(int g) {
+    LaneConsts c;
+    c.kshift = xpow(8ull * 16ull * (uint64_t)(g - 1) + 32ull);
+    for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), c.basis[k]);
+    return c;
+}
+
+const LaneConsts& lane_consts(int g) {
+    static LaneConsts tab[7];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int lg = 2; lg <= 6; ++lg) tab[lg] = make_lane_consts(1 << lg);
+    });
+    int lg = g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2;
+    return tab[lg];
+}
+
+const PowTable& pow_table() {
+    static PowTable t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        uint32_t v = xpow(8);  // x^8
+        for (int i = 0; i < 64; ++i) {
+            t.x8pow2[i] = v;
+            v = mulmod(v, v);
+        }
+    });
+    return t;
+}
+
+// Lanes per buffer: one wavefront per buffer for large buffers; pack small
+// buffers so every lane still walks >= 16 rows (DESIGN.md "Lane groups").
+int choose_lanes(uint64_t typical_len) {
+    if (g_lanes_override) return g_lanes_override;
+    if (typical_len >= 16384) return 64;
+    if (typical_len >= 8192) return 32;
+    if (typical_len >= 4096) return 16;
+    if (typical_len >= 2048) return 8;
+    return 4;
+}
+
+int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
+    if (a.count == 0) return 0;
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const int g = choose_lanes(typical_len);
+    const uint64_t gpw = 64 / g;
+    const uint64_t waves = (a.count + gpw - 1) / gpw;
+    uint64_t grid = (waves + kWaves - 1) / kWaves;
+    if (grid > (uint64_t)cus) grid = cus;
+    const LaneConsts& kc = lane_consts(g);
+    switch (g) {
+        case 64: hipLaunchKernelGGL(crc32c_batch_kernel<64>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        case 32: hipLaunchKernelGGL(crc32c_batch_kernel<32>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        case 16: hipLaunchKernelGGL(crc32c_batch_kernel<16>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        case 8: hipLaunchKernelGGL(crc32c_batch_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        default: hipLaunchKernelGGL(crc32c_batch_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "crc32c_batch_kernel launch");
+    return 0;
+}
+
+}  // namespace
+}  // namespace pcrc
+
+using namespace pcrc;
+
+extern "C" {
+
+int photon_crc_device_count(void) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    int ok = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++ok;
+    }
+    if (!ok) return fail(-ENODEV, "photon_crc: no gfx950 device");
+    return ok;
+}
+
+const char* photon_crc_last_error(void) { return g_err.c_str(); }
+
+int photon_crc_set_lanes_per_buffer(int g) {
+    if (g != 0 && g != 4 && g != 8 && g != 16 && g != 32 && g != 64)
+        return fail(-EINVAL, "lanes per buffer must be 0, 4, 8, 16, 32 or 64");
+    g_lanes_override = g;
+    return 0;
+}
+
+int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
+    if (count && (!d_out || (!d_base && nbytes))) return fail(-EINVAL, "null buffer or output");
+    BatchArgs a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.stride = stride;
+    a.nbytes = nbytes;
+    a.iov = nullptr;
+    a.count = count;
+    a.seeds = d_seeds;
+    a.out = d_out;
+    a.seed0 = seed0;
+    return launch_batch(a, nbytes, static_cast<hipStream_t>(stream));
+}
+
+int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                     uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
+    int rc = photon_crc32c_batch_strided(d_base, stride, nbytes, count, seed0, d_seeds, d_out, stream);
+    if (rc) return rc;
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}
+
+int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint32_t seed0,
+                            const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
+    if (count && (!d_iov || !d_out)) return fail(-EINVAL, "null descriptor array or output");
+    BatchArgs a{};
+    a.iov = d_iov;
+    a.count = count;
+    a.seeds = d_seeds;
+    a.out = d_out;
+    a.seed0 = seed0;
+    // Descriptors live on the device; lengths are unknown to the host, so the
+    // lane-group size is the generic one unless overridden.
+    return launch_batch(a, 65536, static_cast<hipStream_t>(stream));
+}
+
+int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                            uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
+                            void* stream) {
+    if (!nmsg) return 0;
+    if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t nseg = 0;
+    hipError_t e = hipMemcpyAsync(&nseg, d_msg_start + nmsg, sizeof(nseg), hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(msg_start)");
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    BatchArgs a{};
+    a.iov = d_iov;
+    a.count = nseg;
+    a.out = d_seg_out;
+    a.seed0 = 0;
+    int rc = launch_batch(a, 8192, st);
+    if (rc) return rc;
+    const int bs = 256;
+    hipLaunchKernelGGL(crc32c_msg_fold_kernel, dim3((nmsg + bs - 1) / bs), dim3(bs), 0, st, d_iov, d_msg_start,
+                       nmsg, d_seg_out, seed0, d_seeds, d_out, pow_table());
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "crc32c_msg_fold_kernel launch");
+    return 0;
+}
+
+int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,
+                                uint64_t count, uint32_t* d_out, void* stream) {
+    if (!count) return 0;
+    if (!d_crc1 || !d_crc2 || !d_len2 || !d_out) return fail(-EINVAL, "null argument");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const int bs = 256;
+    hipLaunchKernelGGL(crc32c_combine_kernel, dim3((count + bs - 1) / bs), dim3(bs), 0,
+                       static_cast<hipStream_t>(stream), d_crc1, d_crc2, d_len2, count, d_out, pow_table());
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "crc32c_combine_kernel launch");
+    return 0;
+}
+
+int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                  uint64_t seed_base, void* stream) {
+    if (!count || !nbytes) return 0;
+    if (!d_base) return fail(-EINVAL, "null buffer");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const uint64_t words = (nbytes + 7) / 8 * count;
+    uint64_t grid = (words + 255) / 256;
+    if (grid > (uint64_t)cus * 16) grid = (uint64_t)cus * 16;
+    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<uint8_t*>(d_base), stride, nbytes, count, seed_base);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "fill_splitmix_kernel launch");
+    return 0;
+}
+
+}  // extern "C"

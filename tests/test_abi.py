@@ -1,0 +1,79 @@
+"""The C-ABI library loads and exports every symbol the public headers
+declare; without a GPU the device entry points fail loudly (no compute, no
+CPU fallback). CPU only."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from photonlibos_amd import _native
+from photonlibos_amd import checksum as ck
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _exported():
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _native.LIB_PATH], text=True)
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def _c_abi_functions():
+    txt = open(os.path.join(REPO, "include", "photon_crc", "crc32c_gpu.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(photon_crc\w*)\s*\(", txt)))
+
+
+def test_c_abi_symbols_exported():
+    names = _c_abi_functions()
+    assert len(names) >= 9
+    exp = _exported()
+    missing = [n for n in names if n not in exp]
+    assert not missing, missing
+
+
+def test_dropin_symbols_exported():
+    # The reference's exported C++ symbols, same mangling.
+    want = [
+        "_Z9crc32c_swPKhmj", "_Z9crc32c_hwPKhmj", "_Z16crc32c_hw_simplePKhmj", "_Z18crc32c_hw_portablePKhmj",
+        "_Z16crc32c_series_swPKhjjPj", "_Z16crc32c_series_hwPKhjjPj", "_Z17crc32c_combine_swjjj",
+        "_Z17crc32c_combine_hwjjj", "_Z24crc32c_combine_series_swPjjj", "_Z24crc32c_combine_series_hwPjjj",
+        "_Z14crc32c_trim_sw16CRC32C_ComponentS_S_", "_Z14crc32c_trim_hw16CRC32C_ComponentS_S_",
+        "crc32c_auto", "crc32c_series_auto", "crc32c_combine_auto", "crc32c_combine_series_auto",
+        "crc32c_trim_auto",
+    ]
+    exp = _exported()
+    assert not [w for w in want if w not in exp]
+
+
+def test_header_declarations_are_exported():
+    # Every non-inline function declared in the drop-in header is defined by the library.
+    txt = open(os.path.join(REPO, "include", "photon", "common", "checksum", "crc32c.h")).read()
+    decl = re.findall(r"^(?:uint32_t|void)\s+(crc32c_\w+)\(", txt, flags=re.M)
+    demangled = subprocess.check_output(["nm", "-DC", "--defined-only", _native.LIB_PATH], text=True)
+    for d in decl:
+        assert re.search(rf"\b{d}\(", demangled), d
+
+
+def test_library_is_gfx950_only():
+    # One code object, for gfx950, and no other GPU target (no multi-arch dispatch).
+    blob = open(_native.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
+    assert set(re.findall(rb"\bgfx[0-9]{3,4}[a-z]?\b", blob)) == {b"gfx950"}
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
+def test_device_calls_fail_loudly_without_gpu():
+    with pytest.raises(ck.CrcError):
+        ck.device_count()
+    with pytest.raises(ck.CrcError):
+        ck.batch_strided(0x1000, 4096, 4096, 1, 0x2000)
+
+
+def test_argument_validation():
+    with pytest.raises(ck.CrcError) as e:
+        ck.set_lanes_per_buffer(3)
+    assert e.value.code == -22
+    with pytest.raises(ck.CrcError):
+        ck.batch_strided(None, 4096, 4096, 4, None)

@@ -1,0 +1,123 @@
+"""The host drop-in entry points of libphoton_checksum.so (crc32c_sw/hw,
+series, combine, combine_series, trim, dispatch pointers) against the
+reference's own outputs (ref_vectors.json) and the pinned oracle. CPU only:
+these are the synchronous per-buffer engines Photon callers keep for small
+host buffers (reference common/checksum/crc32c.h:20-92)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from photonlibos_amd import checksum as ck
+from photonlibos_amd import datagen
+
+ALPHA = (b"abcdefghijklmnopqrstuvwxyz" * 200)
+ENGINES = ["crc32c_sw", "crc32c_hw", "crc32c_hw_simple", "crc32c_hw_portable"]
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_golden_512(engine, golden_in):
+    f = getattr(ck, engine)
+    for k, want in enumerate(golden_in["crc32c"]):
+        assert f(ALPHA[: k + 1]) == want, k
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_alphabet_0_4096(engine, ref_vectors):
+    f = getattr(ck, engine)
+    for n, want in enumerate(ref_vectors["alphabet_crc32c"]):
+        assert f(ALPHA[:n]) == want, n
+
+
+@pytest.mark.parametrize("engine", ENGINES + ["auto"])
+def test_random_offsets_seeds(engine, ref_vectors):
+    rv = ref_vectors
+    for n, off, seed, st, want in zip(rv["rand_len"], rv["rand_off"], rv["rand_seed"], rv["rand_stream"],
+                                      rv["rand_crc32c"]):
+        buf = bytearray(n + 16)
+        buf[off:off + n] = datagen.stream_bytes(st, n).tobytes()
+        view = memoryview(buf)[off:off + n]
+        got = ck.crc32c_extend(view, seed) if engine == "auto" else getattr(ck, engine)(view, seed)
+        assert got == want, (engine, n, off, seed)
+
+
+def test_dispatch_is_hw_on_sse42_host():
+    assert ck.is_crc32c_hw_available()
+    assert ck.crc32c(b"123456789") == 0x58E3FA20
+    assert ck.crc32c("123456789") == 0x58E3FA20  # string_view overload (crc32c.h:43-45)
+
+
+@pytest.mark.parametrize("which", ["sw", "hw", "auto"])
+def test_combine(which, ref_vectors):
+    rv = ref_vectors
+    f = {"sw": ck.crc32c_combine_sw, "hw": ck.crc32c_combine_hw, "auto": ck.crc32c_combine}[which]
+    for c1, c2, l2, want in zip(rv["comb_crc1"], rv["comb_crc2"], rv["comb_len2"], rv["comb_sw"]):
+        assert f(c1, c2, l2) == want, (c1, c2, l2)
+
+
+def test_combine_property_like_reference():
+    # test_checksum.cpp:231-245 with a seeded buffer: combine(crc(A), crc(B), |B|) == crc(AB).
+    buf = datagen.stream_bytes(0xAB, 5100).tobytes()
+    x = ck.crc32c_sw(buf)
+    assert x == ck.crc32c_hw(buf)
+    rnd = random.Random(7)
+    for _ in range(2000):
+        l1 = rnd.randrange(len(buf) // 2)
+        c1, c2 = ck.crc32c_hw(buf[:l1]), ck.crc32c_hw(buf[l1:])
+        assert ck.crc32c_combine_hw(c1, c2, len(buf) - l1) == x
+        assert ck.crc32c_combine_sw(c1, c2, len(buf) - l1) == x
+
+
+def test_series_and_combine_series(ref_vectors):
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDA000, 1 << 20).tobytes()
+    pos = 0
+    for i, (ps, npart) in enumerate(zip(rv["series_part"], rv["series_n"])):
+        sw = rv["series_sw"][pos:pos + npart]
+        hw = rv["series_hw"][pos:pos + npart]
+        pos += npart
+        assert ck.crc32c_series_sw(buf, ps, npart) == sw
+        assert ck.crc32c_series_hw(buf, ps, npart) == hw   # incl. the part_size < 8 quirk
+        assert ck.crc32c_series(buf, ps, npart) == hw      # x86 dispatch picks _hw (crc.cpp:139-144)
+        for f in (ck.crc32c_combine_series_sw, ck.crc32c_combine_series_hw, ck.crc32c_combine_series):
+            assert f(sw, ps) == rv["cseries_sw"][i]
+    assert ck.crc32c_combine_series([], 4096) == 0
+
+
+@pytest.mark.parametrize("which", ["sw", "hw", "auto"])
+def test_trim(which, ref_vectors):
+    rv = ref_vectors
+    f = {"sw": ck.crc32c_trim_sw, "hw": ck.crc32c_trim_hw, "auto": ck.crc32c_trim}[which]
+    buf = datagen.stream_bytes(0x5EEDB000, 5100).tobytes()
+    x = rv["trim_all"][0]
+    for l1, l3, want in zip(rv["trim_l1"], rv["trim_l3"], rv["trim_sw"]):
+        c1 = ck.crc32c_sw(buf[:l1])
+        c3 = ck.crc32c_sw(buf[5100 - l3:]) if l3 else 0
+        assert f((x, 5100), (c1, l1), (c3, l3)) == want
+
+
+def test_trim_error_behaviour(capfd):
+    # crc.cpp:444-445: LOG_ERRNO_RETURN(EINVAL, 0, ...): logs, errno = EINVAL, returns 0.
+    fn = ctypes.CDLL(ck.lib()._name, use_errno=True)["_Z14crc32c_trim_hw16CRC32C_ComponentS_S_"]
+    fn.restype = ctypes.c_uint32
+    fn.argtypes = [ctypes.c_uint64] * 3
+    ctypes.set_errno(0)
+    r = fn(123 | (10 << 32), 1 | (6 << 32), 2 | (6 << 32))
+    assert r == 0 and ctypes.get_errno() == 22
+    assert "must be >" in capfd.readouterr().err
+
+
+def test_large_buffers_match_oracle(oracle):
+    for n in (12288, 12289, 3 * 4096 * 3 + 5, 1 << 20):
+        for off in (0, 3):
+            b = bytes(off) + datagen.stream_bytes(n + off, n).tobytes()
+            d = memoryview(b)[off:]
+            want = oracle.crc32c(d, 0x9876)
+            assert ck.crc32c_hw(d, 0x9876) == want
+            assert ck.crc32c_sw(d, 0x9876) == want
+
+
+def test_numpy_buffers():
+    a = np.frombuffer(datagen.stream_bytes(1, 4096).tobytes(), np.uint8)
+    assert ck.crc32c(a) == ck.crc32c_sw(a.tobytes())

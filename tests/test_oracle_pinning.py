@@ -1,0 +1,120 @@
+"""Pin the oracle (oracle/crc_oracle.c) before trusting it:
+  * against the reference's own golden data (common/checksum/test/checksum.in,
+    checksum.crc64 -> tests/golden/checksum_in.json), and
+  * against outputs of the reference's own crc.cpp/crc_tables.cpp, built
+    unmodified by oracle/ref/Makefile (tests/golden/ref_vectors.json).
+CPU only."""
+import numpy as np
+
+from photonlibos_amd import datagen
+
+ALPHA = (b"abcdefghijklmnopqrstuvwxyz" * 200)
+
+
+def test_checksum_in_crc32c(oracle, golden_in):
+    # test_checksum.cpp:50-63 / 117-119: every known answer, both oracle engines.
+    for k, want in enumerate(golden_in["crc32c"]):
+        s = ALPHA[: k + 1]
+        assert oracle.crc32c(s) == want, k
+        assert oracle.crc32c_bitwise(s) == want, k
+
+
+def test_checksum_in_crc64(oracle, golden_in):
+    for k, want in enumerate(golden_in["crc64ecma"]):
+        assert oracle.crc64ecma(ALPHA[: k + 1]) == want, k
+
+
+def test_shift_tables(oracle, ref_vectors):
+    # crc_tables.cpp:104-107 generators vs the reference's compiled tables.
+    assert [oracle.lshift_hw(i) for i in range(28)] == ref_vectors["lshift_table_hw"]
+    assert [oracle.rshift_hw(i) for i in range(32)] == ref_vectors["rshift_table_hw"]
+    assert [oracle.lshift_sw(i) for i in range(32)] == ref_vectors["lshift_table_sw"]
+    assert [oracle.rshift_sw(i) for i in range(32)] == ref_vectors["rshift_table_sw"]
+    # SURVEY.md §7 known shift-table answers.
+    assert ref_vectors["lshift_table_sw"][:6] == [0x00800000, 0x00008000, 0x82F63B78, 0x6EA2D55C, 0x18B8EA18,
+                                                  0x510AC59A]
+    assert ref_vectors["lshift_table_hw"][:4] == [0x493C7D27, 0xBA4FC28E, 0x9E4ADDF8, 0x0D3B6092]
+
+
+def test_alphabet_lengths(oracle, ref_vectors):
+    # test_checksum.cpp:70-84 differential pattern, lengths 0..4096.
+    for n, want in enumerate(ref_vectors["alphabet_crc32c"]):
+        assert oracle.crc32c(ALPHA[:n]) == want, n
+
+
+def test_random_buffers_with_seeds_and_offsets(oracle, ref_vectors):
+    rv = ref_vectors
+    for n, off, seed, st, want in zip(rv["rand_len"], rv["rand_off"], rv["rand_seed"], rv["rand_stream"],
+                                      rv["rand_crc32c"]):
+        data = datagen.stream_bytes(st, n)
+        # The oracle is alignment-agnostic; place the data at the same offset anyway.
+        buf = np.zeros(n + 16, np.uint8)
+        buf[off:off + n] = data
+        assert oracle.crc32c(buf[off:off + n], seed) == want, (n, off, seed)
+        # crc32c_extend(d, n, s) == combine(s, crc32c(d, n), n)  
+        assert oracle.combine(seed, oracle.crc32c(data), n) == want
+
+
+def test_combine(oracle, ref_vectors):
+    rv = ref_vectors
+    for c1, c2, l2, sw, hw in zip(rv["comb_crc1"], rv["comb_crc2"], rv["comb_len2"], rv["comb_sw"], rv["comb_hw"]):
+        assert sw == hw
+        assert oracle.combine(c1, c2, l2) == sw, (c1, c2, l2)
+
+
+def test_series_and_combine_series(oracle, ref_vectors):
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDA000, 1 << 20)
+    pos = 0
+    for i, (ps, npart) in enumerate(zip(rv["series_part"], rv["series_n"])):
+        sw = rv["series_sw"][pos:pos + npart]
+        hw = rv["series_hw"][pos:pos + npart]
+        pos += npart
+        assert oracle.series(buf, ps, npart) == sw
+        assert oracle.series(buf, ps, npart, hw_quirk=True) == hw
+        if ps < 8:
+            assert hw == [0] * npart  # the crc32c_series_hw quirk (crc.cpp:481-500)
+        assert oracle.combine_series(sw, ps) == rv["cseries_sw"][i] == rv["cseries_hw"][i]
+        assert rv["cseries_sw"][i] == oracle.crc32c(buf[: ps * npart])
+
+
+def test_trim(oracle, ref_vectors):
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDB000, 5100)
+    x = rv["trim_all"][0]
+    assert oracle.crc32c(buf) == x
+    for l1, l3, sw, hw in zip(rv["trim_l1"], rv["trim_l3"], rv["trim_sw"], rv["trim_hw"]):
+        c1 = oracle.crc32c(buf[:l1])
+        c3 = oracle.crc32c(buf[5100 - l3:]) if l3 else 0
+        got = oracle.trim((x, 5100), (c1, l1), (c3, l3))
+        assert got == sw == hw
+        assert got == oracle.crc32c(buf[l1:5100 - l3])
+
+
+def test_trim_error_path(oracle):
+    # crc.cpp:444-445: inconsistent sizes -> errno = EINVAL, return 0.
+    assert oracle.trim((123, 10), (1, 6), (2, 6)) == 0
+    assert oracle.errno() == 22
+
+
+def test_known_answers(oracle, ref_vectors):
+    ka = ref_vectors["known_answers"]
+    assert ka == [0x58E3FA20, 0x269ABBE0, 0]
+    assert oracle.crc32c(b"123456789") == 0x58E3FA20
+    assert (~oracle.crc32c(b"123456789", 0xFFFFFFFF)) & 0xFFFFFFFF == 0xE3069283  # iSCSI check value
+    assert oracle.crc32c(b"\xff" * 65536) == 0x269ABBE0
+    assert oracle.crc32c(bytes(4096)) == 0
+    assert oracle.crc32c(b"") == 0
+    assert oracle.crc32c(b"a") == 0x93AD1061
+
+
+def test_crc64(oracle, ref_vectors):
+    for n, want, st in zip(ref_vectors["crc64_len"], ref_vectors["crc64_sw"], range(0x5EED6401, 0x5EED6401 + 99)):
+        assert oracle.crc64ecma(datagen.stream_bytes(st, n)) == want, n
+
+
+def test_gf2_identities(oracle):
+    # pow/ipow inverse, x^8, x^16, x^32.
+    assert oracle.pow32(8) == 0x00800000 and oracle.pow32(16) == 0x00008000 and oracle.pow32(32) == 0x82F63B78
+    for n in (1, 7, 33, 1000, 123456789):
+        assert oracle.clmul_modp32(oracle.pow32(n), oracle.ipow32(n)) == 0x80000000
