@@ -87,12 +87,25 @@ int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64
  * lanes per buffer G in {4,8,16,32,64}; 0 = automatic (default). */
 int photon_crc_set_lanes_per_buffer(int g);
 
+/* Streaming-kernel shape for uniform batches (testing / tuning): rows per
+ * step and steps in flight, one of (4,2) (4,3) (4,4) (2,4) (8,2); default
+ * (4,3). rows_per_step = 0 disables the streaming kernel (generic kernel for
+ * every batch). */
+int photon_crc_set_stream_config(int rows_per_step, int steps_in_flight);
+
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
  * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),
  * little-endian; identical to photonlibos_amd.datagen. */
 int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                   uint64_t seed_base, void* stream);
+
+/* Bench utility (not on the checksum path): read nbytes (16-byte aligned
+ * base) once with the CRC kernels' load instructions and fold them into
+ * d_sink (>= 256 words; grid = min(8*CUs, sink_words/256) blocks of 256):
+ * the achievable HBM-read rate the roofline is compared against. */
+int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
+                                void* stream);
 
 #ifdef __cplusplus
 }

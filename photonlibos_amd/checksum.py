@@ -25,7 +25,7 @@ __all__ = [
     "crc32c_combine_series", "crc32c_combine_series_sw", "crc32c_combine_series_hw",
     "crc32c_trim", "crc32c_trim_sw", "crc32c_trim_hw", "is_crc32c_hw_available",
     "device_count", "set_lanes_per_buffer", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
-    "combine_batch", "fill_splitmix", "IOVEC_DTYPE",
+    "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
 _CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
@@ -233,6 +233,16 @@ def combine_batch(crc1, crc2, len2, count, out, stream=None):
     """out[i] = crc32c_combine(crc1[i], crc2[i], len2[i]). Async."""
     _check(lib().photon_crc32c_combine_batch(_ptr(crc1), _ptr(crc2), _ptr(len2), count, _ptr(out),
                                              _stream(stream)))
+
+
+def set_stream_config(rows_per_step, steps_in_flight):
+    """Streaming-kernel shape for uniform batches; (0, 0) disables it."""
+    _check(lib().photon_crc_set_stream_config(rows_per_step, steps_in_flight))
+
+
+def read_stream(base, nbytes, sink, sink_words, stream=None):
+    """Bench utility: HBM read-only stream over nbytes (achievable-roofline probe)."""
+    _check(lib().photon_crc_util_read_stream(_ptr(base), nbytes, _ptr(sink), sink_words, _stream(stream)))
 
 
 def fill_splitmix(base, stride, nbytes, count, seed_base, stream=None):

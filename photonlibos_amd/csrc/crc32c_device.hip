@@ -9,21 +9,25 @@
 // buffer; G < 64 packs 64/G small buffers per wavefront) walks the buffer in
 // rows of G 16-byte blocks: lane l of the group loads block (row*G + l) with
 // one coalesced global_load_dwordx4, so a row is one contiguous 16*G-byte
-// sweep. Each lane keeps a partial CRC over "its" blocks as if the other
-// lanes' bytes were zeros, so between two of its blocks it must skip
-// gap = 16*(G-1) zero bytes: P <- P * x^(8*gap) mod P, folded into the first
-// word's table step. All GF(2) products by constants are byte-sliced LDS
-// table lookups (no carry-less multiply on CDNA4, no MFMA: this is GF(2)):
+// sweep. Each lane keeps a partial CRC P over "its" column of blocks, as if
+// the other lanes' bytes were zeros:
+//     P <- P * x^(8*16*G) mod P  XOR  crc16(block)
+// crc16(block) (the CRC of the 16 bytes alone) does not depend on P, so the
+// U blocks a lane holds are reduced in parallel and only the cheap shift is
+// on the loop-carried chain. All GF(2) products by constants are byte-sliced
+// LDS table lookups (no carry-less multiply on CDNA4, no MFMA: this is GF(2)):
 //   D tables: x -> x * x^32 mod P, 4 byte slices, replicated 32x so that lane
 //             l always hits bank l%32 (conflict-free random lookups), 128 KiB;
-//   S tables: P -> P * x^(8*gap+32) mod P, 4 slices, 4 replicas, 16 KiB.
+//   S tables: P -> P * x^(8*16*G) mod P, 4 slices, 4 replicas, 16 KiB.
 // At the end lane l multiplies its partial by x^(128*d_l), d_l = number of
-// 16-byte blocks between its last block and the end (6 constant-basis GF(2)
-// multiplies, bits of d_l), and the group XOR-reduces with __shfl_xor.
+// 16-byte blocks between its last block and the end (constant-basis GF(2)
+// multiplies on the bits of d_l), and the group XOR-reduces with __shfl_xor.
 // Unaligned heads use zero-prefix invariance (crc.md:24-32): the leading
 // bytes of the first aligned block are masked to 0 and the seed is XORed into
 // the first four data bytes (init-value linearity), so every load is an
 // aligned 16-byte load. Ragged tails (<16 B) are finished byte-serially.
+// Uniform batches (aligned, equal length, whole rows) take a streaming kernel
+// whose load ring runs continuously across buffer boundaries.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -44,14 +48,22 @@ namespace pcrc {
 constexpr uint32_t kDataBytes = 2u * 65536u;   // 4 slices x 256 idx x 32 replicas x 4 B
 constexpr uint32_t kShiftBase = kDataBytes;    // S tables follow
 constexpr uint32_t kShiftBytes = 4u * 4096u;   // 4 slices x 256 idx x 4 replicas x 4 B
-constexpr uint32_t kLdsBytes = kShiftBase + kShiftBytes;  // 147456 B of the 160 KiB
+constexpr uint32_t kBasisBase = kShiftBase + kShiftBytes;  // lane-combine constants
+constexpr uint32_t kBasisBytes = 6u * 32u * 4u;
+constexpr uint32_t kLdsBytes = kBasisBase + kBasisBytes;   // 148224 B of the 160 KiB
 constexpr int kBlock = 1024;                   // 16 waves, one workgroup per CU
 constexpr int kWaves = kBlock / 64;
 
 // Kernel constants computed on the host (gf2.h) per lanes-per-buffer G.
 struct LaneConsts {
-    uint32_t kshift;           // x^(8*16*(G-1) + 32) mod P
+    uint32_t kshift;           // x^(8*16*G) mod P: one row of the lane's column
     uint32_t basis[6][32];     // basis of x^(128 * 2^k) mod P, k = 0..5
+};
+
+// Seed application for uniform-length batches: crc32c_extend(d, n, s) =
+// crc32c(d, n) XOR s * x^(8n) (combine identity).
+struct SeedConsts {
+    uint32_t basis[32];        // basis of x^(8 * nbytes) mod P
 };
 
 struct BatchArgs {
@@ -100,12 +112,29 @@ __device__ __forceinline__ uint32_t bytestep(const uint32_t* lds, uint32_t c, ui
     return lds_word(lds, ((x << 8) & 0xff00u) | a.d3) ^ (c >> 8);
 }
 
-// One 16-byte block of this lane's stream, `gap` zero bytes after the previous one.
-__device__ __forceinline__ uint32_t block_step(const uint32_t* lds, uint32_t p, uint4 w, const LaneAddr& a) {
-    uint32_t c = sstep(lds, p, a.s) ^ dstep(lds, w.x, a);
+// CRC (init 0, no xorout) of one 16-byte block: four chained word steps.
+__device__ __forceinline__ uint32_t crc16(const uint32_t* lds, uint4 w, const LaneAddr& a) {
+    uint32_t c = dstep(lds, w.x, a);
     c = dstep(lds, c ^ w.y, a);
     c = dstep(lds, c ^ w.z, a);
     return dstep(lds, c ^ w.w, a);
+}
+
+// U blocks of one lane's column: the crc16s are independent (ILP), only the
+// row shift is carried.
+template <int U>
+__device__ __forceinline__ uint32_t column_step(const uint32_t* lds, uint32_t p, const uint4 (&w)[U],
+                                                const LaneAddr& a) {
+    uint32_t c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = crc16(lds, w[u], a);
+#pragma unroll
+    for (int u = 0; u < U; ++u) p = sstep(lds, p, a.s) ^ c[u];
+    return p;
+}
+
+__device__ __forceinline__ uint32_t column_step1(const uint32_t* lds, uint32_t p, uint4 w, const LaneAddr& a) {
+    return sstep(lds, p, a.s) ^ crc16(lds, w, a);
 }
 
 // Word at byte offset `off` (relative to the aligned start A0) of the first
@@ -142,40 +171,82 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p) {
 
 __device__ __forceinline__ uint8_t load8(const uint8_t* p) { return *(g_u8*)p; }
 
-template <int G>
-__global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-
-    // ---- build the tables (every workgroup; 1024 threads = 1024 entries)
-    {
-        const uint32_t tid = threadIdx.x;
-        const uint32_t t = tid >> 8, b = tid & 255u;
-        const uint32_t v = b << (8 * t);
-        const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
-        const uint32_t dbase = (((t >> 1) << 16) + (b << 8) + ((t & 1) << 7)) >> 2;
+// Build the D and S tables in LDS (every workgroup; 1024 threads = one entry of
+// each table per thread).
+__device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc) {
+    const uint32_t kshift = kc.kshift;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 6 * 32) lds[kBasisBase / 4 + tid] = kc.basis[tid >> 5][tid & 31];
+    const uint32_t t = tid >> 8, b = tid & 255u;
+    const uint32_t v = b << (8 * t);
+    const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
+    const uint32_t dbase = (((t >> 1) << 16) + (b << 8) + ((t & 1) << 7)) >> 2;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) lds[dbase + r] = dv;
-        const uint32_t sv = mulmod(v, kc.kshift);
-        const uint32_t sbase = (kShiftBase + t * 4096u + b * 16u) >> 2;
+    for (int r = 0; r < 32; ++r) lds[dbase + r] = dv;
+    const uint32_t sv = mulmod(v, kshift);
+    const uint32_t sbase = (kShiftBase + t * 4096u + b * 16u) >> 2;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) lds[sbase + r] = sv;
-    }
+    for (int r = 0; r < 4; ++r) lds[sbase + r] = sv;
     __syncthreads();
+}
 
-    constexpr int GPW = 64 / G;  // buffers per wavefront
-    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
-    constexpr int U = 4;         // rows in flight per lane
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t gl = lane & (G - 1);
-    const uint32_t grp = lane / G;
-
+__device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
     LaneAddr la;
     la.d0 = ((lane & 31u) << 2);
     la.d1 = (1u << 7) | ((lane & 31u) << 2);
     la.d2 = (1u << 16) | ((lane & 31u) << 2);
     la.d3 = (1u << 16) | (1u << 7) | ((lane & 31u) << 2);
     la.s = kShiftBase + ((lane & 3u) << 2);
+    return la;
+}
+
+// Shift lane partials to the end of the body (d blocks of 16 bytes) and
+// XOR-reduce over the G lanes of the group.
+// p * K with K's basis (32 words) in LDS, read 4 words at a time (broadcast).
+__device__ __forceinline__ uint32_t mul_basis_lds(uint32_t p, const uint32_t* basis) {
+    uint32_t r = 0;
+#pragma unroll 2
+    for (int q = 0; q < 8; ++q) {
+        const uint4 b = reinterpret_cast<const uint4*>(basis)[q];
+        r ^= (0u - ((p >> (4 * q)) & 1u)) & b.x;
+        r ^= (0u - ((p >> (4 * q + 1)) & 1u)) & b.y;
+        r ^= (0u - ((p >> (4 * q + 2)) & 1u)) & b.z;
+        r ^= (0u - ((p >> (4 * q + 3)) & 1u)) & b.w;
+    }
+    return r;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_reduce(uint32_t pc, uint32_t d, const uint32_t* lds) {
+    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
+    // basis[k][i] of x^(128*2^k), staged in LDS by build_tables.
+    const uint32_t* basis = lds + kBasisBase / 4;
+#pragma unroll 1
+    for (int k = 0; k < LOG2G; ++k)
+        if ((d >> k) & 1u) pc = mul_basis_lds(pc, basis + 32 * k);
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
+    return pc;
+}
+
+__device__ __forceinline__ uint32_t wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+// -------------------------------------------------------------- generic path
+// Any pointer, any length, any seed; one group of G lanes per buffer.
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    build_tables(lds, kc);
+
+    constexpr int GPW = 64 / G;  // buffers per wavefront
+    constexpr int U = 4;         // blocks per lane per step
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = wave_id();
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const LaneAddr la = lane_addr(lane);
 
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.count; wv += nwaves) {
@@ -223,9 +294,9 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                     w.z = head_word(w.z, off + 8, s0, seed);
                     w.w = head_word(w.w, off + 12, s0, seed);
                 }
-                pc = block_step(lds, 0u, w, la);
+                pc = crc16(lds, w, la);
             }
-            // Full rows 1..full-1: branch-free, U rows in flight while U are processed.
+            // Full rows 1..full-1: U rows per step, the next U in flight.
             uint64_t row = 1;
             if (row + U <= full) {
                 uint4 cur[U];
@@ -235,33 +306,125 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                     uint4 nxt[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-#pragma unroll
-                    for (int u = 0; u < U; ++u) pc = block_step(lds, pc, cur[u], la);
+                    pc = column_step<U>(lds, pc, cur, la);
 #pragma unroll
                     for (int u = 0; u < U; ++u) cur[u] = nxt[u];
                 }
-#pragma unroll
-                for (int u = 0; u < U; ++u) pc = block_step(lds, pc, cur[u], la);
+                pc = column_step<U>(lds, pc, cur, la);
                 row += U;
             }
-            for (; row < full; ++row) pc = block_step(lds, pc, load16(lp + row * (16 * G)), la);
+            for (; row < full; ++row) pc = column_step1(lds, pc, load16(lp + row * (16 * G)), la);
             // Partial last row.
-            if (full >= 1 && full < rows && full * G + gl < nb) pc = block_step(lds, pc, load16(lp + full * (16 * G)), la);
+            if (full >= 1 && full < rows && full * G + gl < nb)
+                pc = column_step1(lds, pc, load16(lp + full * (16 * G)), la);
 
-            // Shift each partial to the end of the body: d = (rlast-1-gl) mod G blocks.
-            const uint32_t d = (rlast + G - 1 - gl) & (G - 1);
-#pragma unroll
-            for (int k = 0; k < LOG2G; ++k)
-                if ((d >> k) & 1u) pc = mul_basis_dev(pc, kc.basis[k]);
-#pragma unroll
-            for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
-            crc = pc;
+            crc = group_reduce<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds);
             // Ragged tail (< 16 bytes) after the last aligned block.
             if (gl == 0)
                 for (const uint8_t* q = eb; q < e; ++q) crc = bytestep(lds, crc, load8(q), la);
         }
         if (active && gl == 0) args.out[bi] = crc;
     }
+}
+
+// ------------------------------------------------------------ streaming path
+// Uniform batches: base and stride 16-byte aligned, nbytes = R*16*G with
+// R % U == 0. Each wave walks the rows of its buffers (slots j = 0,1,...:
+// buffer tuple wv0 + j*nwaves) as ONE stream of steps of U rows, with a ring
+// of D steps of loads in flight that never drains at buffer boundaries.
+struct UniformArgs {
+    const uint8_t* base;
+    uint64_t stride;
+    uint64_t rows;       // R = nbytes / (16*G)
+    uint64_t count;
+    uint32_t* out;          // crc32c with seed 0; seeds are folded in by crc32c_seed_kernel
+};
+
+template <int G, int U, int D>
+__global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args, LaneConsts kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    build_tables(lds, kc);
+
+    constexpr uint64_t GPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const LaneAddr la = lane_addr(lane);
+
+    const uint64_t ngroups = (args.count + GPW - 1) / GPW;
+    const uint64_t wv0 = (uint64_t)blockIdx.x * kWaves + wave_id();
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    if (wv0 >= ngroups) return;
+    const uint64_t nslots = (ngroups - 1 - wv0) / nwaves + 1;
+    const uint64_t spb = args.rows / U;               // steps per buffer
+    const uint64_t nsteps = nslots * spb;
+    const uint64_t row_bytes = 16ull * G;
+    const uint64_t step_bytes = row_bytes * U;
+
+    auto buffer_of = [&](uint64_t slot) -> uint64_t {
+        const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
+        return bi < args.count ? bi : args.count - 1;  // idle lanes of a last partial tuple
+    };
+    auto slot_base = [&](uint64_t slot) -> const uint8_t* {
+        if (slot >= nslots) slot = nslots - 1;           // padding steps re-read valid rows
+        return args.base + buffer_of(slot) * args.stride + 16ull * gl;
+    };
+
+    // Load cursor (slot, step-in-buffer, pointer).
+    uint64_t lslot = 0, lstep = 0;
+    const uint8_t* lptr = slot_base(0);
+    auto advance = [&]() {
+        if (++lstep == spb) {
+            lstep = 0;
+            ++lslot;
+            lptr = slot_base(lslot);
+        } else if (lslot < nslots) {
+            lptr += step_bytes;
+        }
+    };
+
+    // D steps in flight; D+1 register sets so that a refill never targets a
+    // set that is still being read (no register copies across the loop edge,
+    // which would force a vmcnt(0) drain).
+    constexpr int S = D + 1;
+    uint4 ring[S][U];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) ring[d][u] = load16(lptr + u * row_bytes);
+        advance();
+    }
+    const uint64_t padded = (nsteps + S - 1) / S * S;
+
+    uint64_t slot = 0, step = 0;
+    uint32_t pc = 0;
+    for (uint64_t s = 0; s < padded; s += S) {
+#pragma unroll
+        for (int d = 0; d < S; ++d) {
+            const int refill = (d + D) % S;  // the set read by the previous stage
+#pragma unroll
+            for (int u = 0; u < U; ++u) ring[refill][u] = load16(lptr + u * row_bytes);
+            advance();
+            pc = column_step<U>(lds, pc, ring[d], la);
+            if (++step == spb) {
+                // End of this buffer: lane gl's last block is G-1-gl blocks from the end.
+                const uint32_t crc = group_reduce<G>(pc, (uint32_t)(G - 1 - gl), lds);
+                const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
+                if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = crc;
+                pc = 0;
+                step = 0;
+                ++slot;
+            }
+        }
+    }
+}
+
+// out[i] ^= seed_i * x^(8*nbytes): crc32c_extend(d, n, s) = crc32c(d, n) ^ s*x^(8n).
+__global__ void crc32c_seed_kernel(uint32_t* out, uint64_t count, const uint32_t* seeds, uint32_t seed0,
+                                   SeedConsts sc) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    out[i] ^= mul_basis_dev(seeds ? seeds[i] : seed0, sc.basis);
 }
 
 // Per-message fold of per-segment CRCs: acc = seed; acc = acc*x^(8 len)+crc.
@@ -320,11 +483,35 @@ __global__ void fill_splitmix_kernel(uint8_t* base, uint64_t stride, uint64_t nb
     }
 }
 
+// Read-only HBM stream (bench reference for the achievable read roofline):
+// every 16-byte word read once with the same nontemporal dwordx4 loads as the
+// CRC kernels, XOR-folded so nothing is dead code.
+__global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint64_t nvec, uint32_t* sink) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = tid;
+    for (; i + 7 * nth < nvec; i += 8 * nth) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = load16(p + 16 * (i + k * nth));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < nvec; i += nth) {
+        const uint4 v = load16(p + 16 * i);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    sink[tid] = acc;
+}
+
 // ------------------------------------------------------------------ host side
 namespace {
 
 thread_local std::string g_err;
 int g_lanes_override = 0;
+int g_stream_u = 4, g_stream_d = 3;   // streaming kernel: rows per step, steps in flight
+bool g_stream_enabled = true;
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -368,7 +555,7 @@ int current_device(int* cus) {
 
 LaneConsts make_lane_consts(int g) {
     LaneConsts c;
-    c.kshift = xpow(8ull * 16ull * (uint64_t)(g - 1) + 32ull);
+    c.kshift = xpow(8ull * 16ull * (uint64_t)g);
     for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), c.basis[k]);
     return c;
 }
@@ -430,6 +617,75 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
     return 0;
 }
 
+SeedConsts seed_consts(uint64_t nbytes) {
+    static std::mutex mu;
+    static uint64_t cached_n = ~0ull;
+    static SeedConsts cached;
+    std::lock_guard<std::mutex> lk(mu);
+    if (cached_n != nbytes) {
+        mul_basis(xpow(8ull * nbytes), cached.basis);
+        cached_n = nbytes;
+    }
+    return cached;
+}
+
+template <int G, int U, int D>
+void launch_uniform_t(const UniformArgs& a, dim3 grid, hipStream_t stream) {
+    hipLaunchKernelGGL((crc32c_uniform_kernel<G, U, D>), grid, dim3(kBlock), 0, stream, a, lane_consts(G));
+}
+
+template <int G>
+bool launch_uniform_g(const UniformArgs& a, dim3 grid, hipStream_t stream) {
+    const int u = g_stream_u, d = g_stream_d;
+    if (u == 4 && d == 3) launch_uniform_t<G, 4, 3>(a, grid, stream);
+    else if (u == 4 && d == 2) launch_uniform_t<G, 4, 2>(a, grid, stream);
+    else if (u == 2 && d == 4) launch_uniform_t<G, 2, 4>(a, grid, stream);
+    else if (u == 8 && d == 2) launch_uniform_t<G, 8, 2>(a, grid, stream);
+    else if (u == 4 && d == 4) launch_uniform_t<G, 4, 4>(a, grid, stream);
+    else return false;
+    return true;
+}
+
+// Streaming kernel when the batch is uniform: aligned base/stride, equal
+// length made of whole rows, row count a multiple of the step. Returns 1 if
+// it does not apply (caller falls back to the generic kernel), else 0 / error.
+int try_launch_uniform(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint32_t seed0,
+                       const uint32_t* seeds, uint32_t* out, hipStream_t stream) {
+    if (!g_stream_enabled || count == 0) return 1;
+    const int g = choose_lanes(nbytes);
+    const uint64_t row = 16ull * g;
+    if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
+    const uint64_t rows = nbytes / row;
+    if (rows % (uint64_t)g_stream_u) return 1;
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const uint64_t gpw = 64 / g;
+    const uint64_t waves = (count + gpw - 1) / gpw;
+    uint64_t grid = (waves + kWaves - 1) / kWaves;
+    if (grid > (uint64_t)cus) grid = cus;
+    UniformArgs a{base, stride, rows, count, out};
+    bool ok = false;
+    switch (g) {
+        case 64: ok = launch_uniform_g<64>(a, dim3(grid), stream); break;
+        case 32: ok = launch_uniform_g<32>(a, dim3(grid), stream); break;
+        case 16: ok = launch_uniform_g<16>(a, dim3(grid), stream); break;
+        case 8: ok = launch_uniform_g<8>(a, dim3(grid), stream); break;
+        default: ok = launch_uniform_g<4>(a, dim3(grid), stream); break;
+    }
+    if (!ok) return fail(-EINVAL, "unsupported streaming configuration");
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "crc32c_uniform_kernel launch");
+    if (seeds || seed0) {
+        const int bs = 256;
+        hipLaunchKernelGGL(crc32c_seed_kernel, dim3((count + bs - 1) / bs), dim3(bs), 0, stream, out, count, seeds,
+                           seed0, seed_consts(nbytes));
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "crc32c_seed_kernel launch");
+    }
+    return 0;
+}
+
 }  // namespace
 }  // namespace pcrc
 
@@ -459,9 +715,26 @@ int photon_crc_set_lanes_per_buffer(int g) {
     return 0;
 }
 
+int photon_crc_set_stream_config(int rows_per_step, int steps_in_flight) {
+    if (rows_per_step == 0) {
+        g_stream_enabled = false;
+        return 0;
+    }
+    const int u = rows_per_step, d = steps_in_flight;
+    if (!((u == 4 && (d == 2 || d == 3 || d == 4)) || (u == 2 && d == 4) || (u == 8 && d == 2)))
+        return fail(-EINVAL, "unsupported (rows_per_step, steps_in_flight)");
+    g_stream_enabled = true;
+    g_stream_u = u;
+    g_stream_d = d;
+    return 0;
+}
+
 int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                 uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
     if (count && (!d_out || (!d_base && nbytes))) return fail(-EINVAL, "null buffer or output");
+    int rc = try_launch_uniform(static_cast<const uint8_t*>(d_base), stride, nbytes, count, seed0, d_seeds, d_out,
+                                static_cast<hipStream_t>(stream));
+    if (rc <= 0) return rc;
     BatchArgs a{};
     a.base = static_cast<const uint8_t*>(d_base);
     a.stride = stride;
@@ -535,6 +808,22 @@ int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, 
                        static_cast<hipStream_t>(stream), d_crc1, d_crc2, d_len2, count, d_out, pow_table());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "crc32c_combine_kernel launch");
+    return 0;
+}
+
+int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
+                                void* stream) {
+    if (!d_base || !d_sink || (reinterpret_cast<uintptr_t>(d_base) & 15)) return fail(-EINVAL, "bad arguments");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    uint64_t grid = (uint64_t)cus * 8;
+    if (grid * 256 > sink_words) grid = sink_words / 256;
+    if (!grid) return fail(-EINVAL, "sink too small (need >= 256 words)");
+    hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t*>(d_base), nbytes / 16, d_sink);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "read_stream_kernel launch");
     return 0;
 }
 
