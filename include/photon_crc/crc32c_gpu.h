@@ -87,11 +87,11 @@ int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64
  * lanes per buffer G in {4,8,16,32,64}; 0 = automatic (default). */
 int photon_crc_set_lanes_per_buffer(int g);
 
-/* Streaming-kernel shape for uniform batches (testing / tuning): rows per
- * step and steps in flight, one of (4,2) (4,3) (4,4) (2,4) (8,2); default
- * (4,3). rows_per_step = 0 disables the streaming kernel (generic kernel for
- * every batch). */
-int photon_crc_set_stream_config(int rows_per_step, int steps_in_flight);
+/* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
+ * lane run B, rows per step U and steps in flight D, one of (1,4,3) (default),
+ * (2,2,3), (2,2,4), (1,2,4), (4,1,3), (4,1,4). run_blocks = 0 disables the
+ * streaming kernel (generic kernel for every batch). */
+int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
 
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed

@@ -235,9 +235,9 @@ def combine_batch(crc1, crc2, len2, count, out, stream=None):
                                              _stream(stream)))
 
 
-def set_stream_config(rows_per_step, steps_in_flight):
-    """Streaming-kernel shape for uniform batches; (0, 0) disables it."""
-    _check(lib().photon_crc_set_stream_config(rows_per_step, steps_in_flight))
+def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
+    """Streaming-kernel shape (B, U, D) for uniform batches; B = 0 disables it."""
+    _check(lib().photon_crc_set_stream_config(run_blocks, rows_per_step, steps_in_flight))
 
 
 def read_stream(base, nbytes, sink, sink_words, stream=None):

@@ -88,11 +88,19 @@ struct LaneAddr {
 };
 
 // x * x^32 mod P = CRC register after absorbing the 32-bit word x.
+// Address of slice t for byte t of x in ONE v_perm_b32: result bytes are
+// {d.byte0, x.byte t, d.byte2, 0} (selector 0..3 = second operand's bytes,
+// 4..7 = first operand's bytes, 12 = 0x00).
+template <int T>
+__device__ __forceinline__ uint32_t daddr(uint32_t x, uint32_t d) {
+    return __builtin_amdgcn_perm(x, d, 0x0C020000u | ((4u + T) << 8));
+}
+
 __device__ __forceinline__ uint32_t dstep(const uint32_t* lds, uint32_t x, const LaneAddr& a) {
-    const uint32_t t0 = lds_word(lds, ((x << 8) & 0xff00u) | a.d0);
-    const uint32_t t1 = lds_word(lds, (x & 0xff00u) | a.d1);
-    const uint32_t t2 = lds_word(lds, ((x >> 8) & 0xff00u) | a.d2);
-    const uint32_t t3 = lds_word(lds, ((x >> 16) & 0xff00u) | a.d3);
+    const uint32_t t0 = lds_word(lds, daddr<0>(x, a.d0));
+    const uint32_t t1 = lds_word(lds, daddr<1>(x, a.d1));
+    const uint32_t t2 = lds_word(lds, daddr<2>(x, a.d2));
+    const uint32_t t3 = lds_word(lds, daddr<3>(x, a.d3));
     return t0 ^ t1 ^ t2 ^ t3;
 }
 
@@ -109,7 +117,7 @@ __device__ __forceinline__ uint32_t sstep(const uint32_t* lds, uint32_t p, uint3
 // classic byte table).
 __device__ __forceinline__ uint32_t bytestep(const uint32_t* lds, uint32_t c, uint8_t b, const LaneAddr& a) {
     const uint32_t x = c ^ b;
-    return lds_word(lds, ((x << 8) & 0xff00u) | a.d3) ^ (c >> 8);
+    return lds_word(lds, daddr<0>(x, a.d3)) ^ (c >> 8);
 }
 
 // CRC (init 0, no xorout) of one 16-byte block: four chained word steps.
@@ -328,19 +336,75 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
 }
 
 // ------------------------------------------------------------ streaming path
-// Uniform batches: base and stride 16-byte aligned, nbytes = R*16*G with
-// R % U == 0. Each wave walks the rows of its buffers (slots j = 0,1,...:
-// buffer tuple wv0 + j*nwaves) as ONE stream of steps of U rows, with a ring
-// of D steps of loads in flight that never drains at buffer boundaries.
+// Uniform batches: base and stride 16-byte aligned, nbytes = R*16*B*G with
+// R % U == 0. A row is B*G consecutive 16-byte blocks; load b of a row is the
+// coalesced sweep of blocks [b*G, (b+1)*G). A DPP butterfly inside groups of
+// B lanes then gives every lane a RUN of B consecutive blocks, so the
+// loop-carried row shift (4 S-table lookups) is paid once per 16*B bytes.
+// Each wave walks the rows of its buffers (slots j = 0,1,...: buffer tuple
+// wv0 + j*nwaves) as ONE stream of steps of U rows, with a ring of D steps of
+// loads in flight that never drains at buffer boundaries.
 struct UniformArgs {
     const uint8_t* base;
     uint64_t stride;
-    uint64_t rows;       // R = nbytes / (16*G)
+    uint64_t rows;       // R = nbytes / (16*B*G)
     uint64_t count;
-    uint32_t* out;          // crc32c with seed 0; seeds are folded in by crc32c_seed_kernel
+    uint32_t* out;       // crc32c with seed 0; seeds are folded in by crc32c_seed_kernel
 };
 
-template <int G, int U, int D>
+// Exchange with lane (lane ^ BIT) (BIT = 1 or 2: DPP quad permutations).
+template <int BIT>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+    constexpr int ctrl = BIT == 1 ? 0xB1 : 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, false);
+}
+
+template <int BIT>
+__device__ __forceinline__ void bfly_word(uint32_t& lo_reg, uint32_t& hi_reg, bool hi) {
+    const uint32_t send = hi ? lo_reg : hi_reg;
+    const uint32_t recv = lane_xor<BIT>(send);
+    lo_reg = hi ? recv : lo_reg;
+    hi_reg = hi ? hi_reg : recv;
+}
+
+template <int BIT>
+__device__ __forceinline__ void bfly(uint4& lo, uint4& hi_blk, bool hi) {
+    bfly_word<BIT>(lo.x, hi_blk.x, hi);
+    bfly_word<BIT>(lo.y, hi_blk.y, hi);
+    bfly_word<BIT>(lo.z, hi_blk.z, hi);
+    bfly_word<BIT>(lo.w, hi_blk.w, hi);
+}
+
+// Transpose r[b] (lane t of a B-group holds block t + b*G) into the run
+// r[b] = block (t*G + b) of the group's first block: butterfly over the bits of B.
+template <int B>
+__device__ __forceinline__ void to_runs(uint4 (&r)[B], uint32_t t) {
+    if constexpr (B >= 2) {
+#pragma unroll
+        for (int m = 0; m < B; m += 2) bfly<1>(r[m], r[m + 1], (t & 1u) != 0);
+    }
+    if constexpr (B >= 4) {
+#pragma unroll
+        for (int m = 0; m < B; ++m)
+            if ((m & 2) == 0) bfly<2>(r[m], r[m + 2], (t & 2u) != 0);
+    }
+}
+
+// CRC (init 0) of a run of B blocks.
+template <int B>
+__device__ __forceinline__ uint32_t run_crc(const uint32_t* lds, const uint4 (&r)[B], const LaneAddr& a) {
+    uint32_t c = crc16(lds, r[0], a);
+#pragma unroll
+    for (int b = 1; b < B; ++b) {
+        c = dstep(lds, c ^ r[b].x, a);
+        c = dstep(lds, c ^ r[b].y, a);
+        c = dstep(lds, c ^ r[b].z, a);
+        c = dstep(lds, c ^ r[b].w, a);
+    }
+    return c;
+}
+
+template <int G, int B, int U, int D>
 __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args, LaneConsts kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     build_tables(lds, kc);
@@ -349,6 +413,8 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp = lane / G;
+    const uint32_t tb = gl & (B - 1);                    // position in the B-group
+    const uint32_t run = tb * (G / B) + gl / B;          // this lane's run index within a row
     const LaneAddr la = lane_addr(lane);
 
     const uint64_t ngroups = (args.count + GPW - 1) / GPW;
@@ -358,8 +424,8 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
     const uint64_t nslots = (ngroups - 1 - wv0) / nwaves + 1;
     const uint64_t spb = args.rows / U;               // steps per buffer
     const uint64_t nsteps = nslots * spb;
-    const uint64_t row_bytes = 16ull * G;
-    const uint64_t step_bytes = row_bytes * U;
+    constexpr uint64_t kSweep = 16ull * G;            // bytes of one load instruction's sweep
+    constexpr uint64_t kRow = kSweep * B;
 
     auto buffer_of = [&](uint64_t slot) -> uint64_t {
         const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
@@ -379,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
             ++lslot;
             lptr = slot_base(lslot);
         } else if (lslot < nslots) {
-            lptr += step_bytes;
+            lptr += kRow * U;
         }
     };
 
@@ -387,11 +453,13 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
     // set that is still being read (no register copies across the loop edge,
     // which would force a vmcnt(0) drain).
     constexpr int S = D + 1;
-    uint4 ring[S][U];
+    uint4 ring[S][U][B];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) ring[d][u] = load16(lptr + u * row_bytes);
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int b = 0; b < B; ++b) ring[d][u][b] = load16(lptr + u * kRow + b * kSweep);
         advance();
     }
     const uint64_t padded = (nsteps + S - 1) / S * S;
@@ -403,12 +471,21 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
         for (int d = 0; d < S; ++d) {
             const int refill = (d + D) % S;  // the set read by the previous stage
 #pragma unroll
-            for (int u = 0; u < U; ++u) ring[refill][u] = load16(lptr + u * row_bytes);
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int b = 0; b < B; ++b) ring[refill][u][b] = load16(lptr + u * kRow + b * kSweep);
             advance();
-            pc = column_step<U>(lds, pc, ring[d], la);
+            uint32_t c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                to_runs<B>(ring[d][u], tb);
+                c[u] = run_crc<B>(lds, ring[d][u], la);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) pc = sstep(lds, pc, la.s) ^ c[u];
             if (++step == spb) {
-                // End of this buffer: lane gl's last block is G-1-gl blocks from the end.
-                const uint32_t crc = group_reduce<G>(pc, (uint32_t)(G - 1 - gl), lds);
+                // End of this buffer: this lane's last run is G-1-run runs from the end.
+                const uint32_t crc = group_reduce<G>(pc, (uint32_t)(G - 1 - run), lds);
                 const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
                 if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = crc;
                 pc = 0;
@@ -510,7 +587,7 @@ namespace {
 
 thread_local std::string g_err;
 int g_lanes_override = 0;
-int g_stream_u = 4, g_stream_d = 3;   // streaming kernel: rows per step, steps in flight
+int g_stream_b = 1, g_stream_u = 4, g_stream_d = 3;  // streaming kernel: run blocks, rows/step, steps in flight
 bool g_stream_enabled = true;
 
 int fail(int code, const std::string& what) {
@@ -553,21 +630,25 @@ int current_device(int* cus) {
     return dev;
 }
 
-LaneConsts make_lane_consts(int g) {
+// Constants for G lanes per buffer and runs of B blocks per lane per row:
+// row shift x^(8*16*B*G), lane-combine basis of x^(8*16*B*2^k).
+LaneConsts make_lane_consts(int g, int b) {
     LaneConsts c;
-    c.kshift = xpow(8ull * 16ull * (uint64_t)g);
-    for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), c.basis[k]);
+    c.kshift = xpow(8ull * 16ull * (uint64_t)b * (uint64_t)g);
+    for (int k = 0; k < 6; ++k) mul_basis(xpow((128ull * (uint64_t)b) << k), c.basis[k]);
     return c;
 }
 
-const LaneConsts& lane_consts(int g) {
-    static LaneConsts tab[7];
+const LaneConsts& lane_consts(int g, int b = 1) {
+    static LaneConsts tab[7][3];
     static std::once_flag once;
     std::call_once(once, [] {
-        for (int lg = 2; lg <= 6; ++lg) tab[lg] = make_lane_consts(1 << lg);
+        for (int lg = 2; lg <= 6; ++lg)
+            for (int lb = 0; lb <= 2; ++lb) tab[lg][lb] = make_lane_consts(1 << lg, 1 << lb);
     });
-    int lg = g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2;
-    return tab[lg];
+    const int lg = g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2;
+    const int lb = b == 4 ? 2 : b == 2 ? 1 : 0;
+    return tab[lg][lb];
 }
 
 const PowTable& pow_table() {
@@ -587,9 +668,10 @@ const PowTable& pow_table() {
 // buffers so every lane still walks >= 16 rows (DESIGN.md "Lane groups").
 int choose_lanes(uint64_t typical_len) {
     if (g_lanes_override) return g_lanes_override;
-    if (typical_len >= 16384) return 64;
-    if (typical_len >= 8192) return 32;
-    if (typical_len >= 4096) return 16;
+    // Measured with scripts/tune_gpu.py (profiles/tune_r01.md): 1 MiB buffers
+    // G=64, 64 KiB G=32, 4-8 KiB G=8.
+    if (typical_len >= (512u << 10)) return 64;
+    if (typical_len >= (32u << 10)) return 32;
     if (typical_len >= 2048) return 8;
     return 4;
 }
@@ -629,31 +711,35 @@ SeedConsts seed_consts(uint64_t nbytes) {
     return cached;
 }
 
-template <int G, int U, int D>
+template <int G, int B, int U, int D>
 void launch_uniform_t(const UniformArgs& a, dim3 grid, hipStream_t stream) {
-    hipLaunchKernelGGL((crc32c_uniform_kernel<G, U, D>), grid, dim3(kBlock), 0, stream, a, lane_consts(G));
+    hipLaunchKernelGGL((crc32c_uniform_kernel<G, B, U, D>), grid, dim3(kBlock), 0, stream, a, lane_consts(G, B));
 }
 
+// The instantiated (B, U, D) shapes: ring registers (D+1)*U*B*4 <= 80 VGPRs.
 template <int G>
 bool launch_uniform_g(const UniformArgs& a, dim3 grid, hipStream_t stream) {
-    const int u = g_stream_u, d = g_stream_d;
-    if (u == 4 && d == 3) launch_uniform_t<G, 4, 3>(a, grid, stream);
-    else if (u == 4 && d == 2) launch_uniform_t<G, 4, 2>(a, grid, stream);
-    else if (u == 2 && d == 4) launch_uniform_t<G, 2, 4>(a, grid, stream);
-    else if (u == 8 && d == 2) launch_uniform_t<G, 8, 2>(a, grid, stream);
-    else if (u == 4 && d == 4) launch_uniform_t<G, 4, 4>(a, grid, stream);
+    const int b = g_stream_b, u = g_stream_u, d = g_stream_d;
+    if (b == 2 && u == 2 && d == 3) launch_uniform_t<G, 2, 2, 3>(a, grid, stream);
+    else if (b == 1 && u == 4 && d == 3) launch_uniform_t<G, 1, 4, 3>(a, grid, stream);
+    else if (b == 4 && u == 1 && d == 3) launch_uniform_t<G, 4, 1, 3>(a, grid, stream);
+    else if (b == 2 && u == 2 && d == 4) launch_uniform_t<G, 2, 2, 4>(a, grid, stream);
+    else if (b == 4 && u == 1 && d == 4) launch_uniform_t<G, 4, 1, 4>(a, grid, stream);
+    else if (b == 1 && u == 2 && d == 4) launch_uniform_t<G, 1, 2, 4>(a, grid, stream);
     else return false;
     return true;
 }
 
-// Streaming kernel when the batch is uniform: aligned base/stride, equal
-// length made of whole rows, row count a multiple of the step. Returns 1 if
-// it does not apply (caller falls back to the generic kernel), else 0 / error.
+bool stream_shape_ok(int b, int u, int d) {
+    return (b == 2 && u == 2 && (d == 3 || d == 4)) || (b == 1 && ((u == 4 && d == 3) || (u == 2 && d == 4))) ||
+           (b == 4 && u == 1 && (d == 3 || d == 4));
+}
+
 int try_launch_uniform(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint32_t seed0,
                        const uint32_t* seeds, uint32_t* out, hipStream_t stream) {
     if (!g_stream_enabled || count == 0) return 1;
     const int g = choose_lanes(nbytes);
-    const uint64_t row = 16ull * g;
+    const uint64_t row = 16ull * g * (uint64_t)g_stream_b;
     if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
     const uint64_t rows = nbytes / row;
     if (rows % (uint64_t)g_stream_u) return 1;
@@ -715,17 +801,17 @@ int photon_crc_set_lanes_per_buffer(int g) {
     return 0;
 }
 
-int photon_crc_set_stream_config(int rows_per_step, int steps_in_flight) {
-    if (rows_per_step == 0) {
+int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight) {
+    if (run_blocks == 0) {
         g_stream_enabled = false;
         return 0;
     }
-    const int u = rows_per_step, d = steps_in_flight;
-    if (!((u == 4 && (d == 2 || d == 3 || d == 4)) || (u == 2 && d == 4) || (u == 8 && d == 2)))
-        return fail(-EINVAL, "unsupported (rows_per_step, steps_in_flight)");
+    if (!stream_shape_ok(run_blocks, rows_per_step, steps_in_flight))
+        return fail(-EINVAL, "unsupported (run_blocks, rows_per_step, steps_in_flight)");
     g_stream_enabled = true;
-    g_stream_u = u;
-    g_stream_d = d;
+    g_stream_b = run_blocks;
+    g_stream_u = rows_per_step;
+    g_stream_d = steps_in_flight;
     return 0;
 }
 

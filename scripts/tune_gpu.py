@@ -18,12 +18,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--variants", default="stream:4:3,stream:4:2,stream:2:4,stream:8:2,stream:4:4,generic")
+ap.add_argument("--variants", default="stream:2:2:3,stream:1:4:3,stream:4:1:3,stream:2:2:4,stream:4:1:4,stream:1:2:4,generic")
 ap.add_argument("--lanes", default="0")
+ap.add_argument("--count", type=int, default=0, help="override buffer count")
 args = ap.parse_args()
 
 shapes = {"c2": (65536, 65536), "c3": (4096, 1 << 20), "c4": (1 << 20, 4096), "c5seg": (8192, 1 << 19)}
 nbytes, count = shapes[args.config]
+count = args.count or count
 stream = torch.cuda.current_stream()
 buf = torch.empty(nbytes * count, dtype=torch.uint8, device="cuda")
 ck.fill_splitmix(buf, nbytes, nbytes, count, 0x5EED0001)
@@ -50,10 +52,10 @@ def make(v, lanes):
     def f():
         ck.set_lanes_per_buffer(lanes)
         if v == "generic":
-            ck.set_stream_config(0, 0)
+            ck.set_stream_config(0)
         else:
-            _, u, d = v.split(":")
-            ck.set_stream_config(int(u), int(d))
+            _, b, u, d = v.split(":")
+            ck.set_stream_config(int(b), int(u), int(d))
         ck.batch_strided(buf, nbytes, nbytes, count, out, stream=stream)
     return f
 
@@ -71,7 +73,7 @@ for r in range(args.rounds):
             if ref is None:
                 ref = o
             assert np.array_equal(o, ref), f"variant {v}/G{l} disagrees"
-ck.set_stream_config(4, 3)
+ck.set_stream_config(1, 4, 3)
 ck.set_lanes_per_buffer(0)
 rows = []
 for k, ms in res.items():

@@ -29,6 +29,10 @@ def torch_dev():
 def _reset_lanes():
     yield
     ck.set_lanes_per_buffer(0)
+    ck.set_stream_config(1, 4, 3)
+
+
+STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (0, 0, 0)]
 
 
 def to_dev(torch, arr):
@@ -123,6 +127,22 @@ def test_strided_all_lane_groups(torch_dev, oracle, g, nbytes, stride):
         want = [oracle.crc32c(host[base_off + i * stride: base_off + i * stride + nbytes], seeds[i])
                 for i in range(count)]
         assert list(got) == want, (g, nbytes, stride, base_off)
+
+
+@pytest.mark.parametrize("shape", STREAM_SHAPES)
+@pytest.mark.parametrize("g", [8, 16, 32, 64])
+def test_stream_shapes(torch_dev, oracle, shape, g):
+    # Every streaming-kernel shape (and the generic kernel, shape 0) on uniform
+    # batches whose buffer count does not fill whole tuples or ring turns.
+    ck.set_stream_config(*shape)
+    ck.set_lanes_per_buffer(g)
+    for nbytes, count in ((16 * 4 * 64 * 4, 37), (65536, 300), (4096, 1001)):
+        d = torch_dev.empty(nbytes * count, dtype=torch_dev.uint8, device="cuda")
+        ck.fill_splitmix(d, nbytes, nbytes, count, 0x77 + nbytes)
+        got = run_strided(torch_dev, d, nbytes, nbytes, count, seeds=[(7 * i) & 0xFFFFFFFF for i in range(count)])
+        for i in list(range(0, count, max(1, count // 40))) + [count - 1]:
+            want = oracle.crc32c(datagen.stream_bytes(0x77 + nbytes + i, nbytes), (7 * i) & 0xFFFFFFFF)
+            assert got[i] == want, (shape, g, nbytes, i)
 
 
 def test_device_fill_matches_datagen(torch_dev):
