@@ -2,15 +2,17 @@
 """Benchmark of the north-star path: CRC32C over device-resident buffers on
 MI355X through the C-ABI engine (libphoton_checksum.so).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--h2d]
 
 One "step" = one pass of the hot path over one batch (BASELINE.json configs):
   c2 (default, configs[1]): 65,536 x 64 KiB random buffers, device-resident
-  c3: 1,048,576 x 4 KiB                c4: 32,768 x 1 MiB per GPU (the 8-GPU config's shard)
+  c3: 1,048,576 x 4 KiB        c4: 32,768 x 1 MiB per GPU (the 8-GPU config's shard)
   c5: 65,536 messages x 8 non-contiguous 8 KiB segments (per-segment CRC + combine)
+  --h2d: the c2 batch starting and ending in pinned host memory (chunked
+         H2D + kernel + D2H); reported in DESIGN.md, never as `value`.
 Multi-GPU: one process per GPU (torchrun); every rank checksums its own
-independent batch (weak scaling, no data-path collective; gloo is used only
-for the timing barrier and the max-over-ranks). Rank 0 prints one JSON line.
+independent batch (weak scaling, no data-path collective; gloo carries only
+the timing barrier and the max-over-ranks). Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -29,6 +31,7 @@ from photonlibos_amd import checksum as ck  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
 GIB = float(1 << 30)
+METRIC = "GiB/s CRC32C over device-resident buffers; % of HBM-read roofline"
 
 CONFIGS = {
     "c2": dict(kind="strided", nbytes=65536, count=65536,
@@ -42,18 +45,60 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=25,
+                    help="untimed steps; the first ~10 back-to-back launches run slower while clocks settle")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--h2d", action="store_true", help="host-memory end-to-end rate (for DESIGN.md)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (profiles/*.json) giving HBM bytes per launch")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def shard_seed_base(rank, count):
+    """Rank r checksums buffers with global ids [r*count, (r+1)*count):
+    splitmix streams 0x5EED0001 + global id (disjoint shards, no collective)."""
+    return 0x5EED0001 + rank * count
+
+
+def timed_region(step, steps, warmup, sync, dist=None, on_step=None):
+    """Run `warmup` untimed steps, then exactly `steps` steps bracketed by a
+    barrier + device sync on both sides. Returns the max over ranks of the
+    wall time and of the mean per-step time reported by `on_step` (ms)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    marks = []
+    t0 = time.perf_counter()
+    for s in range(steps):
+        if on_step:
+            marks.append(on_step(s, step))
+        else:
+            step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    per_step_ms = float(np.mean([m() for m in marks])) if marks else elapsed / steps * 1e3
+    if dist is not None:
+        t = torch.tensor([elapsed, per_step_ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, per_step_ms = float(t[0]), float(t[1])
+    return elapsed, per_step_ms
+
+
+def aggregate_gibps(bytes_per_step_per_rank, steps, world, elapsed):
+    """Whole-job throughput: every rank's bytes over the slowest rank's time."""
+    return bytes_per_step_per_rank * steps * world / elapsed / GIB
 
 
 class Workload:
@@ -63,18 +108,19 @@ class Workload:
         self.cfg = cfg
         self.stream = stream
         n, cnt = cfg["nbytes"], cfg["count"]
-        seed_base = 0x5EED0001 + rank * cnt
-        self.payload = torch.empty(n * cnt, dtype=torch.uint8, device="cuda")
-        ck.fill_splitmix(self.payload, n, n, cnt, seed_base, stream=stream)
-        self.bytes_per_step = n * cnt
+        if cfg["kind"] == "strided":
+            slots = cnt
+        else:
+            slots = cnt * cfg["nseg"]
+        seed_base = shard_seed_base(rank, slots)
+        self.payload = torch.empty(n * slots, dtype=torch.uint8, device="cuda")
+        ck.fill_splitmix(self.payload, n, n, slots, seed_base, stream=stream)
+        self.bytes_per_step = n * slots
         if cfg["kind"] == "strided":
             self.out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
         else:
-            nmsg, nseg = cnt, cfg["nseg"]
-            slots = nmsg * nseg
-            # the payload above is a pool of `count` slots; re-make it with nmsg*nseg slots
-            self.payload = torch.empty(n * slots, dtype=torch.uint8, device="cuda")
-            ck.fill_splitmix(self.payload, n, n, slots, seed_base, stream=stream)
+            nseg = cfg["nseg"]
+            # C5 layout: message m's segment j lives at pool slot perm[m*nseg + j].
             rng = np.random.default_rng(0x5EED0005 + rank)
             perm = rng.permutation(slots).astype(np.uint64)
             iov = np.empty((slots, 2), np.uint64)
@@ -83,8 +129,7 @@ class Workload:
             self.iov = torch.from_numpy(iov.view(np.int64)).cuda()
             self.start = torch.from_numpy(np.arange(0, slots + 1, nseg, dtype=np.uint64).view(np.int64)).cuda()
             self.seg_out = torch.zeros(slots, dtype=torch.int32, device="cuda")
-            self.out = torch.zeros(nmsg, dtype=torch.int32, device="cuda")
-            self.bytes_per_step = n * slots
+            self.out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
 
     def step(self):
@@ -95,15 +140,25 @@ class Workload:
             ck.batch_msg(self.iov, self.start, c["count"], self.seg_out, self.out, stream=self.stream)
 
     def self_check(self):
-        """Spot-check 4 results against the product's own host engine (crc32c_hw)."""
+        """Spot-check results against the product's own host engine (crc32c_hw
+        and crc32c_combine), not the oracle."""
         c = self.cfg
         n = c["nbytes"]
-        if c["kind"] != "strided":
-            return None
         out = self.out.cpu().numpy().view(np.uint32)
-        for i in (0, 1, c["count"] // 2, c["count"] - 1):
-            host = self.payload[i * n:(i + 1) * n].cpu().numpy().tobytes()
-            if ck.crc32c_hw(host) != out[i]:
+        if c["kind"] == "strided":
+            for i in (0, 1, c["count"] // 2, c["count"] - 1):
+                host = self.payload[i * n:(i + 1) * n].cpu().numpy().tobytes()
+                if ck.crc32c_hw(host) != out[i]:
+                    return False
+            return True
+        iov = self.iov.cpu().numpy().view(np.uint64)
+        base = self.payload.data_ptr()
+        for m in (0, c["count"] - 1):
+            acc = 0
+            for j in range(c["nseg"]):
+                off = int(iov[m * c["nseg"] + j, 0]) - base
+                acc = ck.crc32c_extend(self.payload[off:off + n].cpu().numpy().tobytes(), acc)
+            if acc != out[m]:
                 return False
         return True
 
@@ -123,7 +178,7 @@ def cpu_baseline(cfg, seconds):
             r = json.loads(out.stdout.strip().splitlines()[-1])
             cpu = ""
             try:
-                cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+                cpu = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
             except Exception:
                 pass
             return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
@@ -149,7 +204,29 @@ def load_traffic(path, config):
         return None
     with open(path) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch")
+    v = d.get("hbm_bytes_per_launch")
+    return int(v) if v else None  # HBM bytes per launch (PMC, corrected), vs the algorithmic bytes
+
+
+def run_h2d(args, stream):
+    """Host-memory end-to-end rate for the c2 batch (pinned host -> CRCs on host)."""
+    cfg = CONFIGS["c2"]
+    n, cnt = cfg["nbytes"], cfg["count"]
+    dev = torch.empty(n * cnt, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dev, n, n, cnt, shard_seed_base(0, cnt), stream=stream)
+    host = torch.empty(n * cnt, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dev)
+    del dev
+    torch.cuda.synchronize()
+    out = torch.zeros(cnt, dtype=torch.int32, pin_memory=True)
+    step = lambda: ck.host_batch_strided(host, n, n, cnt, out)  # noqa: E731
+    steps = max(2, min(args.steps, 10))
+    elapsed, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
+    ok = ck.crc32c_hw(host[:n].numpy().tobytes()) == int(out[0].item()) & 0xFFFFFFFF
+    print(json.dumps({"metric": "GiB/s CRC32C host-resident (pinned) end to end: H2D + kernel + D2H",
+                      "value": round(n * cnt * steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
+                      "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 3), "self_check": ok,
+                      "config": {"workload": cfg["workload"].replace("device-resident", "pinned host memory")}}))
 
 
 def main():
@@ -163,42 +240,32 @@ def main():
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     ck.set_lanes_per_buffer(args.lanes)
-    cfg = CONFIGS[args.config]
     stream = torch.cuda.current_stream()
+    if args.h2d:
+        if rank == 0:
+            run_h2d(args, stream)
+        return
+    cfg = CONFIGS[args.config]
     wl = Workload(cfg, rank, stream)
-
-    for _ in range(args.warmup):
-        wl.step()
+    wl.step()
     torch.cuda.synchronize()
     ok = wl.self_check()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        ev[s][0].record(stream)
-        wl.step()
-        ev[s][1].record(stream)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        dist.barrier()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+    def on_step(s, step):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        step()
+        b.record(stream)
+        return lambda: a.elapsed_time(b)
 
-    total_bytes = wl.bytes_per_step * args.steps * world
-    value = total_bytes / elapsed / GIB
+    elapsed, kernel_ms = timed_region(wl.step, args.steps, args.warmup, torch.cuda.synchronize, dist, on_step)
+    value = aggregate_gibps(wl.bytes_per_step, args.steps, world, elapsed)
     per_launch_gbps = wl.bytes_per_step / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic(args.traffic_json, args.config)
 
     if rank == 0:
         res = {
-            "metric": "GiB/s CRC32C over device-resident buffers; % of HBM-read roofline",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -215,7 +282,7 @@ def main():
                        "lanes_per_buffer": args.lanes or "auto"},
             "roofline": {"bound": "hbm", "achieved": round(per_launch_gbps, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(per_launch_gbps / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic},
+                         "traffic": traffic, "algorithmic_bytes": wl.bytes_per_step},
             "self_check": ok,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -59,6 +59,15 @@ const char* photon_crc_last_error(void);
 int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                 uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
+/* (i-h) Host-memory batch, the path's real source (socket / file buffers in
+ * host RAM feeding rpc/ and fs/): chunks of the batch are copied to the
+ * device (stream-ordered, 2-D so any stride packs densely) while earlier
+ * chunks are checksummed; the CRCs come back to h_out[count]. Synchronous.
+ * h_base should be pinned (hipHostMalloc / hipHostRegister) for the copies to
+ * overlap; h_seeds (optional) and h_out are host arrays. Buffers up to 256 MiB. */
+int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                     uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out);
+
 /* (ii) Arbitrary buffers: d_iov[count] (device-resident descriptors); any
  * alignment, any length (0 returns the seed). */
 int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint32_t seed0,

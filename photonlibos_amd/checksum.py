@@ -24,7 +24,7 @@ __all__ = [
     "crc32c_combine", "crc32c_combine_sw", "crc32c_combine_hw",
     "crc32c_combine_series", "crc32c_combine_series_sw", "crc32c_combine_series_hw",
     "crc32c_trim", "crc32c_trim_sw", "crc32c_trim_hw", "is_crc32c_hw_available",
-    "device_count", "set_lanes_per_buffer", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
+    "device_count", "set_lanes_per_buffer", "host_batch_strided", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
@@ -215,6 +215,13 @@ def batch_strided(base, stride, nbytes, count, out, seed=0, seeds=None, stream=N
 def batch_strided_sync(base, stride, nbytes, count, out, seed=0, seeds=None, stream=None):
     _check(lib().photon_crc32c_batch_strided_sync(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFF,
                                                   _ptr(seeds), _ptr(out), _stream(stream)))
+
+
+def host_batch_strided(base, stride, nbytes, count, out, seed=0, seeds=None):
+    """Host-memory batch through the device (chunked H2D + kernel + D2H). Synchronous.
+    base/out/seeds are host pointers (ints) or objects with data_ptr() (pinned tensors)."""
+    _check(lib().photon_crc32c_host_batch_strided(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFF,
+                                                  _ptr(seeds), _ptr(out)))
 
 
 def batch_iov(iov, count, out, seed=0, seeds=None, stream=None):

@@ -772,6 +772,46 @@ int try_launch_uniform(const uint8_t* base, uint64_t stride, uint64_t nbytes, ui
     return 0;
 }
 
+// Host-memory pipeline (photon_crc32c_host_batch_strided): per device, a copy
+// stream and a compute stream, kNumStage device staging chunks. Chunk i is
+// copied (H2D, 2-D so any host stride packs densely) while chunk i-1 is
+// checksummed; events order reuse of a staging chunk after its kernel.
+constexpr int kNumStage = 3;
+constexpr uint64_t kStageBytes = 256ull << 20;
+
+struct HostPipe {
+    bool ready = false;
+    hipStream_t copy = nullptr, comp = nullptr;
+    void* stage[kNumStage] = {};
+    hipEvent_t copied[kNumStage] = {}, consumed[kNumStage] = {};
+    uint32_t* d_out = nullptr;
+    uint32_t* d_seeds = nullptr;
+    uint64_t out_cap = 0;
+};
+
+std::mutex g_pipe_mu;
+std::vector<HostPipe> g_pipes;
+
+int pipe_for(int dev, HostPipe** out) {
+    if ((int)g_pipes.size() <= dev) g_pipes.resize(dev + 1);
+    HostPipe& p = g_pipes[dev];
+    if (!p.ready) {
+        hipError_t e;
+        if ((e = hipStreamCreateWithFlags(&p.copy, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "stream");
+        if ((e = hipStreamCreateWithFlags(&p.comp, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "stream");
+        for (int i = 0; i < kNumStage; ++i) {
+            if ((e = hipMalloc(&p.stage[i], kStageBytes)) != hipSuccess) return hip_fail(e, "hipMalloc(stage)");
+            if ((e = hipEventCreateWithFlags(&p.copied[i], hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "event");
+            if ((e = hipEventCreateWithFlags(&p.consumed[i], hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "event");
+        }
+        p.ready = true;
+    }
+    *out = &p;
+    return 0;
+}
+
 }  // namespace
 }  // namespace pcrc
 
@@ -838,6 +878,56 @@ int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64
     int rc = photon_crc32c_batch_strided(d_base, stride, nbytes, count, seed0, d_seeds, d_out, stream);
     if (rc) return rc;
     hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return 0;
+}
+
+int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                     uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out) {
+    if (!count) return 0;
+    if (!h_base || !h_out || stride < nbytes) return fail(-EINVAL, "bad arguments");
+    const uint64_t pitch = (nbytes + 255) & ~uint64_t(255);
+    if (pitch > kStageBytes) return fail(-EINVAL, "buffer larger than a staging chunk (256 MiB)");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    HostPipe* p = nullptr;
+    int rc = pipe_for(dev, &p);
+    if (rc) return rc;
+    hipError_t e;
+    if (p->out_cap < count) {
+        if (p->d_out) (void)hipFree(p->d_out);
+        if (p->d_seeds) (void)hipFree(p->d_seeds);
+        p->d_out = p->d_seeds = nullptr;
+        p->out_cap = 0;
+        if ((e = hipMalloc(&p->d_out, count * 4)) != hipSuccess) return hip_fail(e, "hipMalloc(out)");
+        if ((e = hipMalloc(&p->d_seeds, count * 4)) != hipSuccess) return hip_fail(e, "hipMalloc(seeds)");
+        p->out_cap = count;
+    }
+    if (h_seeds) {
+        e = hipMemcpyAsync(p->d_seeds, h_seeds, count * 4, hipMemcpyHostToDevice, p->comp);
+        if (e != hipSuccess) return hip_fail(e, "seeds H2D");
+    }
+    const uint64_t per_chunk = kStageBytes / pitch;
+    const uint8_t* src = static_cast<const uint8_t*>(h_base);
+    for (uint64_t first = 0, i = 0; first < count; first += per_chunk, ++i) {
+        const int slot = (int)(i % kNumStage);
+        const uint64_t k = count - first < per_chunk ? count - first : per_chunk;
+        if ((e = hipStreamWaitEvent(p->copy, p->consumed[slot], 0)) != hipSuccess) return hip_fail(e, "wait");
+        e = hipMemcpy2DAsync(p->stage[slot], pitch, src + first * stride, stride, nbytes, k, hipMemcpyHostToDevice,
+                             p->copy);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy2DAsync H2D");
+        if ((e = hipEventRecord(p->copied[slot], p->copy)) != hipSuccess) return hip_fail(e, "record");
+        if ((e = hipStreamWaitEvent(p->comp, p->copied[slot], 0)) != hipSuccess) return hip_fail(e, "wait");
+        rc = photon_crc32c_batch_strided(p->stage[slot], pitch, nbytes, k, seed0, h_seeds ? p->d_seeds + first : nullptr,
+                                         p->d_out + first, p->comp);
+        if (rc) return rc;
+        if ((e = hipEventRecord(p->consumed[slot], p->comp)) != hipSuccess) return hip_fail(e, "record");
+    }
+    e = hipMemcpyAsync(h_out, p->d_out, count * 4, hipMemcpyDeviceToHost, p->comp);
+    if (e != hipSuccess) return hip_fail(e, "out D2H");
+    e = hipStreamSynchronize(p->comp);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return 0;
 }

@@ -30,13 +30,16 @@ def main():
     ap.add_argument("--kernel", default="crc32c")
     ap.add_argument("--payload-bytes", type=float, required=True, help="algorithmic bytes per launch")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--last", type=int, default=0, help="average only the last N launches (the timed steps)")
     args = ap.parse_args()
     res = {"payload_bytes_per_launch": args.payload_bytes}
     if args.stats:
         kt = [r for r in rows(os.path.join(args.stats, "**", "*kernel_trace.csv")) if args.kernel in r["Kernel_Name"]]
         durs = {}
-        for r in kt:
+        for r in sorted(kt, key=lambda r: int(r["Start_Timestamp"])):
             durs.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        if args.last:
+            durs = {k: v[-args.last:] for k, v in durs.items()}
         res["kernels"] = {k: {"launches": len(v), "avg_ns": statistics.mean(v), "min_ns": min(v),
                               "achieved_GBps": args.payload_bytes / statistics.mean(v)}
                           for k, v in durs.items()}

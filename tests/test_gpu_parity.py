@@ -292,3 +292,18 @@ def test_single_bit_flips_detected(torch_dev, oracle):
         e[bit // 8] = 1 << (bit % 8)
         assert got[k] != got[0]
         assert got[k] ^ got[0] == oracle.crc32c(e)
+
+
+def test_host_batch_pipeline(torch_dev, oracle):
+    # Host-resident (pinned) batch through the chunked H2D + kernel + D2H pipeline,
+    # more buffers than one staging chunk holds, odd stride, per-buffer seeds.
+    nbytes, stride, count = 65536 + 8, 65536 + 24, 5000
+    host = torch_dev.empty(stride * count, dtype=torch_dev.uint8, pin_memory=True)
+    host.numpy()[:] = np.resize(datagen.stream_bytes(0xB0B, 1 << 20), stride * count)
+    seeds = torch_dev.from_numpy(np.arange(count, dtype=np.uint32).view(np.int32)).pin_memory()
+    out = torch_dev.zeros(count, dtype=torch_dev.int32, pin_memory=True)
+    ck.host_batch_strided(host, stride, nbytes, count, out, seeds=seeds)
+    got = out.numpy().view(np.uint32)
+    h = host.numpy()
+    for i in list(range(0, count, 97)) + [count - 1]:
+        assert got[i] == oracle.crc32c(h[i * stride:i * stride + nbytes], i), i
