@@ -18,8 +18,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=40)
 ap.add_argument("--rest", type=float, default=2.0, help="idle seconds between variants")
 ap.add_argument("--variants", default="read,crc:0:1:4:3,crc:32:1:4:3,crc:64:1:4:3,crc:32:0:0:0")
+ap.add_argument("--repeat", type=int, default=1)
+ap.add_argument("--shape", default="65536x65536", help="nbytes x count")
 args = ap.parse_args()
-nbytes, count = 65536, 65536
+nbytes, count = (int(x) for x in args.shape.split("x"))
 total = nbytes * count
 st = torch.cuda.current_stream()
 buf = torch.empty(total, dtype=torch.uint8, device="cuda")
@@ -27,7 +29,7 @@ ck.fill_splitmix(buf, nbytes, nbytes, count, 0x5EED0001)
 out = torch.zeros(count, dtype=torch.int32, device="cuda")
 sink = torch.zeros(256 * 256 * 8, dtype=torch.int32, device="cuda")
 torch.cuda.synchronize()
-for v in args.variants.split(","):
+for v in args.variants.split(",") * args.repeat:
     if v == "read":
         fn = lambda: ck.read_stream(buf, total, sink, sink.numel(), stream=st)  # noqa: E731
     else:
