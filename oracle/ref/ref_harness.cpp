@@ -40,6 +40,9 @@ uint64_t crc64ecma_combine_sw(uint64_t, uint64_t, uint32_t);
 uint64_t crc64ecma_combine_hw(uint64_t, uint64_t, uint32_t);
 struct CRC64ECMA_Component { uint64_t crc; uint64_t size; };
 uint64_t crc64ecma_trim_sw(CRC64ECMA_Component, CRC64ECMA_Component, CRC64ECMA_Component);
+uint64_t crc64ecma_trim_hw(CRC64ECMA_Component, CRC64ECMA_Component, CRC64ECMA_Component);
+uint64_t crc64ecma_hw_avx512(const uint8_t*, size_t, uint64_t);
+extern uint64_t (*crc64ecma_auto)(const uint8_t*, size_t, uint64_t);
 extern const uint32_t (&crc32c_lshift_table_hw)[28];
 extern const uint32_t (&crc32c_rshift_table_hw)[32];
 extern const uint32_t (&crc32c_lshift_table_sw)[32];
@@ -188,19 +191,63 @@ static int vectors() {
         v.push_back(crc32c_auto(z.data(), z.size(), 0));
         o.arr("known_answers", v); v.clear();
     }
-    // CRC64ECMA (next row): sw over random buffers (sse128 cross-checked).
+    // CRC64ECMA (next row): sw over random buffers with seeds (sse128
+    // cross-checked); avx512 outputs recorded to document its mismatch.
     {
         const size_t lens[] = {0, 1, 7, 8, 15, 16, 17, 100, 255, 256, 257, 1000, 4096, 4097, 65536};
+        const uint64_t seeds[] = {0ull, ~0ull, 0x0123456789abcdefull};
         std::vector<uint8_t> buf(65536 + 16);
-        std::vector<uint64_t> L, C;
+        std::vector<uint64_t> L, C, S, A, R;
         uint64_t rs = 0x5EED6400ull;
         for (size_t n : lens) {
             fill(buf.data(), n, ++rs);
-            uint64_t a = crc64ecma_sw(buf.data(), n, 0), b = crc64ecma_hw_sse128(buf.data(), n, 0);
-            if (a != b) { fprintf(stderr, "crc64 sw/sse disagree n=%zu\n", n); return 1; }
-            L.push_back(n); C.push_back(a);
+            for (uint64_t sd : seeds) {
+                uint64_t a = crc64ecma_sw(buf.data(), n, sd), b = crc64ecma_hw_sse128(buf.data(), n, sd);
+                if (a != b) { fprintf(stderr, "crc64 sw/sse disagree n=%zu\n", n); return 1; }
+                L.push_back(n); C.push_back(a); S.push_back(sd); R.push_back(rs);
+                A.push_back(crc64ecma_hw_avx512(buf.data(), n, sd));
+            }
         }
-        o.arr("crc64_len", L); o.arr("crc64_sw", C);
+        o.arr("crc64_len", L); o.arr("crc64_sw", C); o.arr("crc64_seed", S); o.arr("crc64_stream", R);
+        o.arr("crc64_avx512", A);
+        std::vector<uint64_t> al;
+        std::vector<uint8_t> alpha(4097);
+        for (size_t i = 0; i < alpha.size(); ++i) alpha[i] = 'a' + i % 26;
+        for (size_t n = 0; n <= 4096; ++n) {
+            uint64_t a = crc64ecma_sw(alpha.data(), n, 0);
+            if (a != crc64ecma_hw_sse128(alpha.data(), n, 0)) { fprintf(stderr, "crc64 alpha\n"); return 1; }
+            al.push_back(a);
+        }
+        o.arr("crc64_alphabet", al);
+        std::vector<uint64_t> c1v, c2v, l2v, csw, chw;
+        uint64_t st = 0xC64C64ull;
+        for (int i = 0; i < 1000; ++i) {
+            uint64_t c1 = mix64(st += 0x9E3779B97F4A7C15ull), c2 = mix64(st += 0x9E3779B97F4A7C15ull);
+            uint32_t l2 = (uint32_t)mix64(st += 0x9E3779B97F4A7C15ull);
+            if (i % 3 == 1) l2 &= 0xffff;
+            if (i == 4) c1 = 0;
+            if (i == 6) l2 = 0;
+            c1v.push_back(c1); c2v.push_back(c2); l2v.push_back(l2);
+            csw.push_back(crc64ecma_combine_sw(c1, c2, l2)); chw.push_back(crc64ecma_combine_hw(c1, c2, l2));
+        }
+        o.arr("c64_crc1", c1v); o.arr("c64_crc2", c2v); o.arr("c64_len2", l2v);
+        o.arr("c64_comb_sw", csw); o.arr("c64_comb_hw", chw);
+        std::vector<uint8_t> tb(5100);
+        fill(tb.data(), tb.size(), 0x5EEDB064ull);
+        uint64_t x = crc64ecma_sw(tb.data(), tb.size(), 0);
+        std::vector<uint64_t> t1, t3, tsw, thw;
+        for (int i = 0; i < 300; ++i) {
+            uint32_t l1 = (uint32_t)(mix64(st += 0x9E3779B97F4A7C15ull) % 2600);
+            uint32_t l3 = (uint32_t)(mix64(st += 0x9E3779B97F4A7C15ull) % (5100 - l1 + 1));
+            if (i == 0) { l1 = 0; l3 = 0; }
+            uint64_t c1 = crc64ecma_sw(tb.data(), l1, 0), c3 = crc64ecma_sw(tb.data() + 5100 - l3, l3, 0);
+            t1.push_back(l1); t3.push_back(l3);
+            tsw.push_back(crc64ecma_trim_sw({x, 5100}, {c1, l1}, {c3, l3}));
+            thw.push_back(crc64ecma_trim_hw({x, 5100}, {c1, l1}, {c3, l3}));
+        }
+        o.arr("t64_l1", t1); o.arr("t64_l3", t3); o.arr("t64_sw", tsw); o.arr("t64_hw", thw);
+        std::vector<uint64_t> tall{x};
+        o.arr("t64_all", tall);
     }
     printf("{%s\n}\n", o.s.c_str());
     return 0;

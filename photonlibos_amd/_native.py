@@ -64,6 +64,17 @@ def _declare(L):
         "crc32c_combine_series_hw": ("_Z24crc32c_combine_series_hwPjjj", u32, u32p, u32, u32),
         "crc32c_trim_sw": ("_Z14crc32c_trim_sw16CRC32C_ComponentS_S_", u32, u64, u64, u64),
         "crc32c_trim_hw": ("_Z14crc32c_trim_hw16CRC32C_ComponentS_S_", u32, u64, u64, u64),
+        # CRC-64/ECMA (crc64ecma.h). CRC64ECMA_Component is 16 bytes: passed as two u64 each.
+        "crc64ecma_sw": ("_Z12crc64ecma_swPKhmm", u64, u8p, sz, u64),
+        "crc64ecma_hw": ("_Z12crc64ecma_hwPKhmm", u64, u8p, sz, u64),
+        "crc64ecma_series_sw": ("_Z19crc64ecma_series_swPKhjjPm", None, u8p, u32, u32, ctypes.POINTER(u64)),
+        "crc64ecma_series_hw": ("_Z19crc64ecma_series_hwPKhjjPm", None, u8p, u32, u32, ctypes.POINTER(u64)),
+        "crc64ecma_combine_sw": ("_Z20crc64ecma_combine_swmmj", u64, u64, u64, u32),
+        "crc64ecma_combine_hw": ("_Z20crc64ecma_combine_hwmmj", u64, u64, u64, u32),
+        "crc64ecma_combine_series_sw": ("_Z27crc64ecma_combine_series_swPmjj", u64, ctypes.POINTER(u64), u32, u32),
+        "crc64ecma_combine_series_hw": ("_Z27crc64ecma_combine_series_hwPmjj", u64, ctypes.POINTER(u64), u32, u32),
+        "crc64ecma_trim_sw": ("_Z17crc64ecma_trim_sw19CRC64ECMA_ComponentS_S_", u64, u64, u64, u64, u64, u64, u64),
+        "crc64ecma_trim_hw": ("_Z17crc64ecma_trim_hw19CRC64ECMA_ComponentS_S_", u64, u64, u64, u64, u64, u64, u64),
     }
     L.cpp = {}
     for py, (mangled, res, *args) in cpp.items():
@@ -74,5 +85,6 @@ def _declare(L):
     # Dispatch pointers (data symbols).
     L.auto = {}
     for name in ("crc32c_auto", "crc32c_series_auto", "crc32c_combine_auto", "crc32c_combine_series_auto",
-                 "crc32c_trim_auto"):
+                 "crc32c_trim_auto", "crc64ecma_auto", "crc64ecma_series_auto", "crc64ecma_combine_auto",
+                 "crc64ecma_combine_series_auto", "crc64ecma_trim_auto"):
         L.auto[name] = ctypes.c_void_p.in_dll(L, name)

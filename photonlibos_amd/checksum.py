@@ -25,6 +25,8 @@ __all__ = [
     "crc32c_combine_series", "crc32c_combine_series_sw", "crc32c_combine_series_hw",
     "crc32c_trim", "crc32c_trim_sw", "crc32c_trim_hw", "is_crc32c_hw_available",
     "device_count", "set_lanes_per_buffer", "host_batch_strided", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
+    "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
+    "crc64ecma_combine_series", "crc64ecma_trim",
     "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
@@ -163,6 +165,60 @@ def is_crc32c_hw_available():
     """crc32c.h:89-92."""
     L = lib()
     return L.auto["crc32c_auto"].value != ctypes.cast(L.cpp["crc32c_sw"], ctypes.c_void_p).value
+
+
+# ------------------------------------------------------------ CRC-64/ECMA drop-in
+
+_CRC64_FN = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64)
+_COMB64_FN = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32)
+_TRIM64_FN = ctypes.CFUNCTYPE(ctypes.c_uint64, *([ctypes.c_uint64] * 6))
+
+
+def _cp(b):
+    return ctypes.cast(b, ctypes.c_char_p) if not isinstance(b, bytes) else b
+
+
+def crc64ecma_extend(data, crc):
+    """crc64ecma_extend (crc64ecma.h:23-30): inverted in and out (crc.cpp:119-122)."""
+    b, n = _buf(data)
+    return _auto("crc64ecma_auto", _CRC64_FN)(_cp(b), n, crc & 0xFFFFFFFFFFFFFFFF)
+
+
+def crc64ecma(data, crc=0):
+    """crc64ecma(buffer, nbytes, crc) (crc64ecma.h:36-38)."""
+    return crc64ecma_extend(data, crc)
+
+
+def crc64ecma_sw(data, crc=0):
+    b, n = _buf(data)
+    return lib().cpp["crc64ecma_sw"](_cp(b), n, crc & 0xFFFFFFFFFFFFFFFF)
+
+
+def crc64ecma_hw(data, crc=0):
+    b, n = _buf(data)
+    return lib().cpp["crc64ecma_hw"](_cp(b), n, crc & 0xFFFFFFFFFFFFFFFF)
+
+
+def crc64ecma_combine(crc1, crc2, len2):
+    """crc64ecma_combine (crc64ecma.h:53-58)."""
+    return _auto("crc64ecma_combine_auto", _COMB64_FN)(crc1, crc2, len2)
+
+
+def crc64ecma_series(buffer, part_size, n_parts):
+    b, n = _buf(buffer)
+    out = (ctypes.c_uint64 * max(n_parts, 1))()
+    lib().cpp["crc64ecma_series_sw"](_cp(b), part_size, n_parts, out)
+    return list(out)[:n_parts]
+
+
+def crc64ecma_combine_series(crcs, part_size):
+    arr = (ctypes.c_uint64 * max(len(crcs), 1))(*crcs)
+    return lib().cpp["crc64ecma_combine_series_sw"](arr, part_size, len(crcs))
+
+
+def crc64ecma_trim(all_, prefix, suffix):
+    """crc64ecma_trim (crc64ecma.h:68-87); components are (crc, size)."""
+    return _auto("crc64ecma_trim_auto", _TRIM64_FN)(all_[0], all_[1], prefix[0], prefix[1], suffix[0], suffix[1])
 
 
 # ---------------------------------------------------------- batched device API

@@ -67,4 +67,36 @@ PCRC_HD void mul_basis(uint32_t k, uint32_t basis[32]) {
     for (int i = 0; i < 32; ++i) basis[i] = mulmod(1u << i, k);
 }
 
+// ------------------------------------------------------------ CRC-64/ECMA
+// Same reflected representation at 64 bits (crc_tables.cpp:48-96 with
+// T = uint64_t): ONE = 1<<63, X = 1<<62, x^-1 = 0x92d8af2baf0e1e85.
+constexpr uint64_t kPoly64 = 0xc96c5795d7870f42ull;
+constexpr uint64_t kXInv64 = 0x92d8af2baf0e1e85ull;
+
+PCRC_HD uint64_t mulmod64(uint64_t a, uint64_t b) {
+    uint64_t r = 0;
+    for (int i = 0; i < 64; ++i, b >>= 1) {
+        r = (r >> 1) ^ ((0ull - (r & 1ull)) & kPoly64) ^ ((0ull - (b & 1ull)) & a);
+    }
+    return r;
+}
+
+PCRC_HD uint64_t xpow64(uint64_t n) {
+    uint64_t result = 1ull << 63, base = 1ull << 62;
+    for (; n; n >>= 1) {
+        if (n & 1) result = mulmod64(result, base);
+        base = mulmod64(base, base);
+    }
+    return result;
+}
+
+PCRC_HD uint64_t xpow64_inv(uint64_t n) {
+    uint64_t result = 1ull << 63, base = kXInv64;
+    for (; n; n >>= 1) {
+        if (n & 1) result = mulmod64(result, base);
+        base = mulmod64(base, base);
+    }
+    return result;
+}
+
 }  // namespace pcrc

@@ -46,13 +46,19 @@ def test_dropin_symbols_exported():
     assert not [w for w in want if w not in exp]
 
 
-def test_header_declarations_are_exported():
-    # Every non-inline function declared in the drop-in header is defined by the library.
-    txt = open(os.path.join(REPO, "include", "photon", "common", "checksum", "crc32c.h")).read()
-    decl = re.findall(r"^(?:uint32_t|void)\s+(crc32c_\w+)\(", txt, flags=re.M)
+@pytest.mark.parametrize("header", ["crc32c.h", "crc64ecma.h"])
+def test_header_declarations_are_exported(header):
+    # Every non-inline function and dispatch pointer declared in the drop-in
+    # headers is defined by the library.
+    txt = open(os.path.join(REPO, "include", "photon", "common", "checksum", header)).read()
+    decl = re.findall(r"^(?:uint32_t|uint64_t|void)\s+(crc\w+)\(", txt, flags=re.M)
+    ptrs = re.findall(r"^extern \w+ \(\*(crc\w+_auto)\)", txt, flags=re.M)
+    assert decl and ptrs
     demangled = subprocess.check_output(["nm", "-DC", "--defined-only", _native.LIB_PATH], text=True)
     for d in decl:
         assert re.search(rf"\b{d}\(", demangled), d
+    for pname in ptrs:
+        assert re.search(rf"\b{pname}$", demangled, flags=re.M), pname
 
 
 def test_library_is_gfx950_only():

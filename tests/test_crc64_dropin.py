@@ -1,0 +1,61 @@
+"""CRC-64/ECMA host drop-in (include/photon/common/checksum/crc64ecma.h)
+against the reference's golden data (checksum.crc64) and the reference's own
+outputs (ref_vectors.json: crc64ecma_sw, combine_sw/hw, trim_sw/hw). CPU only."""
+import ctypes
+
+import pytest
+
+from photonlibos_amd import checksum as ck
+from photonlibos_amd import datagen
+
+ALPHA = (b"abcdefghijklmnopqrstuvwxyz" * 200)
+
+
+@pytest.mark.parametrize("f", [ck.crc64ecma_sw, ck.crc64ecma_hw, ck.crc64ecma])
+def test_golden_checksum_crc64(f, golden_in):
+    for k, want in enumerate(golden_in["crc64ecma"]):
+        assert f(ALPHA[: k + 1]) == want, k
+
+
+@pytest.mark.parametrize("f", [ck.crc64ecma_sw, ck.crc64ecma_hw, ck.crc64ecma])
+def test_reference_vectors(f, ref_vectors):
+    rv = ref_vectors
+    for n, sd, st, want in zip(rv["crc64_len"], rv["crc64_seed"], rv["crc64_stream"], rv["crc64_sw"]):
+        assert f(datagen.stream_bytes(st, n).tobytes(), sd) == want, (n, sd)
+    for n, want in enumerate(rv["crc64_alphabet"]):
+        assert f(ALPHA[:n]) == want
+
+
+def test_combine(ref_vectors):
+    rv = ref_vectors
+    for c1, c2, l2, want in zip(rv["c64_crc1"], rv["c64_crc2"], rv["c64_len2"], rv["c64_comb_sw"]):
+        assert ck.crc64ecma_combine(c1, c2, l2) == want
+
+
+def test_combine_identity_and_series():
+    buf = datagen.stream_bytes(64, 5100).tobytes()
+    x = ck.crc64ecma(buf)
+    for l1 in (0, 1, 7, 100, 2550, 5099):
+        assert ck.crc64ecma_combine(ck.crc64ecma(buf[:l1]), ck.crc64ecma(buf[l1:]), len(buf) - l1) == x
+        assert ck.crc64ecma(buf[l1:], ck.crc64ecma(buf[:l1])) == x  # extend
+    parts = ck.crc64ecma_series(buf, 510, 10)
+    assert ck.crc64ecma_combine_series(parts, 510) == x
+
+
+def test_trim(ref_vectors):
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDB064, 5100).tobytes()
+    x = rv["t64_all"][0]
+    assert ck.crc64ecma(buf) == x
+    for l1, l3, want in zip(rv["t64_l1"], rv["t64_l3"], rv["t64_sw"]):
+        c1 = ck.crc64ecma(buf[:l1])
+        c3 = ck.crc64ecma(buf[5100 - l3:]) if l3 else 0
+        assert ck.crc64ecma_trim((x, 5100), (c1, l1), (c3, l3)) == want
+
+
+def test_trim_error_path():
+    fn = ctypes.CDLL(ck.lib()._name, use_errno=True)["_Z17crc64ecma_trim_hw19CRC64ECMA_ComponentS_S_"]
+    fn.restype = ctypes.c_uint64
+    fn.argtypes = [ctypes.c_uint64] * 6
+    ctypes.set_errno(0)
+    assert fn(1, 10, 2, 6, 3, 6) == 0 and ctypes.get_errno() == 22
