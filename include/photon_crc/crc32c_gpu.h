@@ -88,6 +88,15 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
 int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,
                                 uint64_t count, uint32_t* d_out, void* stream);
 
+/* CRC-64/ECMA batches (reference crc64ecma.h:20-38: reflected polynomial
+ * 0xC96C5795D7870F42, init and result inverted):
+ *   out[i] = crc64ecma_extend(buffer_i, nbytes_i, seed_i)
+ * Same shapes and rules as the CRC32C strided / iovec batches. */
+int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                   uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_out, void* stream);
+int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint64_t seed0,
+                               const uint64_t* d_seeds, uint64_t* d_out, void* stream);
+
 /* Synchronous convenience: photon_crc32c_batch_strided + stream sync. */
 int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                      uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream);

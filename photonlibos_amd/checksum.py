@@ -27,7 +27,7 @@ __all__ = [
     "device_count", "set_lanes_per_buffer", "host_batch_strided", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
     "crc64ecma_combine_series", "crc64ecma_trim",
-    "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
+    "batch64_strided", "batch64_iov", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
 _CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
@@ -290,6 +290,18 @@ def batch_msg(iov, msg_start, nmsg, seg_out, out, seed=0, seeds=None, stream=Non
     """out[m] = chained crc32c_extend over message m's segments. Async."""
     _check(lib().photon_crc32c_batch_msg(_ptr(iov), _ptr(msg_start), nmsg, seed & 0xFFFFFFFF, _ptr(seeds),
                                          _ptr(seg_out), _ptr(out), _stream(stream)))
+
+
+def batch64_strided(base, stride, nbytes, count, out, seed=0, seeds=None, stream=None):
+    """out[i] = crc64ecma_extend(base + i*stride, nbytes, seeds[i] or seed) (uint64 out). Async."""
+    _check(lib().photon_crc64ecma_batch_strided(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFFFFFFFFFF,
+                                                _ptr(seeds), _ptr(out), _stream(stream)))
+
+
+def batch64_iov(iov, count, out, seed=0, seeds=None, stream=None):
+    """out[i] = crc64ecma_extend(iov[i].base, iov[i].len, seed_i) (uint64 out). Async."""
+    _check(lib().photon_crc64ecma_batch_iov(_ptr(iov), count, seed & 0xFFFFFFFFFFFFFFFF, _ptr(seeds), _ptr(out),
+                                            _stream(stream)))
 
 
 def combine_batch(crc1, crc2, len2, count, out, stream=None):

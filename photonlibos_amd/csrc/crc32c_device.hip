@@ -162,6 +162,46 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
     return 0;
 }
 
+LaneConsts64 make_lane_consts64(int g) {
+    LaneConsts64 c;
+    c.kshift = xpow64(8ull * 16ull * (uint64_t)g);
+    for (int k = 0; k < 6; ++k)
+        for (int i = 0; i < 64; ++i) c.basis[k][i] = mulmod64(1ull << i, xpow64(128ull << k));
+    return c;
+}
+
+const LaneConsts64& lane_consts64(int g) {
+    static LaneConsts64 tab[7];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int lg = 2; lg <= 6; ++lg) tab[lg] = make_lane_consts64(1 << lg);
+    });
+    return tab[g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2];
+}
+
+int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t stream) {
+    if (a.count == 0) return 0;
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const int g = choose_lanes(typical_len);
+    const uint64_t gpw = 64 / g;
+    const uint64_t waves = (a.count + gpw - 1) / gpw;
+    uint64_t grid = (waves + kWaves - 1) / kWaves;
+    if (grid > (uint64_t)cus) grid = cus;
+    const LaneConsts64& kc = lane_consts64(g);
+    switch (g) {
+        case 64: hipLaunchKernelGGL(crc64_batch_kernel<64>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        case 32: hipLaunchKernelGGL(crc64_batch_kernel<32>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        case 16: hipLaunchKernelGGL(crc64_batch_kernel<16>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        case 8: hipLaunchKernelGGL(crc64_batch_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+        default: hipLaunchKernelGGL(crc64_batch_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "crc64_batch_kernel launch");
+    return 0;
+}
+
 SeedConsts seed_consts(uint64_t nbytes) {
     static std::mutex mu;
     static uint64_t cached_n = ~0ull;
@@ -439,6 +479,32 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "crc32c_msg_fold_kernel launch");
     return 0;
+}
+
+int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                   uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
+    if (count && (!d_out || (!d_base && nbytes))) return fail(-EINVAL, "null buffer or output");
+    Batch64Args a{};
+    a.base = static_cast<const uint8_t*>(d_base);
+    a.stride = stride;
+    a.nbytes = nbytes;
+    a.count = count;
+    a.seeds = d_seeds;
+    a.out = d_out;
+    a.seed0 = seed0;
+    return launch_batch64(a, nbytes, static_cast<hipStream_t>(stream));
+}
+
+int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint64_t seed0,
+                               const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
+    if (count && (!d_iov || !d_out)) return fail(-EINVAL, "null descriptor array or output");
+    Batch64Args a{};
+    a.iov = d_iov;
+    a.count = count;
+    a.seeds = d_seeds;
+    a.out = d_out;
+    a.seed0 = seed0;
+    return launch_batch64(a, 65536, static_cast<hipStream_t>(stream));
 }
 
 int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,

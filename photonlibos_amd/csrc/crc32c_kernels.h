@@ -562,4 +562,171 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint
     sink[tid] = acc;
 }
 
+// ============================================================ CRC-64/ECMA
+// Same column algorithm at 64 bits (reference crc64ecma_sw, crc.cpp:119-122:
+// reflected poly 0xC96C5795D7870F42, register inverted in and out). 64-bit
+// table entries are read with ds_read_b64; LDS holds
+//   D64: x -> x * x^64 mod P, 8 byte slices x 256 x 4 replicas x 8 B = 64 KiB
+//   S64: P -> P * x^(8*16*G),  same shape                            = 64 KiB
+//   lane-combine bases x^(128*2^k), k < 6: 6 x 64 x 8 B              =  3 KiB
+constexpr uint32_t k64SBase = 65536u;
+constexpr uint32_t k64BasisBase = 131072u;
+constexpr uint32_t k64LdsBytes = k64BasisBase + 6u * 64u * 8u;
+
+struct LaneConsts64 {
+    uint64_t kshift;           // x^(8*16*G) mod P64
+    uint64_t basis[6][64];     // basis of x^(128 * 2^k)
+};
+
+struct Batch64Args {
+    const uint8_t* base;
+    uint64_t stride;
+    uint64_t nbytes;
+    const photon_crc_iovec* iov;
+    uint64_t count;
+    const uint64_t* seeds;
+    uint64_t* out;
+    uint64_t seed0;
+};
+
+__device__ __forceinline__ uint64_t lds_dword(const uint64_t* lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+
+// Slice t of table base `tb` (layout [slice][idx][lane%4], 8-byte entries).
+template <int T>
+__device__ __forceinline__ uint64_t look64(const uint64_t* lds, uint64_t x, uint32_t tb) {
+    const uint32_t idx = (uint32_t)(x >> (8 * T)) & 0xffu;
+    return lds_dword(lds, tb + T * 8192u + idx * 32u);
+}
+
+__device__ __forceinline__ uint64_t step64(const uint64_t* lds, uint64_t x, uint32_t tb) {
+    return look64<0>(lds, x, tb) ^ look64<1>(lds, x, tb) ^ look64<2>(lds, x, tb) ^ look64<3>(lds, x, tb) ^
+           look64<4>(lds, x, tb) ^ look64<5>(lds, x, tb) ^ look64<6>(lds, x, tb) ^ look64<7>(lds, x, tb);
+}
+
+__device__ __forceinline__ uint64_t bytestep64(const uint64_t* lds, uint64_t c, uint8_t b, uint32_t db) {
+    // D64 slice 7: (b << 56) * x^64 = b * x^8, the classic byte table.
+    return look64<7>(lds, (uint64_t)((c ^ b) & 0xffu) << 56, db) ^ (c >> 8);
+}
+
+__device__ __forceinline__ uint64_t mul_basis64(uint64_t p, const uint64_t* basis) {
+    uint64_t r = 0;
+#pragma unroll 4
+    for (int i = 0; i < 64; ++i) r ^= (0ull - ((p >> i) & 1ull)) & basis[i];
+    return r;
+}
+
+// Words at byte offset `off` of the first 16-byte blocks: zero the bytes
+// before the data start s0, XOR the (already inverted) 64-bit init into data
+// bytes s0..s0+7.
+__device__ __forceinline__ uint64_t head_word64(uint64_t w, int off, int s0, uint64_t init) {
+    const int k = s0 - off;
+    if (k >= 8) return 0ull;
+    if (k > 0) w &= ~0ull << (8 * k);
+    if (k >= 0) w ^= init << (8 * k);
+    else if (k > -8) w ^= init >> (8 * -k);
+    return w;
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
+    __shared__ __attribute__((aligned(16))) uint64_t lds[k64LdsBytes / 8];
+    {
+        // 1024 threads: thread -> (slice t, index b); 2048 entries per table.
+        const uint32_t tid = threadIdx.x;
+        for (uint32_t e = tid; e < 2048u; e += kBlock) {
+            const uint32_t t = e >> 8, b = e & 255u;
+            const uint64_t v = (uint64_t)b << (8 * t);
+            const uint64_t dv = mulmod64(v, kPoly64 /* x^64 mod P64 = the reflected polynomial */);
+            const uint64_t sv = mulmod64(v, kc.kshift);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                lds[(t * 8192u + b * 32u + r * 8u) / 8] = dv;
+                lds[(k64SBase + t * 8192u + b * 32u + r * 8u) / 8] = sv;
+            }
+        }
+        if (tid < 6 * 64) lds[k64BasisBase / 8 + tid] = kc.basis[tid >> 6][tid & 63];
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    constexpr int GPW = 64 / G;
+    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
+    const uint32_t db = (lane & 3u) * 8u;            // D64 base for this lane's replica
+    const uint32_t sb = k64SBase + (lane & 3u) * 8u;  // S64 base
+    const uint64_t* basis = lds + k64BasisBase / 8;
+
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave_id(); wv * GPW < args.count; wv += nwaves) {
+        const uint64_t bi = wv * GPW + grp;
+        const bool active = bi < args.count;
+        const uint8_t* p = nullptr;
+        uint64_t n = 0, seed = args.seed0;
+        if (active) {
+            if (args.iov) {
+                p = static_cast<const uint8_t*>(args.iov[bi].base);
+                n = args.iov[bi].len;
+            } else {
+                p = args.base + bi * args.stride;
+                n = args.nbytes;
+            }
+            if (args.seeds) seed = args.seeds[bi];
+        }
+        const uint64_t init = ~seed;  // crc.cpp:119-122: register starts at ~crc
+        uint64_t reg;
+        if (n < 64) {
+            reg = init;
+            if (gl == 0)
+                for (uint64_t k = 0; k < n; ++k) reg = bytestep64(lds, reg, load8(p + k), db);
+        } else {
+            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+            const uint8_t* e = p + n;
+            const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
+            const int s0 = (int)(p - a0);
+            const uint64_t nb = (uint64_t)(eb - a0) >> 4;
+            const uint64_t rows = (nb + G - 1) / G;
+            const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);
+            const uint8_t* lp = a0 + 16 * gl;
+            uint64_t pc = 0;
+            for (uint64_t row = 0; row < rows; row += 2) {
+                uint4 w[2];
+                bool have[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const uint64_t i = (row + u) * G + gl;
+                    have[u] = row + u < rows && i < nb;
+                    w[u] = have[u] ? load16(lp + (row + u) * (16 * G)) : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    if (!have[u]) continue;
+                    uint64_t lo = ((uint64_t)w[u].y << 32) | w[u].x, hi = ((uint64_t)w[u].w << 32) | w[u].z;
+                    if (row + u == 0 && gl < 2) {
+                        lo = head_word64(lo, (int)gl * 16, s0, init);
+                        hi = head_word64(hi, (int)gl * 16 + 8, s0, init);
+                    }
+                    const uint64_t c = step64(lds, step64(lds, lo, db) ^ hi, db);
+                    pc = step64(lds, pc, sb) ^ c;
+                }
+            }
+            const uint32_t d = (rlast + G - 1 - gl) & (G - 1);
+#pragma unroll 1
+            for (int k = 0; k < LOG2G; ++k)
+                if ((d >> k) & 1u) pc = mul_basis64(pc, basis + 64 * k);
+#pragma unroll
+            for (int o = G / 2; o > 0; o >>= 1) {
+                const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)pc, o, 64);
+                const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(pc >> 32), o, 64);
+                pc ^= ((uint64_t)hi32 << 32) | lo32;
+            }
+            reg = pc;
+            if (gl == 0)
+                for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), db);
+        }
+        if (active && gl == 0) args.out[bi] = ~reg;
+    }
+}
+
 }  // namespace pcrc
