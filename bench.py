@@ -42,6 +42,8 @@ CONFIGS = {
                workload="C4 shard: 32768 x 1 MiB buffers per GPU (256K x 1 MiB over 8 GPUs)"),
     "c5": dict(kind="msg", nbytes=8192, count=65536, nseg=8,
                workload="C5: 65536 messages x 8 non-contiguous 8 KiB segments, per-segment CRC + combine"),
+    "c2_crc64": dict(kind="strided64", nbytes=65536, count=65536,
+                     workload="C2 shape, CRC-64/ECMA (next row): 65536 x 64 KiB, device-resident, per GPU"),
 }
 
 
@@ -108,7 +110,7 @@ class Workload:
         self.cfg = cfg
         self.stream = stream
         n, cnt = cfg["nbytes"], cfg["count"]
-        if cfg["kind"] == "strided":
+        if cfg["kind"] in ("strided", "strided64"):
             slots = cnt
         else:
             slots = cnt * cfg["nseg"]
@@ -118,6 +120,8 @@ class Workload:
         self.bytes_per_step = n * slots
         if cfg["kind"] == "strided":
             self.out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+        elif cfg["kind"] == "strided64":
+            self.out = torch.zeros(cnt, dtype=torch.int64, device="cuda")
         else:
             nseg = cfg["nseg"]
             # C5 layout: message m's segment j lives at pool slot perm[m*nseg + j].
@@ -136,6 +140,8 @@ class Workload:
         c = self.cfg
         if c["kind"] == "strided":
             ck.batch_strided(self.payload, c["nbytes"], c["nbytes"], c["count"], self.out, stream=self.stream)
+        elif c["kind"] == "strided64":
+            ck.batch64_strided(self.payload, c["nbytes"], c["nbytes"], c["count"], self.out, stream=self.stream)
         else:
             ck.batch_msg(self.iov, self.start, c["count"], self.seg_out, self.out, stream=self.stream)
 
@@ -144,6 +150,13 @@ class Workload:
         and crc32c_combine), not the oracle."""
         c = self.cfg
         n = c["nbytes"]
+        if c["kind"] == "strided64":
+            out = self.out.cpu().numpy().view(np.uint64)
+            for i in (0, c["count"] - 1):
+                host = self.payload[i * n:(i + 1) * n].cpu().numpy().tobytes()
+                if ck.crc64ecma_sw(host) != int(out[i]):
+                    return False
+            return True
         out = self.out.cpu().numpy().view(np.uint32)
         if c["kind"] == "strided":
             for i in (0, 1, c["count"] // 2, c["count"] - 1):
@@ -265,7 +278,7 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": METRIC,
+            "metric": METRIC.replace("CRC32C", "CRC-64/ECMA") if cfg["kind"] == "strided64" else METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,

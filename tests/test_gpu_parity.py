@@ -36,7 +36,7 @@ STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4
 
 
 def to_dev(torch, arr):
-    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+    return torch.from_numpy(np.array(arr, copy=True)).cuda()
 
 
 def u32(t):
