@@ -48,6 +48,13 @@ typedef struct photon_crc_iovec {
     uint64_t len;
 } photon_crc_iovec;
 
+/* Same layout as CRC32C_Component {uint32_t crc; uint32_t size;}
+ * (common/checksum/crc32c.h:76-79); a CRC32C_Component array may be passed. */
+typedef struct photon_crc_component {
+    uint32_t crc;
+    uint32_t size;
+} photon_crc_component;
+
 /* Number of usable gfx950 devices (>0), or a negative error code. */
 int photon_crc_device_count(void);
 
@@ -87,6 +94,42 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
  * reference's shortcuts (crc1 == 0 -> crc2, len2 == 0 -> crc1). */
 int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,
                                 uint64_t count, uint32_t* d_out, void* stream);
+
+/* Device forms of the contiguous-batch calls (crc32c.h:52-57, 71-74, 84-87),
+ * same results as the drop-in host functions for the same inputs:
+ *   series:          d_crc_parts[i] = crc32c(d_buffer + i*part_size, part_size)
+ *                    with crc32c_series' semantics (the SSE4.2 engine that
+ *                    crc32c_series_auto selects: part_size < 8 gives 0s);
+ *   combine_series:  *d_result = crc32c_combine_series(d_crc, part_size,
+ *                    n_parts), including n_parts == 0 -> 0 and the
+ *                    part_size == 0 shortcut behaviour;
+ *   trim_batch:      d_out[i] = crc32c_trim(d_all[i], d_prefix[i],
+ *                    d_suffix[i]); an element whose sizes are inconsistent
+ *                    gives 0 (the reference's EINVAL result) and, when d_nerr
+ *                    is non-null, increments *d_nerr (zero it beforehand);
+ *   extend_device:   *d_out = crc32c_extend(d_data, nbytes, seed) for ONE
+ *                    long buffer: split into up to 4096 pieces that run in
+ *                    parallel, then combined on the device.
+ * Asynchronous on `stream` like the batches. */
+int photon_crc32c_series_device(const void* d_buffer, uint32_t part_size, uint32_t n_parts, uint32_t* d_crc_parts,
+                                void* stream);
+int photon_crc32c_combine_series_device(const uint32_t* d_crc, uint32_t part_size, uint32_t n_parts,
+                                        uint32_t* d_result, void* stream);
+int photon_crc32c_trim_batch(const photon_crc_component* d_all, const photon_crc_component* d_prefix,
+                             const photon_crc_component* d_suffix, uint64_t count, uint32_t* d_out,
+                             uint32_t* d_nerr, void* stream);
+int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, void* stream);
+
+/* Route the drop-in entry points to the device when handed device memory:
+ * with on != 0, crc32c_auto / crc32c_series_auto / crc32c_combine_series_auto
+ * (crc.cpp:126-134) point to wrappers that ask HIP whether the data pointer
+ * is device memory (hipMemoryTypeDevice) and, if so, run the calls above
+ * synchronously on that pointer's device (legacy default stream), else call
+ * the host engine. Off (the default, also at load time) restores the host
+ * engines. Returns 0, or -EIO if a routed call failed since the last switch
+ * (a routed call that fails returns 0 / writes nothing and records the error
+ * text; there is no CPU recomputation). */
+int photon_crc_set_device_dispatch(int on);
 
 /* CRC-64/ECMA batches (reference crc64ecma.h:20-38: reflected polynomial
  * 0xC96C5795D7870F42, init and result inverted):

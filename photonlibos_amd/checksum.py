@@ -310,6 +310,56 @@ def combine_batch(crc1, crc2, len2, count, out, stream=None):
                                              _stream(stream)))
 
 
+def series_device(buffer, part_size, n_parts, out, stream=None):
+    """crc32c_series over device memory (crc32c.h:52-57). Async."""
+    _check(lib().photon_crc32c_series_device(_ptr(buffer), part_size, n_parts, _ptr(out), _stream(stream)))
+
+
+def combine_series_device(crcs, part_size, n_parts, result, stream=None):
+    """*result = crc32c_combine_series(crcs, part_size, n_parts) on the device (crc32c.h:71-74). Async."""
+    _check(lib().photon_crc32c_combine_series_device(_ptr(crcs), part_size, n_parts, _ptr(result),
+                                                     _stream(stream)))
+
+
+def trim_batch(all_, prefix, suffix, count, out, nerr=None, stream=None):
+    """out[i] = crc32c_trim(all_[i], prefix[i], suffix[i]); components are {u32 crc, u32 size}
+    pairs (crc32c.h:76-87). *nerr counts inconsistent elements (their out is 0). Async."""
+    _check(lib().photon_crc32c_trim_batch(_ptr(all_), _ptr(prefix), _ptr(suffix), count, _ptr(out),
+                                          _ptr(nerr) if nerr is not None else None, _stream(stream)))
+
+
+def extend_device(data, nbytes, seed, out, stream=None):
+    """*out = crc32c_extend(data, nbytes, seed) for one long device buffer. Async."""
+    _check(lib().photon_crc32c_extend_device(_ptr(data), nbytes, seed & 0xFFFFFFFF, _ptr(out), _stream(stream)))
+
+
+def set_device_dispatch(on):
+    """Route crc32c_auto / crc32c_series_auto / crc32c_combine_series_auto to the
+    device for device pointers (photon_crc_set_device_dispatch)."""
+    _check(lib().photon_crc_set_device_dispatch(1 if on else 0))
+
+
+_CRC_PTR_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32)
+_SERIES_PTR_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p)
+_CSER_PTR_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32)
+
+
+def crc32c_extend_at(addr, nbytes, crc=0):
+    """crc32c_extend through the crc32c_auto pointer on a raw address (what a
+    C++ caller holding a device pointer would call)."""
+    return _auto("crc32c_auto", _CRC_PTR_FN)(addr, nbytes, crc & 0xFFFFFFFF)
+
+
+def crc32c_series_at(addr, part_size, n_parts, out_addr):
+    """crc32c_series through crc32c_series_auto on raw addresses."""
+    _auto("crc32c_series_auto", _SERIES_PTR_FN)(addr, part_size, n_parts, out_addr)
+
+
+def crc32c_combine_series_at(addr, part_size, n_parts):
+    """crc32c_combine_series through crc32c_combine_series_auto on a raw address."""
+    return _auto("crc32c_combine_series_auto", _CSER_PTR_FN)(addr, part_size, n_parts)
+
+
 def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
     """Streaming-kernel shape (B, U, D) for uniform batches; B = 0 disables it."""
     _check(lib().photon_crc_set_stream_config(run_blocks, rows_per_step, steps_in_flight))

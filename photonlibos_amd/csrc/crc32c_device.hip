@@ -35,9 +35,12 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include <photon/common/checksum/crc32c.h>
 
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "crc32c_kernels.h"
@@ -119,6 +122,31 @@ const PowTable& pow_table() {
     static std::once_flag once;
     std::call_once(once, [] {
         uint32_t v = xpow(8);  // x^8
+        for (int i = 0; i < 64; ++i) {
+            t.x8pow2[i] = v;
+            v = mulmod(v, v);
+        }
+    });
+    return t;
+}
+
+// x^(8*part*2^i): powers of K = x^(8*part) for the combine_series kernel.
+PowTable part_pow_table(uint64_t part) {
+    PowTable t;
+    uint32_t v = xpow(8ull * part);
+    for (int i = 0; i < 64; ++i) {
+        t.x8pow2[i] = v;
+        v = mulmod(v, v);
+    }
+    return t;
+}
+
+// x^(-8*2^i): the right shift of crc32c_rshift_sw (crc_tables.cpp:147-164).
+const PowTable& rshift_table() {
+    static PowTable t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        uint32_t v = xpow_inv(8);
         for (int i = 0; i < 64; ++i) {
             t.x8pow2[i] = v;
             v = mulmod(v, v);
@@ -522,6 +550,102 @@ int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, 
     return 0;
 }
 
+int photon_crc32c_series_device(const void* d_buffer, uint32_t part_size, uint32_t n_parts, uint32_t* d_crc_parts,
+                                void* stream) {
+    if (!n_parts) return 0;
+    if (!d_crc_parts || (!d_buffer && part_size)) return fail(-EINVAL, "null buffer or output");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (part_size < 8) {  // crc32c_series_hw (crc.cpp:481-500) leaves such parts at 0
+        int cus = 0;
+        int dev = current_device(&cus);
+        if (dev < 0) return dev;
+        hipError_t e = hipMemsetAsync(d_crc_parts, 0, 4ull * n_parts, st);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    return photon_crc32c_batch_strided(d_buffer, part_size, part_size, n_parts, 0, nullptr, d_crc_parts, stream);
+}
+
+int photon_crc32c_combine_series_device(const uint32_t* d_crc, uint32_t part_size, uint32_t n_parts,
+                                        uint32_t* d_result, void* stream) {
+    if (!d_result || (!d_crc && n_parts)) return fail(-EINVAL, "null argument");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemsetAsync(d_result, 0, 4, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if (!n_parts) return 0;
+    if (!part_size) {
+        hipLaunchKernelGGL(crc32c_first_nonzero_kernel, dim3(1), dim3(1024), 0, st, d_crc, (uint64_t)n_parts,
+                           d_result);
+    } else {
+        const uint64_t threads = ((uint64_t)n_parts + kSeriesChunk - 1) / kSeriesChunk;
+        hipLaunchKernelGGL(crc32c_combine_series_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, d_crc,
+                           (uint64_t)n_parts, d_result, part_pow_table(part_size));
+    }
+    e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "combine_series kernel launch");
+}
+
+int photon_crc32c_trim_batch(const photon_crc_component* d_all, const photon_crc_component* d_prefix,
+                             const photon_crc_component* d_suffix, uint64_t count, uint32_t* d_out,
+                             uint32_t* d_nerr, void* stream) {
+    if (!count) return 0;
+    if (!d_all || !d_prefix || !d_suffix || !d_out) return fail(-EINVAL, "null argument");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const int bs = 256;
+    hipLaunchKernelGGL(crc32c_trim_kernel, dim3((count + bs - 1) / bs), dim3(bs), 0,
+                       static_cast<hipStream_t>(stream), d_all, d_prefix, d_suffix, count, d_out, d_nerr,
+                       pow_table(), rshift_table());
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "crc32c_trim_kernel launch");
+}
+
+int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, void* stream) {
+    if (!d_out || (!d_data && nbytes)) return fail(-EINVAL, "null buffer or output");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // Pieces: >= 16 KiB, 4 KiB multiples (whole rows for every lane group),
+    // at most 4096 of them (enough waves to fill 256 CUs).
+    uint64_t piece = (nbytes + 4095) / 4096;
+    piece = (piece + 4095) & ~4095ull;
+    if (piece < (16u << 10)) piece = 16u << 10;
+    const uint64_t k = nbytes ? (nbytes + piece - 1) / piece : 1;
+    if (k == 1)  // (nbytes == 0 gives the seed, as crc32c_extend does)
+        return photon_crc32c_batch_strided(d_data, nbytes, nbytes, 1, seed, nullptr, d_out, stream);
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    // Stream-ordered scratch: k descriptors + k piece CRCs.
+    void* scratch = nullptr;
+    hipError_t e = hipMallocAsync(&scratch, k * sizeof(photon_crc_iovec) + k * 4, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    auto* iov = static_cast<photon_crc_iovec*>(scratch);
+    auto* crcs = reinterpret_cast<uint32_t*>(iov + k);
+    hipLaunchKernelGGL(crc32c_split_kernel, dim3((k + 255) / 256), dim3(256), 0, st,
+                       static_cast<const uint8_t*>(d_data), nbytes, piece, k, iov);
+    e = hipGetLastError();
+    int rc = e == hipSuccess ? 0 : hip_fail(e, "crc32c_split_kernel launch");
+    if (!rc) {
+        BatchArgs a{};
+        a.iov = iov;
+        a.count = k;
+        a.out = crcs;
+        rc = launch_batch(a, piece, st);
+    }
+    if (!rc) rc = photon_crc32c_combine_series_device(crcs, (uint32_t)piece, (uint32_t)(k - 1), d_out, stream);
+    if (!rc) {
+        hipLaunchKernelGGL(crc32c_extend_finish_kernel, dim3(1), dim3(1), 0, st, d_out, crcs + (k - 1),
+                           nbytes - (k - 1) * piece, seed, nbytes, pow_table());
+        e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "crc32c_extend_finish_kernel launch");
+    }
+    e = hipFreeAsync(scratch, st);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
+}
+
 int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
                                 void* stream) {
     if (!d_base || !d_sink || (reinterpret_cast<uintptr_t>(d_base) & 15)) return fail(-EINVAL, "bad arguments");
@@ -556,3 +680,129 @@ int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ device dispatch
+// photon_crc_set_device_dispatch: the drop-in dispatch pointers (crc.cpp:126-134)
+// routed to the calls above when the data pointer is device memory.
+namespace pcrc {
+namespace {
+
+std::mutex g_dispatch_mu;
+std::atomic<int> g_dispatch_err{0};
+bool g_dispatch_on = false;
+uint32_t (*g_host_crc)(const uint8_t*, size_t, uint32_t) = nullptr;
+void (*g_host_series)(const uint8_t*, uint32_t, uint32_t, uint32_t*) = nullptr;
+uint32_t (*g_host_cseries)(uint32_t*, uint32_t, uint32_t) = nullptr;
+
+// Device owning `p`, or -1 for host / unregistered memory.
+int device_of(const void* p) {
+    if (!p) return -1;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // do not leave the probe's error for the caller
+        return -1;
+    }
+    return attr.type == hipMemoryTypeDevice ? attr.device : -1;
+}
+
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// A routed call that fails has no error channel in the reference signature:
+// it is reported loudly (stderr, errno = EIO, sticky flag), never recomputed.
+void routed_failure(const char* what, int rc) {
+    g_dispatch_err.store(1);
+    fprintf(stderr, "photon_crc device dispatch: %s failed (%d): %s\n", what, rc, g_err.c_str());
+    errno = EIO;
+}
+
+// Run f(d_tmp) with `bytes` of stream-ordered device scratch on the default
+// stream, copy `out_bytes` of it to `h_out`, and wait.
+template <typename F>
+int with_scratch(uint64_t bytes, void* h_out, uint64_t out_bytes, F f) {
+    void* tmp = nullptr;
+    hipError_t e = hipMallocAsync(&tmp, bytes, nullptr);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    int rc = f(tmp);
+    if (!rc) {
+        e = hipMemcpyAsync(h_out, tmp, out_bytes, hipMemcpyDeviceToHost, nullptr);
+        if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync");
+    }
+    e = hipFreeAsync(tmp, nullptr);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    e = hipStreamSynchronize(nullptr);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    return rc;
+}
+
+uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
+    const int dev = n ? device_of(p) : -1;
+    if (dev < 0) return g_host_crc(p, n, crc);
+    DeviceScope scope(dev);
+    uint32_t r = 0;
+    int rc = with_scratch(4, &r, 4, [&](void* d) {
+        return photon_crc32c_extend_device(p, n, crc, static_cast<uint32_t*>(d), nullptr);
+    });
+    if (rc) routed_failure("crc32c_extend", rc);
+    return rc ? 0 : r;
+}
+
+void dispatch_series(const uint8_t* buf, uint32_t part, uint32_t n, uint32_t* parts) {
+    const int dev = (part && n) ? device_of(buf) : -1;
+    if (dev < 0) return g_host_series(buf, part, n, parts);
+    DeviceScope scope(dev);
+    int rc;
+    if (device_of(parts) == dev) {
+        rc = photon_crc32c_series_device(buf, part, n, parts, nullptr);
+        hipError_t e = rc ? hipSuccess : hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    } else {
+        rc = with_scratch(4ull * n, parts, 4ull * n, [&](void* d) {
+            return photon_crc32c_series_device(buf, part, n, static_cast<uint32_t*>(d), nullptr);
+        });
+    }
+    if (rc) routed_failure("crc32c_series", rc);
+}
+
+uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
+    const int dev = n ? device_of(crc) : -1;
+    if (dev < 0) return g_host_cseries(crc, part, n);
+    DeviceScope scope(dev);
+    uint32_t r = 0;
+    int rc = with_scratch(4, &r, 4, [&](void* d) {
+        return photon_crc32c_combine_series_device(crc, part, n, static_cast<uint32_t*>(d), nullptr);
+    });
+    if (rc) routed_failure("crc32c_combine_series", rc);
+    return rc ? 0 : r;
+}
+
+}  // namespace
+}  // namespace pcrc
+
+extern "C" int photon_crc_set_device_dispatch(int on) {
+    using namespace pcrc;
+    std::lock_guard<std::mutex> lk(g_dispatch_mu);
+    if (on && !g_dispatch_on) {
+        g_host_crc = crc32c_auto;
+        g_host_series = crc32c_series_auto;
+        g_host_cseries = crc32c_combine_series_auto;
+        crc32c_auto = dispatch_crc;
+        crc32c_series_auto = dispatch_series;
+        crc32c_combine_series_auto = dispatch_combine_series;
+        g_dispatch_on = true;
+    } else if (!on && g_dispatch_on) {
+        crc32c_auto = g_host_crc;
+        crc32c_series_auto = g_host_series;
+        crc32c_combine_series_auto = g_host_cseries;
+        g_dispatch_on = false;
+    }
+    return g_dispatch_err.exchange(0) ? -EIO : 0;
+}

@@ -516,6 +516,89 @@ __global__ void crc32c_combine_kernel(const uint32_t* c1, const uint32_t* c2, co
     out[i] = !a ? b : !len ? a : (shift_bytes_tab(a, len, pt) ^ b);
 }
 
+// ------------------------------------------- device series / trim / extend
+// (crc32c.h:52-57, 71-74, 84-87 over device memory.)
+
+// combine_series with part_size > 0 is linear (the crc1 == 0 shortcut of
+// crc.cpp:394 agrees with the formula): result = XOR_i crc[i] * K^(n-1-i),
+// K = x^(8*part_size). Thread t Horner-folds kSeriesChunk consecutive parts,
+// shifts its partial by K^(parts after its chunk) and XOR-reduces into
+// *result (zeroed by the caller; XOR is order-free, so atomics stay exact).
+constexpr int kSeriesChunk = 16;
+
+__global__ __launch_bounds__(256) void crc32c_combine_series_kernel(const uint32_t* crc, uint64_t n,
+                                                                    uint32_t* result, PowTable kp) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t lo = t * kSeriesChunk;
+    uint32_t acc = 0;
+    if (lo < n) {
+        const uint64_t hi = lo + kSeriesChunk < n ? lo + kSeriesChunk : n;
+        for (uint64_t i = lo; i < hi; ++i) acc = mulmod(acc, kp.x8pow2[0]) ^ crc[i];
+        acc = shift_bytes_tab(acc, n - hi, kp);  // kp.x8pow2[j] = K^(2^j)
+    }
+    for (int off = 32; off; off >>= 1) acc ^= __shfl_xor(acc, off);
+    if ((threadIdx.x & 63u) == 0 && acc) atomicXor(result, acc);
+}
+
+// combine_series with part_size == 0: every combine takes a shortcut
+// (crc.cpp:394-395), so the fold is the first non-zero crc (0 if none).
+__global__ __launch_bounds__(1024) void crc32c_first_nonzero_kernel(const uint32_t* crc, uint64_t n,
+                                                                    uint32_t* result) {
+    __shared__ unsigned long long first;
+    if (threadIdx.x == 0) first = ~0ull;
+    __syncthreads();
+    for (uint64_t base = 0; base < n; base += blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        if (i < n && crc[i]) atomicMin(&first, (unsigned long long)i);
+        __syncthreads();
+        if (first != ~0ull) break;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *result = first == ~0ull ? 0u : crc[first];
+}
+
+// crc32c_trim (crc.cpp:442-464) per element, including its 32-bit size sum
+// and the combine shortcuts. Inconsistent sizes give 0 and count an error
+// (the reference sets errno = EINVAL and returns 0).
+__global__ void crc32c_trim_kernel(const photon_crc_component* all, const photon_crc_component* pre,
+                                   const photon_crc_component* suf, uint64_t n, uint32_t* out, uint32_t* nerr,
+                                   PowTable lsh, PowTable rsh) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const photon_crc_component a = all[i], p = pre[i], s = suf[i];
+    if (a.size < (uint32_t)(p.size + s.size)) {
+        out[i] = 0;
+        if (nerr) atomicAdd(nerr, 1u);
+        return;
+    }
+    uint32_t crc = a.crc;
+    if (p.size) {
+        const uint32_t len = a.size - p.size;
+        crc = !p.crc ? crc : !len ? p.crc : (shift_bytes_tab(p.crc, len, lsh) ^ crc);
+    }
+    if (s.size) crc = shift_bytes_tab(crc ^ s.crc, s.size, rsh);
+    out[i] = crc;
+}
+
+// Split one long buffer into `k` pieces of `piece` bytes (the last one
+// shorter) for the batch kernel (photon_crc32c_extend_device).
+__global__ void crc32c_split_kernel(const uint8_t* data, uint64_t nbytes, uint64_t piece, uint64_t k,
+                                    photon_crc_iovec* iov) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const uint64_t off = i * piece;
+    iov[i].base = data + off;
+    iov[i].len = i + 1 < k ? piece : nbytes - off;
+}
+
+// out = (out * x^(8*last_len) ^ last_crc) ^ seed * x^(8*nbytes): append the
+// last piece to the folded equal pieces and apply crc32c_extend's seed.
+__global__ void crc32c_extend_finish_kernel(uint32_t* out, const uint32_t* last_crc, uint64_t last_len,
+                                            uint32_t seed, uint64_t nbytes, PowTable pt) {
+    uint32_t c = shift_bytes_tab(*out, last_len, pt) ^ *last_crc;
+    *out = c ^ shift_bytes_tab(seed, nbytes, pt);
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;

@@ -121,3 +121,19 @@ def test_large_buffers_match_oracle(oracle):
 def test_numpy_buffers():
     a = np.frombuffer(datagen.stream_bytes(1, 4096).tobytes(), np.uint8)
     assert ck.crc32c(a) == ck.crc32c_sw(a.tobytes())
+
+
+def test_device_dispatch_keeps_host_results(alphabet):
+    # With device routing on, host pointers still take the host engines
+    # (photon_crc_set_device_dispatch); on a GPU-less host nothing is routed.
+    from photonlibos_amd import checksum as ck
+    before = (ck.crc32c(alphabet), ck.crc32c_series(alphabet[:4096], 1024, 4),
+              ck.crc32c_combine_series([1, 2, 3], 10))
+    ck.set_device_dispatch(True)
+    try:
+        assert ck.crc32c(b"123456789") == 0x58E3FA20
+        assert (ck.crc32c(alphabet), ck.crc32c_series(alphabet[:4096], 1024, 4),
+                ck.crc32c_combine_series([1, 2, 3], 10)) == before
+    finally:
+        ck.set_device_dispatch(False)
+    assert ck.is_crc32c_hw_available()

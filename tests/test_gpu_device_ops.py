@@ -1,0 +1,214 @@
+"""Device forms of crc32c_series / combine_series / trim and single-buffer
+crc32c_extend, plus the drop-in device dispatch.
+
+Parity: the reference's own outputs (tests/golden/ref_vectors.json, produced by
+oracle/ref from crc.cpp) where they exist, else the pinned oracle. Bit-exact."""
+import random
+
+import numpy as np
+import pytest
+
+from photonlibos_amd import checksum as ck
+from photonlibos_amd import datagen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    assert ck.device_count() >= 1
+    return torch
+
+
+@pytest.fixture(autouse=True)
+def _dispatch_off():
+    yield
+    ck.set_device_dispatch(False)
+
+
+def to_dev(torch, arr):
+    return torch.from_numpy(np.array(arr, copy=True)).cuda()
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def dev_u32(torch, values):
+    return to_dev(torch, np.asarray(values, np.uint32).view(np.int32))
+
+
+def test_series_device_reference_vectors(torch_dev, ref_vectors):
+    torch = torch_dev
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDA000, 1 << 20)
+    dbuf = to_dev(torch, np.frombuffer(buf, np.uint8))
+    pos = 0
+    for i, (ps, npart) in enumerate(zip(rv["series_part"], rv["series_n"])):
+        hw = rv["series_hw"][pos:pos + npart]
+        sw = rv["series_sw"][pos:pos + npart]
+        pos += npart
+        out = torch.full((npart,), -1, dtype=torch.int32, device="cuda")
+        ck.series_device(dbuf, ps, npart, out)
+        torch.cuda.synchronize()
+        # crc32c_series_auto is the SSE4.2 engine on every x86 host: its
+        # results (incl. zeros for parts < 8 B, crc.cpp:481-500) are the target.
+        assert list(u32(out)) == hw, ps
+        res = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ck.combine_series_device(dev_u32(torch, sw), ps, npart, res)
+        torch.cuda.synchronize()
+        assert int(u32(res)[0]) == rv["cseries_hw"][i] == rv["cseries_sw"][i]
+
+
+def test_series_device_empty_and_large(torch_dev, oracle):
+    torch = torch_dev
+    out = torch.full((4,), 7, dtype=torch.int32, device="cuda")
+    ck.series_device(0, 4096, 0, out)  # n_parts == 0: nothing written
+    torch.cuda.synchronize()
+    assert list(u32(out)) == [7] * 4
+    # 256 parts x 64 KiB (the C2 shape's contiguous form), checked per part.
+    ps, n = 65536, 256
+    dbuf = torch.empty(ps * n, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, ps * n, ps * n, 1, 0x5EED0100)
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ck.series_device(dbuf, ps, n, out)
+    torch.cuda.synchronize()
+    host = dbuf.cpu().numpy()
+    got = u32(out)
+    for i in range(0, n, 17):
+        assert int(got[i]) == oracle.crc32c(host[i * ps:(i + 1) * ps])
+    res = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.combine_series_device(out, ps, n, res)
+    torch.cuda.synchronize()
+    assert int(u32(res)[0]) == oracle.crc32c(host)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 15, 16, 17, 1000, 65537])
+@pytest.mark.parametrize("part", [0, 1, 7, 4096, 65536, 0xFFFFFFFF])
+def test_combine_series_device(torch_dev, oracle, n, part):
+    torch = torch_dev
+    rng = random.Random(n * 131 + part)
+    crcs = [rng.getrandbits(32) for _ in range(n)]
+    if n > 3 and part == 0:
+        crcs[0] = crcs[1] = 0  # first-non-zero rule when part_size == 0
+    if n > 40:
+        crcs[5:40] = [0] * 35  # zero entries take the crc1 == 0 shortcut
+    expect = oracle.combine_series(crcs, part) if n <= 1000 else None
+    res = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    ck.combine_series_device(dev_u32(torch, crcs) if n else 0, part, n, res)
+    torch.cuda.synchronize()
+    got = int(u32(res)[0])
+    if expect is None:
+        expect = ck.crc32c_combine_series(crcs, part)  # drop-in host engine for the big case
+        assert oracle.combine_series(crcs[:1000], part) == ck.crc32c_combine_series(crcs[:1000], part)
+    assert got == expect
+
+
+def test_trim_batch_reference_vectors(torch_dev, oracle, ref_vectors):
+    torch = torch_dev
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDB000, 5100)
+    x = rv["trim_all"][0]
+    m = len(rv["trim_l1"])
+    all_ = np.zeros((m, 2), np.uint32)
+    pre = np.zeros((m, 2), np.uint32)
+    suf = np.zeros((m, 2), np.uint32)
+    for i, (l1, l3) in enumerate(zip(rv["trim_l1"], rv["trim_l3"])):
+        all_[i] = (x, 5100)
+        pre[i] = (oracle.crc32c(buf[:l1]), l1)
+        suf[i] = (oracle.crc32c(buf[5100 - l3:]) if l3 else 0, l3)
+    out = torch.zeros(m, dtype=torch.int32, device="cuda")
+    nerr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.trim_batch(dev_u32(torch, all_), dev_u32(torch, pre), dev_u32(torch, suf), m, out, nerr)
+    torch.cuda.synchronize()
+    assert list(u32(out)) == rv["trim_hw"] == rv["trim_sw"]
+    assert int(nerr.item()) == 0
+
+
+def test_trim_batch_edge_cases(torch_dev, oracle):
+    torch = torch_dev
+    rng = random.Random(5)
+    cases = [
+        ((123, 10), (1, 6), (2, 6)),               # EINVAL: 0 and counted
+        ((5, 0x80000000), (1, 0x80000000), (2, 0x80000000)),  # 32-bit size sum wraps (crc.cpp:444)
+        ((0xDEAD, 100), (0xBEEF, 100), (0, 0)),    # all.size == prefix.size: combine's len2 == 0 shortcut
+        ((0xDEAD, 100), (0, 40), (0x1234, 60)),    # prefix.crc == 0 shortcut
+        ((0xDEAD, 100), (0, 0), (0, 0)),           # nothing to trim
+    ]
+    for _ in range(200):
+        a = rng.getrandbits(32), rng.randrange(0, 1 << 32)
+        p = rng.getrandbits(32), rng.randrange(0, a[1] + 1)
+        s = rng.getrandbits(32), rng.randrange(0, a[1] - p[1] + 1)
+        cases.append((a, p, s))
+    arr = [np.asarray([c[k] for c in cases], np.uint32) for k in range(3)]
+    out = torch.zeros(len(cases), dtype=torch.int32, device="cuda")
+    nerr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.trim_batch(*(dev_u32(torch, a) for a in arr), len(cases), out, nerr)
+    torch.cuda.synchronize()
+    got = u32(out)
+    for i, (a, p, s) in enumerate(cases):
+        assert int(got[i]) == oracle.trim(a, p, s), (a, p, s)
+    assert int(nerr.item()) == 1
+
+
+@pytest.mark.parametrize("nbytes", [0, 1, 63, 4096, 16384, 16385, 65536 + 3, 1 << 20, (7 << 20) + 13])
+@pytest.mark.parametrize("off", [0, 5])
+def test_extend_device(torch_dev, oracle, nbytes, off):
+    torch = torch_dev
+    dbuf = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, nbytes + 64, nbytes + 64, 1, 0x5EED0200 + nbytes)
+    host = dbuf.cpu().numpy()[off:off + nbytes]
+    for seed in (0, 0x9E3779B9):
+        out = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ck.extend_device(dbuf.data_ptr() + off, nbytes, seed, out)
+        torch.cuda.synchronize()
+        assert int(u32(out)[0]) == oracle.crc32c(host, seed), (nbytes, off, seed)
+
+
+def test_extend_device_1gib(torch_dev):
+    # Size-independent check at scale: one 1 GiB buffer == combine of its
+    # 64 KiB series (both on the device, different kernels and splits).
+    torch = torch_dev
+    n = 1 << 30
+    dbuf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, n, n, 1, 0x5EED0300)
+    one = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.extend_device(dbuf, n, 0x1234567, one)
+    parts = torch.zeros(n >> 16, dtype=torch.int32, device="cuda")
+    ck.series_device(dbuf, 65536, n >> 16, parts)
+    folded = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.combine_series_device(parts, 65536, n >> 16, folded)
+    torch.cuda.synchronize()
+    # crc32c_extend(d, n, s) == crc32c_combine(s, crc32c(d, n), n)
+    assert int(u32(one)[0]) == ck.crc32c_combine(0x1234567, int(u32(folded)[0]), n)
+
+
+def test_device_dispatch_dropin(torch_dev, oracle):
+    torch = torch_dev
+    n = (3 << 20) + 7
+    dbuf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, n, n, 1, 0x5EED0400)
+    torch.cuda.synchronize()
+    host = dbuf.cpu().numpy()
+    expect = oracle.crc32c(host, 77)
+    hbuf = np.ascontiguousarray(host)
+    ck.set_device_dispatch(True)
+    # device pointer -> device engine; host pointer -> host engine (same pointer variable)
+    assert ck.crc32c_extend_at(dbuf.data_ptr(), n, 77) == expect
+    assert ck.crc32c_extend_at(hbuf.ctypes.data, n, 77) == expect
+    assert ck.crc32c_extend(b"123456789", 0) == 0x58E3FA20
+    # series: device buffer, host output array and device output array
+    ps, np_ = 4096, n // 4096
+    out_h = np.zeros(np_, np.uint32)
+    ck.crc32c_series_at(dbuf.data_ptr(), ps, np_, out_h.ctypes.data)
+    exp_parts = oracle.series(host, ps, np_, hw_quirk=True)
+    assert list(out_h) == exp_parts
+    out_d = torch.zeros(np_, dtype=torch.int32, device="cuda")
+    ck.crc32c_series_at(dbuf.data_ptr(), ps, np_, out_d.data_ptr())
+    assert list(u32(out_d)) == exp_parts
+    # combine_series on a device array
+    assert ck.crc32c_combine_series_at(out_d.data_ptr(), ps, np_) == oracle.crc32c(host[:ps * np_])
+    ck.set_device_dispatch(False)
+    assert ck.crc32c_extend_at(hbuf.ctypes.data, n, 77) == expect
