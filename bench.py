@@ -55,6 +55,7 @@ def parse(argv=None):
                     help="untimed steps; the first ~10 back-to-back launches run slower while clocks settle")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--h2d", action="store_true", help="host-memory end-to-end rate (for DESIGN.md)")
+    ap.add_argument("--rpc-batch", action="store_true", help="CheckedMessage batch over pinned host payloads (DESIGN.md)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -242,6 +243,58 @@ def run_h2d(args, stream):
                       "config": {"workload": cfg["workload"].replace("device-resident", "pinned host memory")}}))
 
 
+def run_rpc_batch(args, stream):
+    """§8(f) row 1: CheckedMessage validation batched over RPC payloads held in
+    pinned host memory (the pinned IOAlloc pool), C5 shape: 65536 messages x 8
+    non-contiguous 8 KiB segments. One step = submit + wait of the whole batch
+    (descriptors H2D, kernels reading the payload in place over the host link,
+    verdicts D2H). Reported in DESIGN.md, never as `value`."""
+    from photonlibos_amd.checked import MessageBatch, PinnedAlloc
+    cfg = CONFIGS["c5"]
+    n, cnt, nseg = cfg["nbytes"], cfg["count"], cfg["nseg"]
+    slots = cnt * nseg
+    alloc = PinnedAlloc()
+    region = 64 << 20  # receive-buffer regions from the IOAlloc pool
+    per_region = region // n
+    regions = [alloc.alloc(region) for _ in range((slots + per_region - 1) // per_region)]
+    for r, a in enumerate(regions):
+        ck.fill_splitmix(a, n, n, per_region, shard_seed_base(0, slots) + r * per_region, stream=stream)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(0x5EED0005)
+    perm = rng.permutation(slots)
+    addr = [regions[p // per_region] + (p % per_region) * n for p in perm.tolist()]
+    batch = MessageBatch(cnt, slots)
+    t0 = time.perf_counter()
+    for m in range(cnt):
+        batch.add([(addr[m * nseg + j], n) for j in range(nseg)])
+    add_s = time.perf_counter() - t0
+    batch.submit(stream.cuda_stream)
+    batch.wait()
+    check = []
+    for m in (0, cnt - 1):
+        acc = 0
+        for j in range(nseg):
+            acc = ck.crc32c_extend(PinnedAlloc.view(addr[m * nseg + j], n).tobytes(), acc)
+        check.append(acc == batch.result(m)[1])
+
+    def step():
+        batch.submit(stream.cuda_stream)
+        batch.wait()
+
+    steps = max(2, min(args.steps, 10))
+    elapsed, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
+    nbytes = n * slots
+    print(json.dumps({"metric": "GiB/s CRC32C CheckedMessage batch validation, payload in pinned host memory "
+                                "(descriptors H2D + zero-copy kernels + verdicts D2H)",
+                      "value": round(nbytes * steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
+                      "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 3),
+                      "add_us_per_message_python": round(add_s / cnt * 1e6, 2), "self_check": all(check),
+                      "config": {"workload": cfg["workload"] + ", pinned host memory (IOAlloc pool)"}}))
+    batch.close()
+    for a in regions:
+        alloc.dealloc(a)
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -257,6 +310,10 @@ def main():
     if args.h2d:
         if rank == 0:
             run_h2d(args, stream)
+        return
+    if args.rpc_batch:
+        if rank == 0:
+            run_rpc_batch(args, stream)
         return
     cfg = CONFIGS[args.config]
     wl = Workload(cfg, rank, stream)

@@ -89,6 +89,12 @@ int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint3
 int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
                             uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
                             void* stream);
+/* As photon_crc32c_batch_msg, with the total segment count nseg
+ * (== d_msg_start[nmsg]) supplied by the caller: fully asynchronous
+ * (photon_crc32c_batch_msg reads it back from the device and waits). */
+int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                              uint64_t nseg, uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out,
+                              uint32_t* d_out, void* stream);
 
 /* d_out[i] = crc32c_combine(d_crc1[i], d_crc2[i], d_len2[i]) with the
  * reference's shortcuts (crc1 == 0 -> crc2, len2 == 0 -> crc1). */

@@ -13,6 +13,11 @@ class NativeLibraryMissing(ImportError):
     pass
 
 
+class PhotonRange(ctypes.Structure):
+    """photon_crc_range == IOAlloc::RangeSize {int min, max;} (common/io-alloc.h:33)."""
+    _fields_ = [("min", ctypes.c_int), ("max", ctypes.c_int)]
+
+
 def lib():
     """The loaded libphoton_checksum.so (built by __graft_entry__.build())."""
     global _lib
@@ -55,6 +60,20 @@ def _declare(L):
     fn("photon_crc32c_trim_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp, vp)
     fn("photon_crc32c_extend_device", ctypes.c_int, vp, u64, u32, vp, vp)
     fn("photon_crc_set_device_dispatch", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc32c_batch_msg_n", ctypes.c_int, vp, vp, u64, u64, u32, vp, vp, vp, vp)
+    # include/photon_crc/checked_batch.h
+    fn("photon_crc_pinned_allocate", ctypes.c_int, vp, PhotonRange, ctypes.POINTER(vp))
+    fn("photon_crc_pinned_deallocate", ctypes.c_int, vp, vp)
+    fn("photon_crc_pinned_stats", ctypes.c_int, ctypes.POINTER(u64), ctypes.POINTER(u64))
+    fn("photon_crc_pinned_release", ctypes.c_int64)
+    fn("photon_crc_msg_batch_create", vp, u32, u32, u32)
+    fn("photon_crc_msg_batch_destroy", None, vp)
+    fn("photon_crc_msg_batch_add", ctypes.c_int64, vp, vp, u32, vp, u64, u32)
+    fn("photon_crc_msg_batch_submit", ctypes.c_int, vp, vp, vp, vp)
+    fn("photon_crc_msg_batch_wait", ctypes.c_int64, vp)
+    fn("photon_crc_msg_batch_result", ctypes.c_int, vp, u64, ctypes.POINTER(u32))
+    fn("photon_crc_msg_batch_count", u64, vp)
+    fn("photon_crc_msg_batch_reset", ctypes.c_int, vp)
 
     # Drop-in host entry points (include/photon/common/checksum/crc32c.h),
     # C++ linkage: bound by their mangled names.

@@ -1,0 +1,371 @@
+// checked_batch.cpp -- pinned IOAlloc pool + batched CheckedMessage checksums
+// (include/photon_crc/checked_batch.h).
+//
+// Reference behaviour mirrored:
+//   IOAlloc::allocate / deallocate callbacks   common/io-alloc.h:31-85
+//   Crc32Hasher::extend_hash                   rpc/serialize.h:239-252
+//   CheckedMessage::validate_checksum          rpc/serialize.h:266-275
+// The checksums themselves are computed by photon_crc32c_batch_msg_n (HIP).
+#include <photon_crc/checked_batch.h>
+
+#include <errno.h>
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "internal.h"
+
+namespace {
+
+using pcrc::report_error;
+using pcrc::report_hip_error;
+
+// ------------------------------------------------------------------ pool
+constexpr int kMinClass = 12;               // 4 KiB blocks
+constexpr int kMaxClass = 26;               // 64 MiB blocks
+constexpr size_t kSlabBytes = 64ull << 20;  // pinned in 64 MiB slabs
+
+struct Slab {
+    size_t size;
+    int cls;        // block class, -1 for a dedicated (oversized) slab
+    uint32_t used;  // blocks handed out
+};
+
+struct Pool {
+    std::mutex mu;
+    std::map<uintptr_t, Slab> slabs;            // keyed by base address
+    std::vector<void*> free_[kMaxClass + 1];
+    std::unordered_map<uintptr_t, uintptr_t> live;  // block -> slab base
+    uint64_t pinned = 0, in_use = 0;
+
+    // Slab containing [p, p+n), or slabs.end().
+    std::map<uintptr_t, Slab>::iterator find(uintptr_t p, uint64_t n) {
+        auto it = slabs.upper_bound(p);
+        if (it == slabs.begin()) return slabs.end();
+        --it;
+        if (p + n > it->first + it->second.size || p + n < p) return slabs.end();
+        return it;
+    }
+};
+
+Pool& pool() {
+    static Pool* p = new Pool;  // never destroyed: callbacks may run at exit
+    return *p;
+}
+
+int size_class(uint64_t n) {
+    int c = kMinClass;
+    while ((1ull << c) < n) ++c;
+    return c;
+}
+
+void* pin(size_t bytes) {
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable);
+    if (e != hipSuccess) {
+        report_hip_error(e, "hipHostMalloc");
+        return nullptr;
+    }
+    return p;
+}
+
+// Is [p, p+n) memory the kernels may read? Returns the device address of p
+// (same as p for hipHostMalloc'd and device memory), or nullptr.
+const void* device_address(const void* p, uint64_t n) {
+    {
+        Pool& P = pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (P.find(reinterpret_cast<uintptr_t>(p), n) != P.slabs.end()) return p;
+    }
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return p;
+    if (a.type == hipMemoryTypeHost && a.devicePointer && a.hostPointer)
+        return static_cast<const char*>(a.devicePointer) + (static_cast<const char*>(p) -
+                                                             static_cast<const char*>(a.hostPointer));
+    return nullptr;
+}
+
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+// ----------------------------------------------------------- batch object
+struct photon_crc_msg_batch {
+    int dev = 0;
+    uint32_t flags = 0;
+    uint32_t max_msg = 0, max_seg = 0;
+    // pinned host staging
+    photon_crc_iovec* h_iov = nullptr;
+    uint64_t* h_start = nullptr;
+    uint32_t* h_expect = nullptr;
+    uint32_t* h_out = nullptr;
+    // device side
+    photon_crc_iovec* d_iov = nullptr;
+    uint64_t* d_start = nullptr;
+    uint32_t* d_seg = nullptr;
+    uint32_t* d_out = nullptr;
+    hipEvent_t done_ev = nullptr;
+    uint64_t nmsg = 0, nseg = 0;
+    bool submitted = false, completed = false;
+    int64_t mismatches = 0;
+};
+
+namespace {
+
+void free_batch(photon_crc_msg_batch* b) {
+    if (b->done_ev) (void)hipEventDestroy(b->done_ev);
+    for (void* p : {(void*)b->h_iov, (void*)b->h_start, (void*)b->h_expect, (void*)b->h_out})
+        if (p) (void)hipHostFree(p);
+    for (void* p : {(void*)b->d_iov, (void*)b->d_start, (void*)b->d_seg, (void*)b->d_out})
+        if (p) (void)hipFree(p);
+    delete b;
+}
+
+// Results are on the host: count mismatches once.
+int64_t finish(photon_crc_msg_batch* b) {
+    if (!b->completed) {
+        hipError_t e = hipEventSynchronize(b->done_ev);
+        if (e != hipSuccess) return report_hip_error(e, "hipEventSynchronize");
+        int64_t bad = 0;
+        for (uint64_t i = 0; i < b->nmsg; ++i) bad += b->h_out[i] != b->h_expect[i];
+        b->mismatches = bad;
+        b->completed = true;
+    }
+    return b->mismatches;
+}
+
+}  // namespace
+
+extern "C" {
+
+int photon_crc_pinned_allocate(void*, photon_crc_range size, void** ptr) {
+    if (!ptr || size.min <= 0 || size.max < size.min) return report_error(-EINVAL, "bad IOAlloc range");
+    Pool& P = pool();
+    const uint64_t n = (uint64_t)size.max;
+    const int cls = size_class(n);
+    std::lock_guard<std::mutex> lk(P.mu);
+    void* blk = nullptr;
+    uintptr_t slab_base = 0;
+    if (cls > kMaxClass) {
+        blk = pin(n);
+        if (!blk) return -ENOMEM;
+        slab_base = reinterpret_cast<uintptr_t>(blk);
+        P.slabs[slab_base] = Slab{n, -1, 0};
+        P.pinned += n;
+    } else {
+        auto& fl = P.free_[cls];
+        if (fl.empty()) {
+            char* s = static_cast<char*>(pin(kSlabBytes));
+            if (!s) return -ENOMEM;
+            P.slabs[reinterpret_cast<uintptr_t>(s)] = Slab{kSlabBytes, cls, 0};
+            P.pinned += kSlabBytes;
+            for (size_t off = kSlabBytes; off >= (1ull << cls); off -= 1ull << cls) fl.push_back(s + off - (1ull << cls));
+        }
+        blk = fl.back();
+        fl.pop_back();
+        slab_base = P.find(reinterpret_cast<uintptr_t>(blk), 1)->first;
+    }
+    P.slabs[slab_base].used++;
+    P.live[reinterpret_cast<uintptr_t>(blk)] = slab_base;
+    P.in_use += cls > kMaxClass ? n : (1ull << cls);
+    *ptr = blk;
+    return size.max;
+}
+
+int photon_crc_pinned_deallocate(void*, void* ptr) {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.live.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == P.live.end()) return report_error(-EINVAL, "pointer not from photon_crc_pinned_allocate");
+    Slab& s = P.slabs[it->second];
+    s.used--;
+    if (s.cls < 0) {
+        P.in_use -= s.size;
+    } else {
+        P.in_use -= 1ull << s.cls;
+        P.free_[s.cls].push_back(ptr);
+    }
+    P.live.erase(it);
+    return 0;
+}
+
+int photon_crc_pinned_stats(uint64_t* slab_bytes, uint64_t* in_use_bytes) {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (slab_bytes) *slab_bytes = P.pinned;
+    if (in_use_bytes) *in_use_bytes = P.in_use;
+    return 0;
+}
+
+int64_t photon_crc_pinned_release(void) {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    int64_t released = 0;
+    for (auto it = P.slabs.begin(); it != P.slabs.end();) {
+        if (it->second.used) {
+            ++it;
+            continue;
+        }
+        const uintptr_t lo = it->first, hi = lo + it->second.size;
+        if (it->second.cls >= 0) {
+            auto& fl = P.free_[it->second.cls];
+            std::vector<void*> keep;
+            keep.reserve(fl.size());
+            for (void* p : fl)
+                if (reinterpret_cast<uintptr_t>(p) < lo || reinterpret_cast<uintptr_t>(p) >= hi) keep.push_back(p);
+            fl.swap(keep);
+        }
+        (void)hipHostFree(reinterpret_cast<void*>(lo));
+        P.pinned -= it->second.size;
+        released += (int64_t)it->second.size;
+        it = P.slabs.erase(it);
+    }
+    return released;
+}
+
+photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_t max_segments, uint32_t flags) {
+    if (!max_messages || !max_segments) {
+        report_error(-EINVAL, "empty batch capacity");
+        return nullptr;
+    }
+    if (photon_crc_device_count() <= 0) return nullptr;  // error text set by the probe
+    auto* b = new photon_crc_msg_batch;
+    b->flags = flags;
+    b->max_msg = max_messages;
+    b->max_seg = max_segments;
+    hipError_t e = hipGetDevice(&b->dev);
+    const uint64_t M = max_messages, S = max_segments;
+    auto hm = [&](void** p, uint64_t n) {
+        if (e == hipSuccess) e = hipHostMalloc(p, n, hipHostMallocPortable);
+    };
+    auto dm = [&](void** p, uint64_t n) {
+        if (e == hipSuccess) e = hipMalloc(p, n);
+    };
+    hm((void**)&b->h_iov, S * sizeof(photon_crc_iovec));
+    hm((void**)&b->h_start, (M + 1) * 8);
+    hm((void**)&b->h_expect, M * 4);
+    hm((void**)&b->h_out, M * 4);
+    dm((void**)&b->d_iov, S * sizeof(photon_crc_iovec));
+    dm((void**)&b->d_start, (M + 1) * 8);
+    dm((void**)&b->d_seg, S * 4);
+    dm((void**)&b->d_out, M * 4);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        report_hip_error(e, "photon_crc_msg_batch_create");
+        free_batch(b);
+        return nullptr;
+    }
+    b->h_start[0] = 0;
+    return b;
+}
+
+void photon_crc_msg_batch_destroy(photon_crc_msg_batch* b) {
+    if (!b) return;
+    if (b->submitted && !b->completed) (void)hipEventSynchronize(b->done_ev);
+    free_batch(b);
+}
+
+int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec* iov, uint32_t iovcnt,
+                                 const void* body, uint64_t body_length, uint32_t expected) {
+    if (!b || (iovcnt && !iov)) return report_error(-EINVAL, "null batch or iovector");
+    if (b->submitted) return report_error(-EBUSY, "batch already submitted; reset it first");
+    const bool has_body = body && body_length;  // serialize.h:271
+    if (b->nmsg >= b->max_msg || b->nseg + iovcnt + (has_body ? 1 : 0) > b->max_seg)
+        return report_error(-ENOSPC, "batch is full");
+    const bool trusted = b->flags & PHOTON_CRC_BATCH_TRUSTED;
+    uint64_t s = b->nseg;
+    auto put = [&](const void* p, uint64_t n) -> int {
+        if (!n) return 0;  // crc32c_extend over 0 bytes is the identity
+        const void* d = trusted ? p : device_address(p, n);
+        if (!d) return report_error(-EFAULT, "segment is not device-accessible (pin it: photon_crc_pinned_allocate)");
+        b->h_iov[s++] = photon_crc_iovec{d, n};
+        return 0;
+    };
+    for (uint32_t k = 0; k < iovcnt; ++k)
+        if (int rc = put(iov[k].base, iov[k].len)) return rc;
+    if (has_body)
+        if (int rc = put(body, body_length)) return rc;
+    b->nseg = s;
+    b->h_expect[b->nmsg] = expected;
+    b->h_start[++b->nmsg] = s;
+    return (int64_t)(b->nmsg - 1);
+}
+
+int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*done)(void* arg), void* arg) {
+    if (!b) return report_error(-EINVAL, "null batch");
+    if (b->submitted && !b->completed) return report_error(-EBUSY, "batch still running");
+    DeviceScope scope(b->dev);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e = hipSuccess;
+    int rc = 0;
+    if (b->nmsg) {
+        if (b->nseg) e = hipMemcpyAsync(b->d_iov, b->h_iov, b->nseg * sizeof(photon_crc_iovec), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(b->d_start, b->h_start, (b->nmsg + 1) * 8, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return report_hip_error(e, "hipMemcpyAsync(descriptors)");
+        rc = photon_crc32c_batch_msg_n(b->d_iov, b->d_start, b->nmsg, b->nseg, 0, nullptr, b->d_seg, b->d_out,
+                                       stream);
+        if (rc) return rc;
+        e = hipMemcpyAsync(b->h_out, b->d_out, b->nmsg * 4, hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) return report_hip_error(e, "hipMemcpyAsync(results)");
+    }
+    e = hipEventRecord(b->done_ev, st);
+    if (e == hipSuccess && done) e = hipLaunchHostFunc(st, done, arg);
+    if (e != hipSuccess) return report_hip_error(e, "completion");
+    b->submitted = true;
+    b->completed = false;
+    return 0;
+}
+
+int64_t photon_crc_msg_batch_wait(photon_crc_msg_batch* b) {
+    if (!b) return report_error(-EINVAL, "null batch");
+    if (!b->submitted) return report_error(-EINVAL, "batch not submitted");
+    return finish(b);
+}
+
+int photon_crc_msg_batch_result(photon_crc_msg_batch* b, uint64_t i, uint32_t* crc) {
+    if (!b || i >= b->nmsg) return report_error(-EINVAL, "bad batch or index");
+    if (!b->submitted) return report_error(-EBUSY, "batch not submitted");
+    if (!b->completed) {
+        hipError_t e = hipEventQuery(b->done_ev);
+        if (e == hipErrorNotReady) return report_error(-EBUSY, "batch still running");
+        if (e != hipSuccess) return report_hip_error(e, "hipEventQuery");
+        int64_t rc = finish(b);
+        if (rc < 0) return (int)rc;
+    }
+    if (crc) *crc = b->h_out[i];
+    return b->h_out[i] == b->h_expect[i] ? 1 : 0;
+}
+
+uint64_t photon_crc_msg_batch_count(const photon_crc_msg_batch* b) { return b ? b->nmsg : 0; }
+
+int photon_crc_msg_batch_reset(photon_crc_msg_batch* b) {
+    if (!b) return report_error(-EINVAL, "null batch");
+    if (b->submitted && !b->completed) {
+        int64_t rc = finish(b);
+        if (rc < 0) return (int)rc;
+    }
+    b->nmsg = b->nseg = 0;
+    b->submitted = b->completed = false;
+    b->mismatches = 0;
+    return 0;
+}
+
+}  // extern "C"

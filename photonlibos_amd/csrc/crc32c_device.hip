@@ -45,6 +45,7 @@
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "crc32c_kernels.h"
 #include "gf2.h"
+#include "internal.h"
 
 namespace pcrc {
 
@@ -350,6 +351,10 @@ int pipe_for(int dev, HostPipe** out) {
 }
 
 }  // namespace
+
+// For the other translation units of the library (internal.h).
+int report_error(int code, const char* what) { return fail(code, what); }
+int report_hip_error(hipError_t e, const char* what) { return hip_fail(e, what); }
 }  // namespace pcrc
 
 using namespace pcrc;
@@ -494,6 +499,16 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(msg_start)");
     e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    return photon_crc32c_batch_msg_n(d_iov, d_msg_start, nmsg, nseg, seed0, d_seeds, d_seg_out, d_out, stream);
+}
+
+int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                              uint64_t nseg, uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out,
+                              uint32_t* d_out, void* stream) {
+    if (!nmsg) return 0;
+    if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e;
     BatchArgs a{};
     a.iov = d_iov;
     a.count = nseg;

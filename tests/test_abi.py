@@ -19,7 +19,8 @@ def _exported():
 
 
 def _c_abi_functions():
-    txt = open(os.path.join(REPO, "include", "photon_crc", "crc32c_gpu.h")).read()
+    d = os.path.join(REPO, "include", "photon_crc")
+    txt = "".join(open(os.path.join(d, h)).read() for h in sorted(os.listdir(d)) if h.endswith(".h"))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(photon_crc\w*)\s*\(", txt)))
 
@@ -83,3 +84,14 @@ def test_argument_validation():
     assert e.value.code == -22
     with pytest.raises(ck.CrcError):
         ck.batch_strided(None, 4096, 4096, 4, None)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
+def test_checked_batch_fails_loudly_without_gpu():
+    from photonlibos_amd.checked import MessageBatch, PinnedAlloc
+    with pytest.raises(ck.CrcError):
+        MessageBatch(16, 16)
+    with pytest.raises(ck.CrcError):
+        PinnedAlloc().alloc(4096)
+    with pytest.raises(ck.CrcError):  # IOAlloc contract: min > 0, max >= min
+        PinnedAlloc().alloc(0)

@@ -46,3 +46,12 @@ def test_cpp_gpu_batch_example():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_rpc_batch_example():
+    exe = os.path.join(BIN, "rpc_batch_example")
+    assert os.path.exists(exe)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 wrong verdicts" in r.stdout

@@ -1,0 +1,143 @@
+"""Batched CheckedMessage validation over pinned RPC payloads (SURVEY.md §8(f)
+row 1): results equal Crc32Hasher::extend_hash over payload segments then the
+message struct (rpc/serialize.h:244-275), checked against the pinned oracle's
+chained crc32c_extend. Bit-exact."""
+import random
+
+import numpy as np
+import pytest
+
+from photonlibos_amd import checksum as ck
+from photonlibos_amd.checked import MessageBatch, PinnedAlloc, TRUSTED
+from photonlibos_amd.checksum import CrcError
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available()
+    assert ck.device_count() >= 1
+    return torch
+
+
+def _messages(alloc, rng, nmsg, max_seg, seglen_max, struct_len=48):
+    """Received messages laid out like a socket readv into pinned buffers:
+    payload segments (ragged lengths, odd offsets) + a trailing struct."""
+    msgs = []
+    blocks = []
+    for _ in range(nmsg):
+        nseg = rng.randrange(0, max_seg + 1)
+        segs = []
+        for _ in range(nseg):
+            ln = rng.choice([0, 1, 7, 64, 4095, 8192, rng.randrange(1, seglen_max + 1)])
+            off = rng.randrange(0, 16)
+            addr = alloc.alloc(ln + off + 1)
+            blocks.append(addr)
+            v = alloc.view(addr, ln + off + 1)
+            v[:] = np.frombuffer(rng.randbytes(ln + off + 1), np.uint8)
+            segs.append((addr + off, ln))
+        saddr = alloc.alloc(struct_len)
+        blocks.append(saddr)
+        sv = alloc.view(saddr, struct_len)
+        sv[:] = np.frombuffer(rng.randbytes(struct_len), np.uint8)
+        sv[-4:] = 0  # m_checksum zeroed, as validate_checksum does (serialize.h:268)
+        msgs.append((segs, (saddr, struct_len)))
+    return msgs, blocks
+
+
+def _expected(alloc, oracle, segs, body):
+    data = [bytes(alloc.view(a, n)) for a, n in segs if n] + [bytes(alloc.view(*body))]
+    return oracle.extend_chain(data, 0)
+
+
+def test_validate_batch_matches_oracle(torch_dev, oracle):
+    rng = random.Random(11)
+    alloc = PinnedAlloc()
+    msgs, blocks = _messages(alloc, rng, 300, 9, 20000)
+    b = MessageBatch(512, 4096)
+    exp = [_expected(alloc, oracle, s, body) for s, body in msgs]
+    bad = set(rng.sample(range(len(msgs)), 17))
+    for i, (segs, body) in enumerate(msgs):
+        claimed = exp[i] ^ (1 << rng.randrange(32)) if i in bad else exp[i]
+        assert b.add(segs, body, claimed) == i
+    b.submit()
+    assert b.wait() == len(bad)
+    for i in range(len(msgs)):
+        valid, crc = b.result(i)
+        assert crc == exp[i]
+        assert valid == (i not in bad)
+    # reuse after reset; send side (add_checksum): expected 0, read the value
+    b.reset()
+    for segs, body in msgs[:50]:
+        b.add(segs, body)
+    b.submit()
+    b.wait()
+    assert [b.result(i)[1] for i in range(50)] == exp[:50]
+    b.close()
+    for a in blocks:
+        alloc.dealloc(a)
+    slab, used = alloc.stats()
+    assert used == 0 and slab > 0
+    assert alloc.release() == slab
+
+
+def test_payload_corruption_detected(torch_dev, oracle):
+    rng = random.Random(12)
+    alloc = PinnedAlloc()
+    msgs, blocks = _messages(alloc, rng, 64, 8, 8192)
+    exp = [_expected(alloc, oracle, s, body) for s, body in msgs]
+    # flip one payload bit in every odd message after computing its checksum
+    for i, (segs, body) in enumerate(msgs):
+        if i % 2:
+            a, n = body if not any(n for _, n in segs) else next((a, n) for a, n in segs if n)
+            v = alloc.view(a, n)
+            v[rng.randrange(n)] ^= 1 << rng.randrange(8)
+    b = MessageBatch(64, 1024)
+    for i, (segs, body) in enumerate(msgs):
+        b.add(segs, body, exp[i])
+    b.submit()
+    assert b.wait() == 32
+    assert [b.result(i)[0] for i in range(64)] == [i % 2 == 0 for i in range(64)]
+    b.close()
+    for a in blocks:
+        alloc.dealloc(a)
+
+
+def test_device_and_foreign_memory(torch_dev, oracle):
+    torch = torch_dev
+    # device memory is accepted; ordinary (pageable) host memory is refused loudly
+    d = torch.randint(0, 256, (10000,), dtype=torch.uint8, device="cuda")
+    host = d.cpu().numpy()
+    b = MessageBatch(4, 16)
+    b.add([(d.data_ptr(), 10000)], None, oracle.crc32c(host))
+    pageable = np.zeros(4096, np.uint8)
+    with pytest.raises(CrcError) as e:
+        b.add([(pageable.ctypes.data, 4096)])
+    assert e.value.code == -14  # EFAULT
+    b.submit()
+    assert b.wait() == 0
+    assert b.result(0) == (True, oracle.crc32c(host))
+    with pytest.raises(CrcError):
+        b.add([(d.data_ptr(), 1)])  # EBUSY until reset
+    b.close()
+
+
+def test_capacity_and_empty(torch_dev):
+    b = MessageBatch(2, 2, TRUSTED)
+    b.submit()
+    assert b.wait() == 0  # empty batch completes
+    b.reset()
+    alloc = PinnedAlloc()
+    a = alloc.alloc(64)
+    b.add([(a, 8), (a + 8, 8)])
+    with pytest.raises(CrcError) as e:
+        b.add([(a, 8)])
+    assert e.value.code == -28  # ENOSPC
+    b.add([], None, 0)  # an empty message: checksum 0 == init_value()
+    b.submit()
+    b.wait()
+    assert b.result(1) == (True, 0)
+    b.close()
+    alloc.dealloc(a)
