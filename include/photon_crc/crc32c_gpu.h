@@ -155,10 +155,20 @@ int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64
 int photon_crc_set_lanes_per_buffer(int g);
 
 /* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
- * lane run B, rows per step U and steps in flight D, one of (1,4,3) (default),
- * (2,2,3), (2,2,4), (1,2,4), (4,1,3), (4,1,4). run_blocks = 0 disables the
- * streaming kernel (generic kernel for every batch). */
+ * lane run B, rows per step U and steps in flight D, one of (1,4,3), (2,2,3),
+ * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4).
+ * The streaming kernel is OFF by default (the generic kernel is faster with
+ * the current tables); run_blocks = 0 turns it off again. */
 int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
+
+/* Rows per step of the generic batch kernel (testing / tuning): 2, 4
+ * (default) or 8. */
+int photon_crc_set_generic_rows(int rows_per_step);
+
+/* The CRC-64 streaming kernel's shape: rows per step U and steps in flight D,
+ * one of (8,1) (default), (4,2), (4,3), (2,4); U = 0 turns it off (generic
+ * kernel for every CRC-64 batch). */
+int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
 
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed

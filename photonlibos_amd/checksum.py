@@ -365,6 +365,16 @@ def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
     _check(lib().photon_crc_set_stream_config(run_blocks, rows_per_step, steps_in_flight))
 
 
+def set_generic_rows(u):
+    """Generic batch kernel: rows per step (2, 4, 8)."""
+    _check(lib().photon_crc_set_generic_rows(u))
+
+
+def set_stream64_config(rows_per_step, steps_in_flight):
+    """CRC-64 streaming-kernel shape (U, D)."""
+    _check(lib().photon_crc64_set_stream_config(rows_per_step, steps_in_flight))
+
+
 def read_stream(base, nbytes, sink, sink_words, stream=None):
     """Bench utility: HBM read-only stream over nbytes (achievable-roofline probe)."""
     _check(lib().photon_crc_util_read_stream(_ptr(base), nbytes, _ptr(sink), sink_words, _stream(stream)))

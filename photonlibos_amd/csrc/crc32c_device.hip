@@ -54,8 +54,13 @@ namespace {
 
 thread_local std::string g_err;
 int g_lanes_override = 0;
+int g_generic_u = 4;  // generic kernel: rows per step (2, 4, 8)
 int g_stream_b = 1, g_stream_u = 4, g_stream_d = 3;  // streaming kernel: run blocks, rows/step, steps in flight
-bool g_stream_enabled = true;
+// The streaming kernel is a tuning option: with the conflict-free rotated
+// tables the generic kernel measures faster on every config
+// (profiles/tune_r01_generic_rows.jsonl), so it is off by default.
+bool g_stream_enabled = false;
+bool g_stream64_enabled = true;
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -177,15 +182,26 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
     const uint64_t gpw = 64 / g;
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
-    if (grid > (uint64_t)cus) grid = cus;
     const LaneConsts& kc = lane_consts(g);
-    switch (g) {
-        case 64: hipLaunchKernelGGL(crc32c_batch_kernel<64>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
-        case 32: hipLaunchKernelGGL(crc32c_batch_kernel<32>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
-        case 16: hipLaunchKernelGGL(crc32c_batch_kernel<16>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
-        case 8: hipLaunchKernelGGL(crc32c_batch_kernel<8>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
-        default: hipLaunchKernelGGL(crc32c_batch_kernel<4>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
+    if (grid > (uint64_t)cus) grid = cus;
+#define LB(GG, UU) hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc)
+#define LBG(UU)                    \
+    switch (g) {                   \
+        case 64: LB(64, UU); break; \
+        case 32: LB(32, UU); break; \
+        case 16: LB(16, UU); break; \
+        case 8: LB(8, UU); break;   \
+        default: LB(4, UU); break;  \
     }
+    if (g_generic_u == 2) {
+        LBG(2)
+    } else if (g_generic_u == 8) {
+        LBG(8)
+    } else {
+        LBG(4)
+    }
+#undef LBG
+#undef LB
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "crc32c_batch_kernel launch");
     return 0;
@@ -228,6 +244,60 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "crc64_batch_kernel launch");
+    return 0;
+}
+
+// CRC-64 streaming kernel shape (rows per step, steps in flight).
+int g_stream64_u = 8, g_stream64_d = 1;
+
+template <int G>
+bool launch_uniform64_g(const Uniform64Args& a, dim3 grid, hipStream_t st) {
+    const LaneConsts64& kc = lane_consts64(G);
+    const int u = g_stream64_u, d = g_stream64_d;
+    if (u == 4 && d == 2) hipLaunchKernelGGL((crc64_uniform_kernel<G, 4, 2>), grid, dim3(kBlock), 0, st, a, kc);
+    else if (u == 4 && d == 3) hipLaunchKernelGGL((crc64_uniform_kernel<G, 4, 3>), grid, dim3(kBlock), 0, st, a, kc);
+    else if (u == 2 && d == 4) hipLaunchKernelGGL((crc64_uniform_kernel<G, 2, 4>), grid, dim3(kBlock), 0, st, a, kc);
+    else if (u == 8 && d == 1) hipLaunchKernelGGL((crc64_uniform_kernel<G, 8, 1>), grid, dim3(kBlock), 0, st, a, kc);
+    else return false;
+    return true;
+}
+
+int try_launch_uniform64(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint64_t seed0,
+                         const uint64_t* seeds, uint64_t* out, hipStream_t stream) {
+    if (!g_stream64_enabled || count == 0) return 1;
+    const int g = choose_lanes(nbytes);
+    const uint64_t row = 16ull * g;
+    if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
+    const uint64_t rows = nbytes / row;
+    if (rows % (uint64_t)g_stream64_u) return 1;
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    const uint64_t gpw = 64 / g;
+    const uint64_t waves = (count + gpw - 1) / gpw;
+    uint64_t grid = (waves + kWaves - 1) / kWaves;
+    if (grid > (uint64_t)cus) grid = cus;
+    const uint64_t xn = xpow64(8ull * nbytes);
+    Uniform64Args a{base, stride, rows, count, out, mulmod64(seeds ? ~0ull : ~seed0, xn)};
+    bool ok = false;
+    switch (g) {
+        case 64: ok = launch_uniform64_g<64>(a, dim3(grid), stream); break;
+        case 32: ok = launch_uniform64_g<32>(a, dim3(grid), stream); break;
+        case 16: ok = launch_uniform64_g<16>(a, dim3(grid), stream); break;
+        case 8: ok = launch_uniform64_g<8>(a, dim3(grid), stream); break;
+        default: ok = launch_uniform64_g<4>(a, dim3(grid), stream); break;
+    }
+    if (!ok) return fail(-EINVAL, "unsupported CRC-64 streaming configuration");
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "crc64_uniform_kernel launch");
+    if (seeds) {
+        SeedConsts64 sc;
+        for (int i = 0; i < 64; ++i) sc.basis[i] = mulmod64(1ull << i, xn);
+        const int bs = 256;
+        hipLaunchKernelGGL(crc64_seed_kernel, dim3((count + bs - 1) / bs), dim3(bs), 0, stream, out, count, seeds, sc);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "crc64_seed_kernel launch");
+    }
     return 0;
 }
 
@@ -383,6 +453,13 @@ int photon_crc_set_lanes_per_buffer(int g) {
     return 0;
 }
 
+int photon_crc_set_generic_rows(int rows_per_step) {
+    if (rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
+        return fail(-EINVAL, "rows per step must be 2, 4 or 8");
+    g_generic_u = rows_per_step;
+    return 0;
+}
+
 int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight) {
     if (run_blocks == 0) {
         g_stream_enabled = false;
@@ -394,6 +471,20 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
     g_stream_b = run_blocks;
     g_stream_u = rows_per_step;
     g_stream_d = steps_in_flight;
+    return 0;
+}
+
+int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight) {
+    const int u = rows_per_step, d = steps_in_flight;
+    if (u == 0) {
+        g_stream64_enabled = false;
+        return 0;
+    }
+    if (!((u == 4 && (d == 2 || d == 3)) || (u == 2 && d == 4) || (u == 8 && d == 1)))
+        return fail(-EINVAL, "unsupported CRC-64 (rows_per_step, steps_in_flight)");
+    g_stream64_enabled = true;
+    g_stream64_u = u;
+    g_stream64_d = d;
     return 0;
 }
 
@@ -527,6 +618,11 @@ int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_m
 int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                    uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
     if (count && (!d_out || (!d_base && nbytes))) return fail(-EINVAL, "null buffer or output");
+    {
+        const int rc = try_launch_uniform64(static_cast<const uint8_t*>(d_base), stride, nbytes, count, seed0, d_seeds,
+                                            d_out, static_cast<hipStream_t>(stream));
+        if (rc <= 0) return rc;  // launched (0) or failed (< 0); 1 = not a uniform batch
+    }
     Batch64Args a{};
     a.base = static_cast<const uint8_t*>(d_base);
     a.stride = stride;

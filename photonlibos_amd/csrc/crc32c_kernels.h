@@ -11,12 +11,18 @@
 namespace pcrc {
 
 // ------------------------------------------------------------------ LDS map
-constexpr uint32_t kDataBytes = 2u * 65536u;   // 4 slices x 256 idx x 32 replicas x 4 B
-constexpr uint32_t kShiftBase = kDataBytes;    // S tables follow
-constexpr uint32_t kShiftBytes = 4u * 4096u;   // 4 slices x 256 idx x 4 replicas x 4 B
-constexpr uint32_t kBasisBase = kShiftBase + kShiftBytes;  // lane-combine constants
+// One 256-byte row per table index idx:
+//   [idx][  0..127]: D tables, x -> x * x^32 mod P, 4 byte slices t x 8 replicas
+//   [idx][128..255]: S tables, P -> P * x^(8*16*G),  4 byte slices t x 8 replicas
+// (entry (t, r) at t*32 + r*4). ds_read_b32 banks are (addr/4) mod 32 in lane
+// groups of 32; lane l takes its 4 slices in the rotated order t = (i+q)%4,
+// q = (l/8)%4, r = l%8, so in every lookup instruction the 32 lanes of a group
+// hit 32 distinct banks: conflict-free random lookups with 8 replicas.
+constexpr uint32_t kTableBytes = 256u * 256u;                // 64 KiB
+constexpr uint32_t kSOff = 128u;                             // S half of a row
+constexpr uint32_t kBasisBase = kTableBytes;                 // lane-combine constants
 constexpr uint32_t kBasisBytes = 6u * 32u * 4u;
-constexpr uint32_t kLdsBytes = kBasisBase + kBasisBytes;   // 148224 B of the 160 KiB
+constexpr uint32_t kLdsBytes = kBasisBase + kBasisBytes;     // 66304 B of the 160 KiB
 constexpr int kBlock = 1024;                   // 16 waves, one workgroup per CU
 constexpr int kWaves = kBlock / 64;
 
@@ -47,51 +53,61 @@ __device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
-// Per-lane LDS base addresses: D slice t lives at ((t>>1)<<16) + idx*256 +
-// ((t&1)<<7) + (lane&31)*4, so its address is (idx << 8) | d[t].
+// Per-lane lookup constants: the data word is rotated right by 8q bits
+// (byte i of the rotated word = byte (i+q)%4), and off[i] = ((i+q)%4)*32 +
+// r*4 locates slice (i+q)%4, replica r inside a table row.
 struct LaneAddr {
-    uint32_t d0, d1, d2, d3, s;
+    uint32_t rot;      // 8*q
+    uint32_t off[4];
+    uint32_t r4;       // r*4 (byte-serial tail)
 };
 
-// x * x^32 mod P = CRC register after absorbing the 32-bit word x.
-// Address of slice t for byte t of x in ONE v_perm_b32: result bytes are
-// {d.byte0, x.byte t, d.byte2, 0} (selector 0..3 = second operand's bytes,
-// 4..7 = first operand's bytes, 12 = 0x00).
-template <int T>
-__device__ __forceinline__ uint32_t daddr(uint32_t x, uint32_t d) {
-    return __builtin_amdgcn_perm(x, d, 0x0C020000u | ((4u + T) << 8));
+__device__ __forceinline__ uint32_t rot32(uint32_t x, const LaneAddr& a) {
+    return __builtin_amdgcn_alignbit(x, x, a.rot);
 }
 
-__device__ __forceinline__ uint32_t dstep(const uint32_t* lds, uint32_t x, const LaneAddr& a) {
-    const uint32_t t0 = lds_word(lds, daddr<0>(x, a.d0));
-    const uint32_t t1 = lds_word(lds, daddr<1>(x, a.d1));
-    const uint32_t t2 = lds_word(lds, daddr<2>(x, a.d2));
-    const uint32_t t3 = lds_word(lds, daddr<3>(x, a.d3));
-    return t0 ^ t1 ^ t2 ^ t3;
+// Lookup i of a rotated word: address (xr.byte i << 8) | off[i] in ONE
+// v_perm_b32 (result bytes {off.byte0, xr.byte i, 0, 0}; selector 0..3 = the
+// second operand's bytes, 4..7 = the first's, 12 = 0x00); TOFF selects the
+// D (0) or S (kSOff) half of the row through the instruction's offset field.
+template <int I, uint32_t TOFF>
+__device__ __forceinline__ uint32_t look(const uint32_t* lds, uint32_t xr, const LaneAddr& a) {
+    return lds_word(lds, __builtin_amdgcn_perm(xr, a.off[I], 0x0C0C0000u | ((4u + I) << 8)) + TOFF);
 }
 
-// P * x^(8*gap+32) mod P through the S tables (slice t at s + t*4096 + idx*16).
-__device__ __forceinline__ uint32_t sstep(const uint32_t* lds, uint32_t p, uint32_t s) {
-    const uint32_t t0 = lds_word(lds, s + ((p << 4) & 0xff0u));
-    const uint32_t t1 = lds_word(lds, s + 4096u + ((p >> 4) & 0xff0u));
-    const uint32_t t2 = lds_word(lds, s + 8192u + ((p >> 12) & 0xff0u));
-    const uint32_t t3 = lds_word(lds, s + 12288u + ((p >> 20) & 0xff0u));
-    return t0 ^ t1 ^ t2 ^ t3;
+// a ^ b ^ c in ONE instruction (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// x * x^32 mod P (the CRC register after absorbing the 32-bit word x), XORed
+// with e (the next data word, or 0).
+__device__ __forceinline__ uint32_t dstep(const uint32_t* lds, uint32_t x, const LaneAddr& a, uint32_t e = 0) {
+    const uint32_t xr = rot32(x, a);
+    return xor3(xor3(look<0, 0>(lds, xr, a), look<1, 0>(lds, xr, a), look<2, 0>(lds, xr, a)),
+                look<3, 0>(lds, xr, a), e);
+}
+
+// P * x^(8*16*G) mod P through the S tables, XORed with e.
+__device__ __forceinline__ uint32_t sstep(const uint32_t* lds, uint32_t p, const LaneAddr& a, uint32_t e = 0) {
+    const uint32_t pr = rot32(p, a);
+    return xor3(xor3(look<0, kSOff>(lds, pr, a), look<1, kSOff>(lds, pr, a), look<2, kSOff>(lds, pr, a)),
+                look<3, kSOff>(lds, pr, a), e);
 }
 
 // Byte-serial step with the D3 slice (D3[b] = b<<24 * x^32 = b * x^8, the
 // classic byte table).
 __device__ __forceinline__ uint32_t bytestep(const uint32_t* lds, uint32_t c, uint8_t b, const LaneAddr& a) {
-    const uint32_t x = c ^ b;
-    return lds_word(lds, daddr<0>(x, a.d3)) ^ (c >> 8);
+    const uint32_t x = (c ^ b) & 0xffu;
+    return lds_word(lds, (x << 8) + 3u * 32u + a.r4) ^ (c >> 8);
 }
 
 // CRC (init 0, no xorout) of one 16-byte block: four chained word steps.
 __device__ __forceinline__ uint32_t crc16(const uint32_t* lds, uint4 w, const LaneAddr& a) {
-    uint32_t c = dstep(lds, w.x, a);
-    c = dstep(lds, c ^ w.y, a);
-    c = dstep(lds, c ^ w.z, a);
-    return dstep(lds, c ^ w.w, a);
+    uint32_t c = dstep(lds, w.x, a, w.y);
+    c = dstep(lds, c, a, w.z);
+    c = dstep(lds, c, a, w.w);
+    return dstep(lds, c, a);
 }
 
 // U blocks of one lane's column: the crc16s are independent (ILP), only the
@@ -103,12 +119,12 @@ __device__ __forceinline__ uint32_t column_step(const uint32_t* lds, uint32_t p,
 #pragma unroll
     for (int u = 0; u < U; ++u) c[u] = crc16(lds, w[u], a);
 #pragma unroll
-    for (int u = 0; u < U; ++u) p = sstep(lds, p, a.s) ^ c[u];
+    for (int u = 0; u < U; ++u) p = sstep(lds, p, a, c[u]);
     return p;
 }
 
 __device__ __forceinline__ uint32_t column_step1(const uint32_t* lds, uint32_t p, uint4 w, const LaneAddr& a) {
-    return sstep(lds, p, a.s) ^ crc16(lds, w, a);
+    return sstep(lds, p, a, crc16(lds, w, a));
 }
 
 // Word at byte offset `off` (relative to the aligned start A0) of the first
@@ -148,29 +164,28 @@ __device__ __forceinline__ uint8_t load8(const uint8_t* p) { return *(g_u8*)p; }
 // Build the D and S tables in LDS (every workgroup; 1024 threads = one entry of
 // each table per thread).
 __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc) {
-    const uint32_t kshift = kc.kshift;
     const uint32_t tid = threadIdx.x;
     if (tid < 6 * 32) lds[kBasisBase / 4 + tid] = kc.basis[tid >> 5][tid & 31];
     const uint32_t t = tid >> 8, b = tid & 255u;
     const uint32_t v = b << (8 * t);
     const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
-    const uint32_t dbase = (((t >> 1) << 16) + (b << 8) + ((t & 1) << 7)) >> 2;
+    const uint32_t sv = mulmod(v, kc.kshift);
+    const uint32_t base = ((b << 8) + (t << 5)) >> 2;
 #pragma unroll
-    for (int r = 0; r < 32; ++r) lds[dbase + r] = dv;
-    const uint32_t sv = mulmod(v, kshift);
-    const uint32_t sbase = (kShiftBase + t * 4096u + b * 16u) >> 2;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) lds[sbase + r] = sv;
+    for (int r = 0; r < 8; ++r) {
+        lds[base + r] = dv;
+        lds[base + kSOff / 4 + r] = sv;
+    }
     __syncthreads();
 }
 
 __device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
     LaneAddr la;
-    la.d0 = ((lane & 31u) << 2);
-    la.d1 = (1u << 7) | ((lane & 31u) << 2);
-    la.d2 = (1u << 16) | ((lane & 31u) << 2);
-    la.d3 = (1u << 16) | (1u << 7) | ((lane & 31u) << 2);
-    la.s = kShiftBase + ((lane & 3u) << 2);
+    const uint32_t q = (lane >> 3) & 3u, r = lane & 7u;
+    la.rot = 8u * q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) la.off[i] = (((i + q) & 3u) << 5) | (r << 2);
+    la.r4 = r << 2;
     return la;
 }
 
@@ -209,13 +224,13 @@ __device__ __forceinline__ uint32_t wave_id() {
 
 // -------------------------------------------------------------- generic path
 // Any pointer, any length, any seed; one group of G lanes per buffer.
-template <int G>
+// U rows per step per lane, the next U rows' loads in flight.
+template <int G, int U = 4>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     build_tables(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
-    constexpr int U = 4;         // blocks per lane per step
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
     const uint32_t gl = lane & (G - 1);
@@ -362,10 +377,10 @@ __device__ __forceinline__ uint32_t run_crc(const uint32_t* lds, const uint4 (&r
     uint32_t c = crc16(lds, r[0], a);
 #pragma unroll
     for (int b = 1; b < B; ++b) {
-        c = dstep(lds, c ^ r[b].x, a);
-        c = dstep(lds, c ^ r[b].y, a);
-        c = dstep(lds, c ^ r[b].z, a);
-        c = dstep(lds, c ^ r[b].w, a);
+        c = dstep(lds, c ^ r[b].x, a, r[b].y);
+        c = dstep(lds, c, a, r[b].z);
+        c = dstep(lds, c, a, r[b].w);
+        c = dstep(lds, c, a);
     }
     return c;
 }
@@ -461,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if constexpr (ABL & 1) pc = (pc ^ (pc << 1)) ^ c[u];
-                else pc = sstep(lds, pc, la.s) ^ c[u];
+                else pc = sstep(lds, pc, la, c[u]);
             }
             if (++step == spb) {
                 // End of this buffer: this lane's last run is G-1-run runs from the end.
@@ -647,18 +662,32 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint
 
 // ============================================================ CRC-64/ECMA
 // Same column algorithm at 64 bits (reference crc64ecma_sw, crc.cpp:119-122:
-// reflected poly 0xC96C5795D7870F42, register inverted in and out). 64-bit
-// table entries are read with ds_read_b64; LDS holds
-//   D64: x -> x * x^64 mod P, 8 byte slices x 256 x 4 replicas x 8 B = 64 KiB
-//   S64: P -> P * x^(8*16*G),  same shape                            = 64 KiB
-//   lane-combine bases x^(128*2^k), k < 6: 6 x 64 x 8 B              =  3 KiB
+// reflected poly 0xC96C5795D7870F42, register inverted in and out). Values
+// are kept as two 32-bit halves (uint2: .x = low, .y = high); 64-bit table
+// entries are read with ds_read_b64 (bank = (addr/4) mod 64, lane groups of
+// 32 lanes, 2 banks per lane). LDS holds
+//   D64: x -> x * x^64 mod P64, 8 byte slices x 256 x 4 replicas,
+//        layout [idx][slice t][lane%4] (256 B per index)             64 KiB
+//   S64: P -> P * x^(8*16*G), same layout, at +64 KiB                   64 KiB
+//   lane-combine bases x^(128*2^k), k < 6: 6 x 64 x 8 B                 3 KiB
+// Conflict-free lookups with only 4 replicas: lane l takes its 8 slices in
+// the rotated order t = (i + q) % 8, q = (l/4) % 8, so in every lookup
+// instruction i the 32 lanes of a group hit 32 distinct (t, replica) bank
+// pairs. The rotation is applied to the looked-up VALUE (two v_perm_b32 with
+// per-lane selectors: byte i of x_rot = byte (i+q)%8 of x), so the address
+// of lookup i is ONE v_perm_b32 {off_i.byte0, x_rot.byte i, 0 | off_i.byte2, 0}
+// with off_i = ((i+q)%8)*32 + (l%4)*8 (+ 1<<16, selected for S).
 constexpr uint32_t k64SBase = 65536u;
 constexpr uint32_t k64BasisBase = 131072u;
-constexpr uint32_t k64LdsBytes = k64BasisBase + 6u * 64u * 8u;
+constexpr uint32_t k64LdsBytes = k64BasisBase + 6u * 64u * 8u;  // 134144 B
 
 struct LaneConsts64 {
     uint64_t kshift;           // x^(8*16*G) mod P64
     uint64_t basis[6][64];     // basis of x^(128 * 2^k)
+};
+
+struct SeedConsts64 {
+    uint64_t basis[64];        // basis of x^(8 * nbytes) mod P64
 };
 
 struct Batch64Args {
@@ -672,25 +701,104 @@ struct Batch64Args {
     uint64_t seed0;
 };
 
-__device__ __forceinline__ uint64_t lds_dword(const uint64_t* lds, uint32_t byte_addr) {
-    return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+struct Uniform64Args {
+    const uint8_t* base;
+    uint64_t stride;
+    uint64_t rows;             // nbytes / (16*G)
+    uint64_t count;
+    uint64_t* out;
+    uint64_t init_shift;       // (~seed0) * x^(8*nbytes): the inverted init's contribution
+};
+
+__device__ __forceinline__ uint2 lds_u2(const uint32_t* lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
-// Slice t of table base `tb` (layout [slice][idx][lane%4], 8-byte entries).
-template <int T>
-__device__ __forceinline__ uint64_t look64(const uint64_t* lds, uint64_t x, uint32_t tb) {
-    const uint32_t idx = (uint32_t)(x >> (8 * T)) & 0xffu;
-    return lds_dword(lds, tb + T * 8192u + idx * 32u);
+__device__ __forceinline__ uint2 xor2(uint2 a, uint2 b) { return make_uint2(a.x ^ b.x, a.y ^ b.y); }
+
+struct LaneAddr64 {
+    uint32_t rot_lo, rot_hi;   // v_perm selectors rotating a 64-bit value right by 8q bits
+    uint32_t off[8];           // off_i = ((i+q)%8)*32 + (lane%4)*8 | 1<<16
+    uint32_t r8;               // (lane%4)*8, for the byte-serial tail
+};
+
+__device__ __forceinline__ LaneAddr64 lane_addr64(uint32_t lane) {
+    LaneAddr64 a;
+    const uint32_t q = (lane >> 2) & 7u, r = lane & 3u;
+    // perm(hi, lo, sel): source bytes 0-3 = lo, 4-7 = hi; result byte i = byte (i+q)%8.
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        lo |= ((i + q) & 7u) << (8 * i);
+        hi |= ((i + 4 + q) & 7u) << (8 * i);
+    }
+    a.rot_lo = lo;
+    a.rot_hi = hi;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a.off[i] = (((i + q) & 7u) << 5) | (r << 3) | (1u << 16);
+    a.r8 = r << 3;
+    return a;
 }
 
-__device__ __forceinline__ uint64_t step64(const uint64_t* lds, uint64_t x, uint32_t tb) {
-    return look64<0>(lds, x, tb) ^ look64<1>(lds, x, tb) ^ look64<2>(lds, x, tb) ^ look64<3>(lds, x, tb) ^
-           look64<4>(lds, x, tb) ^ look64<5>(lds, x, tb) ^ look64<6>(lds, x, tb) ^ look64<7>(lds, x, tb);
+__device__ __forceinline__ uint2 rot64(uint2 x, const LaneAddr64& a) {
+    return make_uint2(__builtin_amdgcn_perm(x.y, x.x, a.rot_lo), __builtin_amdgcn_perm(x.y, x.x, a.rot_hi));
 }
 
-__device__ __forceinline__ uint64_t bytestep64(const uint64_t* lds, uint64_t c, uint8_t b, uint32_t db) {
-    // D64 slice 7: (b << 56) * x^64 = b * x^8, the classic byte table.
-    return look64<7>(lds, (uint64_t)((c ^ b) & 0xffu) << 56, db) ^ (c >> 8);
+// Lookup i (0..7) of the rotated value's byte i; TS = 0 for D64, 1 for S64.
+template <int I, int TS>
+__device__ __forceinline__ uint2 look64(const uint32_t* lds, uint2 xr, const LaneAddr64& a) {
+    const uint32_t half = I < 4 ? xr.x : xr.y;
+    const uint32_t sel = (TS ? 0x0C020000u : 0x0C0C0000u) | ((4u + (I & 3)) << 8);
+    return lds_u2(lds, __builtin_amdgcn_perm(half, a.off[I], sel));
+}
+
+// Table product of x (8 lookups) XORed with e: 4 v_bitop3 per half.
+template <int TS>
+__device__ __forceinline__ uint2 step64(const uint32_t* lds, uint2 x, const LaneAddr64& a, uint2 e) {
+    const uint2 xr = rot64(x, a);
+    const uint2 l0 = look64<0, TS>(lds, xr, a), l1 = look64<1, TS>(lds, xr, a);
+    const uint2 l2 = look64<2, TS>(lds, xr, a), l3 = look64<3, TS>(lds, xr, a);
+    const uint2 l4 = look64<4, TS>(lds, xr, a), l5 = look64<5, TS>(lds, xr, a);
+    const uint2 l6 = look64<6, TS>(lds, xr, a), l7 = look64<7, TS>(lds, xr, a);
+    return make_uint2(xor3(xor3(l0.x, l1.x, l2.x), xor3(l3.x, l4.x, l5.x), xor3(l6.x, l7.x, e.x)),
+                      xor3(xor3(l0.y, l1.y, l2.y), xor3(l3.y, l4.y, l5.y), xor3(l6.y, l7.y, e.y)));
+}
+
+// x * x^64 mod P64 (^ e).
+__device__ __forceinline__ uint2 dstep64(const uint32_t* lds, uint2 x, const LaneAddr64& a,
+                                         uint2 e = make_uint2(0, 0)) {
+    return step64<0>(lds, x, a, e);
+}
+
+// P * x^(8*16*G) mod P64 (^ e).
+__device__ __forceinline__ uint2 sstep64(const uint32_t* lds, uint2 p, const LaneAddr64& a,
+                                         uint2 e = make_uint2(0, 0)) {
+    return step64<1>(lds, p, a, e);
+}
+
+// CRC register (init 0) after a 16-byte block.
+__device__ __forceinline__ uint2 crc16_64(const uint32_t* lds, uint4 w, const LaneAddr64& a) {
+    return dstep64(lds, dstep64(lds, make_uint2(w.x, w.y), a, make_uint2(w.z, w.w)), a);
+}
+
+__device__ __forceinline__ uint64_t u64of(uint2 v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint2 u2of(uint64_t v) { return make_uint2((uint32_t)v, (uint32_t)(v >> 32)); }
+
+// Byte-serial step: D64 slice 7 = (b << 56) * x^64 = b * x^8, the classic byte table.
+__device__ __forceinline__ uint64_t bytestep64(const uint32_t* lds, uint64_t c, uint8_t b, const LaneAddr64& a) {
+    const uint2 t = lds_u2(lds, ((uint32_t)((c ^ b) & 0xffu) << 8) + 7u * 32u + a.r8);
+    return u64of(t) ^ (c >> 8);
+}
+
+__device__ __forceinline__ uint64_t mul_basis64_lds(uint64_t p, const uint32_t* lds, uint32_t basis_addr) {
+    uint64_t r = 0;
+#pragma unroll 4
+    for (int i = 0; i < 64; i += 2) {
+        const uint4 b = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(lds) + basis_addr + i * 8);
+        r ^= (0ull - ((p >> i) & 1ull)) & (((uint64_t)b.y << 32) | b.x);
+        r ^= (0ull - ((p >> (i + 1)) & 1ull)) & (((uint64_t)b.w << 32) | b.z);
+    }
+    return r;
 }
 
 __device__ __forceinline__ uint64_t mul_basis64(uint64_t p, const uint64_t* basis) {
@@ -712,34 +820,53 @@ __device__ __forceinline__ uint64_t head_word64(uint64_t w, int off, int s0, uin
     return w;
 }
 
+__device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64& kc) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t e = tid; e < 2048u; e += kBlock) {
+        const uint32_t t = e >> 8, b = e & 255u;
+        const uint64_t v = (uint64_t)b << (8 * t);
+        const uint2 dv = u2of(mulmod64(v, kPoly64 /* x^64 mod P64 = the reflected polynomial */));
+        const uint2 sv = u2of(mulmod64(v, kc.kshift));
+        const uint32_t base = (b << 8) + (t << 5);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + base + r * 8) = dv;
+            *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64SBase + base + r * 8) = sv;
+        }
+    }
+    if (tid < 6 * 64)
+        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64BasisBase + tid * 8u) =
+            u2of(kc.basis[tid >> 6][tid & 63]);
+    __syncthreads();
+}
+
+// Shift lane partials by x^(128*d) and XOR-reduce over the G lanes.
+template <int G>
+__device__ __forceinline__ uint64_t group_reduce64(uint64_t pc, uint32_t d, const uint32_t* lds) {
+    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
+#pragma unroll 1
+    for (int k = 0; k < LOG2G; ++k)
+        if ((d >> k) & 1u) pc = mul_basis64_lds(pc, lds, k64BasisBase + 512u * k);
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)pc, o, 64);
+        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(pc >> 32), o, 64);
+        pc ^= ((uint64_t)hi32 << 32) | lo32;
+    }
+    return pc;
+}
+
+// Any pointer / length / seed (iovec batches, ragged and unaligned buffers).
 template <int G>
 __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint64_t lds[k64LdsBytes / 8];
-    {
-        // 1024 threads: thread -> (slice t, index b); 2048 entries per table.
-        const uint32_t tid = threadIdx.x;
-        for (uint32_t e = tid; e < 2048u; e += kBlock) {
-            const uint32_t t = e >> 8, b = e & 255u;
-            const uint64_t v = (uint64_t)b << (8 * t);
-            const uint64_t dv = mulmod64(v, kPoly64 /* x^64 mod P64 = the reflected polynomial */);
-            const uint64_t sv = mulmod64(v, kc.kshift);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                lds[(t * 8192u + b * 32u + r * 8u) / 8] = dv;
-                lds[(k64SBase + t * 8192u + b * 32u + r * 8u) / 8] = sv;
-            }
-        }
-        if (tid < 6 * 64) lds[k64BasisBase / 8 + tid] = kc.basis[tid >> 6][tid & 63];
-        __syncthreads();
-    }
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
+    build_tables64(lds, kc);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp = lane / G;
     constexpr int GPW = 64 / G;
-    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
-    const uint32_t db = (lane & 3u) * 8u;            // D64 base for this lane's replica
-    const uint32_t sb = k64SBase + (lane & 3u) * 8u;  // S64 base
-    const uint64_t* basis = lds + k64BasisBase / 8;
+    constexpr int U = 4;
+    const LaneAddr64 la = lane_addr64(lane);
 
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave_id(); wv * GPW < args.count; wv += nwaves) {
@@ -762,54 +889,147 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
         if (n < 64) {
             reg = init;
             if (gl == 0)
-                for (uint64_t k = 0; k < n; ++k) reg = bytestep64(lds, reg, load8(p + k), db);
+                for (uint64_t k = 0; k < n; ++k) reg = bytestep64(lds, reg, load8(p + k), la);
         } else {
             const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
             const uint8_t* e = p + n;
             const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
             const int s0 = (int)(p - a0);
             const uint64_t nb = (uint64_t)(eb - a0) >> 4;
+            const uint64_t full = nb / G;
             const uint64_t rows = (nb + G - 1) / G;
             const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);
             const uint8_t* lp = a0 + 16 * gl;
-            uint64_t pc = 0;
-            for (uint64_t row = 0; row < rows; row += 2) {
-                uint4 w[2];
-                bool have[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const uint64_t i = (row + u) * G + gl;
-                    have[u] = row + u < rows && i < nb;
-                    w[u] = have[u] ? load16(lp + (row + u) * (16 * G)) : make_uint4(0, 0, 0, 0);
+            uint2 pc = make_uint2(0, 0);
+            // Row 0 (head: masked leading bytes + inverted init).
+            if (gl < nb) {
+                uint4 w = load16(lp);
+                if (gl < 2) {
+                    const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
+                    const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
+                    w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
                 }
+                pc = crc16_64(lds, w, la);
+            }
+            uint64_t row = 1;
+            if (row + U <= full) {
+                uint4 cur[U];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    if (!have[u]) continue;
-                    uint64_t lo = ((uint64_t)w[u].y << 32) | w[u].x, hi = ((uint64_t)w[u].w << 32) | w[u].z;
-                    if (row + u == 0 && gl < 2) {
-                        lo = head_word64(lo, (int)gl * 16, s0, init);
-                        hi = head_word64(hi, (int)gl * 16 + 8, s0, init);
-                    }
-                    const uint64_t c = step64(lds, step64(lds, lo, db) ^ hi, db);
-                    pc = step64(lds, pc, sb) ^ c;
+                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
+                for (; row + 2 * U <= full; row += U) {
+                    uint4 nxt[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+                    uint2 c[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, cur[u], la);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
                 }
-            }
-            const uint32_t d = (rlast + G - 1 - gl) & (G - 1);
-#pragma unroll 1
-            for (int k = 0; k < LOG2G; ++k)
-                if ((d >> k) & 1u) pc = mul_basis64(pc, basis + 64 * k);
+                uint2 c[U];
 #pragma unroll
-            for (int o = G / 2; o > 0; o >>= 1) {
-                const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)pc, o, 64);
-                const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(pc >> 32), o, 64);
-                pc ^= ((uint64_t)hi32 << 32) | lo32;
+                for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, cur[u], la);
+#pragma unroll
+                for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+                row += U;
             }
-            reg = pc;
+            for (; row < full; ++row) pc = sstep64(lds, pc, la, crc16_64(lds, load16(lp + row * (16 * G)), la));
+            if (full >= 1 && full < rows && full * G + gl < nb)
+                pc = sstep64(lds, pc, la, crc16_64(lds, load16(lp + full * (16 * G)), la));
+            reg = group_reduce64<G>(u64of(pc), (rlast + G - 1 - gl) & (G - 1), lds);
             if (gl == 0)
-                for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), db);
+                for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
         }
         if (active && gl == 0) args.out[bi] = ~reg;
     }
+}
+
+// Uniform batches (aligned base and stride, nbytes = R*16*G with R % U == 0):
+// the continuous cross-buffer load ring of crc32c_uniform_kernel (B = 1).
+// Register init 0; lane 0 applies the inverted init (~seed0 * x^(8n)) and the
+// final inversion; per-buffer seeds are folded in by crc64_seed_kernel.
+template <int G, int U, int D>
+__global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
+    build_tables64(lds, kc);
+
+    constexpr uint64_t GPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const LaneAddr64 la = lane_addr64(lane);
+
+    const uint64_t ngroups = (args.count + GPW - 1) / GPW;
+    const uint64_t wv0 = (uint64_t)blockIdx.x * kWaves + wave_id();
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    if (wv0 >= ngroups) return;
+    const uint64_t nslots = (ngroups - 1 - wv0) / nwaves + 1;
+    const uint64_t spb = args.rows / U;
+    const uint64_t nsteps = nslots * spb;
+    constexpr uint64_t kRow = 16ull * G;
+
+    auto buffer_of = [&](uint64_t slot) -> uint64_t {
+        const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
+        return bi < args.count ? bi : args.count - 1;
+    };
+    auto slot_base = [&](uint64_t slot) -> const uint8_t* {
+        if (slot >= nslots) slot = nslots - 1;
+        return args.base + buffer_of(slot) * args.stride + 16ull * gl;
+    };
+    uint64_t lslot = 0, lstep = 0;
+    const uint8_t* lptr = slot_base(0);
+    auto advance = [&]() {
+        if (++lstep == spb) {
+            lstep = 0;
+            ++lslot;
+            lptr = slot_base(lslot);
+        } else if (lslot < nslots) {
+            lptr += kRow * U;
+        }
+    };
+    constexpr int S = D + 1;
+    uint4 ring[S][U];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) ring[d][u] = load16(lptr + u * kRow);
+        advance();
+    }
+    const uint64_t padded = (nsteps + S - 1) / S * S;
+    uint64_t slot = 0, step = 0;
+    uint2 pc = make_uint2(0, 0);
+    for (uint64_t s = 0; s < padded; s += S) {
+#pragma unroll
+        for (int d = 0; d < S; ++d) {
+            const int refill = (d + D) % S;
+#pragma unroll
+            for (int u = 0; u < U; ++u) ring[refill][u] = load16(lptr + u * kRow);
+            advance();
+            uint2 c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, ring[d][u], la);
+#pragma unroll
+            for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+            if (++step == spb) {
+                const uint64_t crc = group_reduce64<G>(u64of(pc), (uint32_t)(G - 1 - gl), lds);
+                const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
+                if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = ~(crc ^ args.init_shift);
+                pc = make_uint2(0, 0);
+                step = 0;
+                ++slot;
+            }
+        }
+    }
+}
+
+// out[i] ^= seed_i * x^(8*nbytes) (the uniform kernel used seed0 = 0:
+// ~(F ^ ~s*X) = ~(F ^ ~0*X) ^ s*X).
+__global__ void crc64_seed_kernel(uint64_t* out, uint64_t count, const uint64_t* seeds, SeedConsts64 sc) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    out[i] ^= mul_basis64(seeds[i], sc.basis);
 }
 
 }  // namespace pcrc

@@ -49,4 +49,4 @@ for v in args.variants.split(",") * args.repeat:
                       "median_ms": round(float(np.median(ms)), 4),
                       "median_GBps": round(total / float(np.median(ms)) / 1e6, 1)}), flush=True)
 ck.set_lanes_per_buffer(0)
-ck.set_stream_config(1, 4, 3)
+ck.set_stream_config(0, 0, 0)

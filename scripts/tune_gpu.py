@@ -30,6 +30,7 @@ stream = torch.cuda.current_stream()
 buf = torch.empty(nbytes * count, dtype=torch.uint8, device="cuda")
 ck.fill_splitmix(buf, nbytes, nbytes, count, 0x5EED0001)
 out = torch.zeros(count, dtype=torch.int32, device="cuda")
+out64 = torch.zeros(count, dtype=torch.int64, device="cuda")
 sink = torch.zeros(256 * 256 * 8, dtype=torch.int32, device="cuda")
 torch.cuda.synchronize()
 total = nbytes * count
@@ -49,9 +50,20 @@ def timed(fn):
 def make(v, lanes):
     if v == "read":
         return lambda: ck.read_stream(buf, total, sink, sink.numel(), stream=stream)
+    if v.startswith("s64") or v == "g64":
+        def f64():
+            ck.set_lanes_per_buffer(lanes)
+            if v == "g64":
+                ck.set_stream64_config(0, 0)
+            else:
+                _, u, d = v.split(":")
+                ck.set_stream64_config(int(u), int(d))
+            ck.batch64_strided(buf, nbytes, nbytes, count, out64, stream=stream)
+        return f64
     def f():
         ck.set_lanes_per_buffer(lanes)
-        if v == "generic":
+        if v.startswith("generic"):
+            ck.set_generic_rows(int(v.split(":")[1]) if ":" in v else 4)
             ck.set_stream_config(0)
         else:
             _, b, u, d = v.split(":")
@@ -61,7 +73,7 @@ def make(v, lanes):
 
 
 variants = [(v, int(l)) for v in args.variants.split(",") for l in args.lanes.split(",")] + [("read", 0)]
-ref = None
+refs = {}
 res = {f"{v}/G{l}": [] for v, l in variants}
 for r in range(args.rounds):
     for v, l in variants:
@@ -69,11 +81,15 @@ for r in range(args.rounds):
         res[f"{v}/G{l}"].append(ms)
         if v != "read":
             torch.cuda.synchronize()
-            o = out.cpu().numpy().copy()
-            if ref is None:
-                ref = o
-            assert np.array_equal(o, ref), f"variant {v}/G{l} disagrees"
-ck.set_stream_config(1, 4, 3)
+            is64 = v.startswith("s64") or v == "g64"
+            o = (out64 if is64 else out).cpu().numpy().copy()
+            key = "64" if is64 else "32"
+            if key not in refs:
+                refs[key] = o
+            assert np.array_equal(o, refs[key]), f"variant {v}/G{l} disagrees"
+ck.set_stream_config(0, 0, 0)
+ck.set_stream64_config(8, 1)
+ck.set_generic_rows(4)
 ck.set_lanes_per_buffer(0)
 rows = []
 for k, ms in res.items():

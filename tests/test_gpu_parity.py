@@ -29,7 +29,7 @@ def torch_dev():
 def _reset_lanes():
     yield
     ck.set_lanes_per_buffer(0)
-    ck.set_stream_config(1, 4, 3)
+    ck.set_stream_config(0, 0, 0)
 
 
 STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (0, 0, 0)]
@@ -176,7 +176,9 @@ def test_full_c2_4gib(torch_dev, oracle):
     ck.set_lanes_per_buffer(16)
     b = run_strided(torch_dev, d, nbytes, nbytes, count)
     ck.set_lanes_per_buffer(0)
+    ck.set_stream_config(1, 4, 3)  # the streaming kernel
     c = run_strided(torch_dev, d, nbytes, nbytes, count)
+    ck.set_stream_config(0, 0, 0)
     assert np.array_equal(a, b) and np.array_equal(a, c)
     rnd = random.Random(2)
     for i in [0, 1, count - 1] + [rnd.randrange(count) for _ in range(61)]:
