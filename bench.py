@@ -144,7 +144,8 @@ class Workload:
         elif c["kind"] == "strided64":
             ck.batch64_strided(self.payload, c["nbytes"], c["nbytes"], c["count"], self.out, stream=self.stream)
         else:
-            ck.batch_msg(self.iov, self.start, c["count"], self.seg_out, self.out, stream=self.stream)
+            ck.batch_msg_n(self.iov, self.start, c["count"], c["count"] * c["nseg"], self.seg_out, self.out,
+                           stream=self.stream)
 
     def self_check(self):
         """Spot-check results against the product's own host engine (crc32c_hw

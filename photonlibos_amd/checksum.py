@@ -292,6 +292,12 @@ def batch_msg(iov, msg_start, nmsg, seg_out, out, seed=0, seeds=None, stream=Non
                                          _ptr(seg_out), _ptr(out), _stream(stream)))
 
 
+def batch_msg_n(iov, msg_start, nmsg, nseg, seg_out, out, seed=0, seeds=None, stream=None):
+    """batch_msg with the total segment count supplied (fully asynchronous)."""
+    _check(lib().photon_crc32c_batch_msg_n(_ptr(iov), _ptr(msg_start), nmsg, nseg, seed & 0xFFFFFFFF, _ptr(seeds),
+                                           _ptr(seg_out), _ptr(out), _stream(stream)))
+
+
 def batch64_strided(base, stride, nbytes, count, out, seed=0, seeds=None, stream=None):
     """out[i] = crc64ecma_extend(base + i*stride, nbytes, seeds[i] or seed) (uint64 out). Async."""
     _check(lib().photon_crc64ecma_batch_strided(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFFFFFFFFFF,

@@ -20,9 +20,11 @@ namespace pcrc {
 // hit 32 distinct banks: conflict-free random lookups with 8 replicas.
 constexpr uint32_t kTableBytes = 256u * 256u;                // 64 KiB
 constexpr uint32_t kSOff = 128u;                             // S half of a row
-constexpr uint32_t kBasisBase = kTableBytes;                 // lane-combine constants
-constexpr uint32_t kBasisBytes = 6u * 32u * 4u;
-constexpr uint32_t kLdsBytes = kBasisBase + kBasisBytes;     // 66304 B of the 160 KiB
+// Lane-combine tables R_k: p -> p * x^(128*B*2^k) mod P, k < 6, 4 byte slices,
+// one replica ([k][t][idx]); used once per buffer (group_reduce).
+constexpr uint32_t kRBase = kTableBytes;
+constexpr uint32_t kRBytes = 6u * 4u * 256u * 4u;            // 24 KiB
+constexpr uint32_t kLdsBytes = kRBase + kRBytes;             // 90112 B of the 160 KiB
 constexpr int kBlock = 1024;                   // 16 waves, one workgroup per CU
 constexpr int kWaves = kBlock / 64;
 
@@ -165,8 +167,16 @@ __device__ __forceinline__ uint8_t load8(const uint8_t* p) { return *(g_u8*)p; }
 // each table per thread).
 __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc) {
     const uint32_t tid = threadIdx.x;
-    if (tid < 6 * 32) lds[kBasisBase / 4 + tid] = kc.basis[tid >> 5][tid & 31];
     const uint32_t t = tid >> 8, b = tid & 255u;
+    // R_k[t][b] = (b << 8t) * x^(128*B*2^k): XOR of the basis words of b's bits
+    // (t is uniform per wavefront, so the basis reads are scalar).
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & kc.basis[k][8 * t + j];
+        lds[kRBase / 4 + k * 1024 + t * 256 + b] = r;
+    }
     const uint32_t v = b << (8 * t);
     const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
     const uint32_t sv = mulmod(v, kc.kshift);
@@ -191,28 +201,18 @@ __device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
 
 // Shift lane partials to the end of the body (d blocks of 16 bytes) and
 // XOR-reduce over the G lanes of the group.
-// p * K with K's basis (32 words) in LDS, read 4 words at a time (broadcast).
-__device__ __forceinline__ uint32_t mul_basis_lds(uint32_t p, const uint32_t* basis) {
-    uint32_t r = 0;
-#pragma unroll 2
-    for (int q = 0; q < 8; ++q) {
-        const uint4 b = reinterpret_cast<const uint4*>(basis)[q];
-        r ^= (0u - ((p >> (4 * q)) & 1u)) & b.x;
-        r ^= (0u - ((p >> (4 * q + 1)) & 1u)) & b.y;
-        r ^= (0u - ((p >> (4 * q + 2)) & 1u)) & b.z;
-        r ^= (0u - ((p >> (4 * q + 3)) & 1u)) & b.w;
-    }
-    return r;
-}
-
 template <int G>
 __device__ __forceinline__ uint32_t group_reduce(uint32_t pc, uint32_t d, const uint32_t* lds) {
     constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
-    // basis[k][i] of x^(128*2^k), staged in LDS by build_tables.
-    const uint32_t* basis = lds + kBasisBase / 4;
-#pragma unroll 1
-    for (int k = 0; k < LOG2G; ++k)
-        if ((d >> k) & 1u) pc = mul_basis_lds(pc, basis + 32 * k);
+    // pc * x^(128*B*d) via the R_k tables on the bits of d (every lane runs
+    // every level; a select keeps the wavefront convergent).
+#pragma unroll
+    for (int k = 0; k < LOG2G; ++k) {
+        const uint32_t* R = lds + kRBase / 4 + k * 1024;
+        const uint32_t m = xor3(xor3(R[pc & 0xffu], R[256 + ((pc >> 8) & 0xffu)], R[512 + ((pc >> 16) & 0xffu)]),
+                                R[768 + (pc >> 24)], 0u);
+        pc = ((d >> k) & 1u) ? m : pc;
+    }
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
     return pc;

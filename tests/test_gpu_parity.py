@@ -218,6 +218,11 @@ def test_msg_scatter_gather(torch_dev, oracle, nmsg, nseg, seglen):
     for m in range(nmsg):
         parts = [slot_data[perm[m * nseg + j]] for j in range(nseg)]
         assert got[m] == oracle.extend_chain(parts, int(seeds[m])), m
+    # the fully asynchronous form (host supplies the segment count) agrees
+    out2 = torch_dev.zeros(nmsg, dtype=torch_dev.int32, device="cuda")
+    ck.batch_msg_n(d_iov, d_start, nmsg, slots, seg_out, out2, seeds=d_seeds)
+    torch_dev.cuda.synchronize()
+    assert np.array_equal(u32(out2), got)
 
 
 def test_msg_ragged_segments(torch_dev, oracle):
