@@ -305,7 +305,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
+    # one process per GPU; ranks beyond the visible devices (a rehearsal on a
+    # smaller box) share them round-robin
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     ck.set_lanes_per_buffer(args.lanes)
     stream = torch.cuda.current_stream()
     if args.h2d:
