@@ -166,9 +166,13 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
 int photon_crc_set_generic_rows(int rows_per_step);
 
 /* The CRC-64 streaming kernel's shape: rows per step U and steps in flight D,
- * one of (8,1) (default), (4,2), (4,3), (2,4); U = 0 turns it off (generic
+ * one of (4,3) (default), (4,2), (8,1), (2,4); U = 0 turns it off (generic
  * kernel for every CRC-64 batch). */
 int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
+
+/* Interleaved row partials per lane in the CRC-64 streaming kernel (testing /
+ * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
+int photon_crc64_set_interleave(int partials);
 
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed

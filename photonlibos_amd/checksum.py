@@ -376,6 +376,11 @@ def set_generic_rows(u):
     _check(lib().photon_crc_set_generic_rows(u))
 
 
+def set_stream64_interleave(v):
+    """CRC-64 streaming kernel: interleaved row partials per lane (1, 2, 4)."""
+    _check(lib().photon_crc64_set_interleave(v))
+
+
 def set_stream64_config(rows_per_step, steps_in_flight):
     """CRC-64 streaming-kernel shape (U, D)."""
     _check(lib().photon_crc64_set_stream_config(rows_per_step, steps_in_flight))

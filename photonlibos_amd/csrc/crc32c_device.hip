@@ -247,17 +247,29 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     return 0;
 }
 
-// CRC-64 streaming kernel shape (rows per step, steps in flight).
-int g_stream64_u = 8, g_stream64_d = 1;
+// CRC-64 streaming kernel shape (rows per step, steps in flight, interleaved
+// partials per lane).
+int g_stream64_u = 4, g_stream64_d = 3, g_stream64_v = 1;
+
+template <int G, int U, int D>
+void launch_uniform64_v(const Uniform64Args& a, dim3 grid, hipStream_t st) {
+    constexpr int V2 = (G <= 32 && U % 2 == 0) ? 2 : 1;
+    constexpr int V4 = (G <= 16 && U % 4 == 0) ? 4 : V2;
+    if (g_stream64_v >= 4)
+        hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, V4>), grid, dim3(kBlock), 0, st, a, lane_consts64(G * V4));
+    else if (g_stream64_v >= 2)
+        hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, V2>), grid, dim3(kBlock), 0, st, a, lane_consts64(G * V2));
+    else
+        hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, 1>), grid, dim3(kBlock), 0, st, a, lane_consts64(G));
+}
 
 template <int G>
 bool launch_uniform64_g(const Uniform64Args& a, dim3 grid, hipStream_t st) {
-    const LaneConsts64& kc = lane_consts64(G);
     const int u = g_stream64_u, d = g_stream64_d;
-    if (u == 4 && d == 2) hipLaunchKernelGGL((crc64_uniform_kernel<G, 4, 2>), grid, dim3(kBlock), 0, st, a, kc);
-    else if (u == 4 && d == 3) hipLaunchKernelGGL((crc64_uniform_kernel<G, 4, 3>), grid, dim3(kBlock), 0, st, a, kc);
-    else if (u == 2 && d == 4) hipLaunchKernelGGL((crc64_uniform_kernel<G, 2, 4>), grid, dim3(kBlock), 0, st, a, kc);
-    else if (u == 8 && d == 1) hipLaunchKernelGGL((crc64_uniform_kernel<G, 8, 1>), grid, dim3(kBlock), 0, st, a, kc);
+    if (u == 4 && d == 2) launch_uniform64_v<G, 4, 2>(a, grid, st);
+    else if (u == 4 && d == 3) launch_uniform64_v<G, 4, 3>(a, grid, st);
+    else if (u == 2 && d == 4) launch_uniform64_v<G, 2, 4>(a, grid, st);
+    else if (u == 8 && d == 1) launch_uniform64_v<G, 8, 1>(a, grid, st);
     else return false;
     return true;
 }
@@ -471,6 +483,12 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
     g_stream_b = run_blocks;
     g_stream_u = rows_per_step;
     g_stream_d = steps_in_flight;
+    return 0;
+}
+
+int photon_crc64_set_interleave(int partials) {
+    if (partials != 1 && partials != 2 && partials != 4) return fail(-EINVAL, "interleave must be 1, 2 or 4");
+    g_stream64_v = partials;
     return 0;
 }
 

@@ -669,7 +669,7 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint
 //   D64: x -> x * x^64 mod P64, 8 byte slices x 256 x 4 replicas,
 //        layout [idx][slice t][lane%4] (256 B per index)             64 KiB
 //   S64: P -> P * x^(8*16*G), same layout, at +64 KiB                   64 KiB
-//   lane-combine bases x^(128*2^k), k < 6: 6 x 64 x 8 B                 3 KiB
+//   lane-combine tables x^(128*2^k), k < 6, nibble-sliced              12 KiB
 // Conflict-free lookups with only 4 replicas: lane l takes its 8 slices in
 // the rotated order t = (i + q) % 8, q = (l/4) % 8, so in every lookup
 // instruction i the 32 lanes of a group hit 32 distinct (t, replica) bank
@@ -678,8 +678,10 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint
 // of lookup i is ONE v_perm_b32 {off_i.byte0, x_rot.byte i, 0 | off_i.byte2, 0}
 // with off_i = ((i+q)%8)*32 + (l%4)*8 (+ 1<<16, selected for S).
 constexpr uint32_t k64SBase = 65536u;
-constexpr uint32_t k64BasisBase = 131072u;
-constexpr uint32_t k64LdsBytes = k64BasisBase + 6u * 64u * 8u;  // 134144 B
+// Lane-combine tables R64_k: p -> p * x^(128*2^k), k < 6, NIBBLE-sliced
+// (16 positions x 16 values x 8 B = 2 KiB per k): used once per buffer.
+constexpr uint32_t k64RBase = 131072u;
+constexpr uint32_t k64LdsBytes = k64RBase + 6u * 16u * 16u * 8u;  // 143360 B
 
 struct LaneConsts64 {
     uint64_t kshift;           // x^(8*16*G) mod P64
@@ -790,15 +792,18 @@ __device__ __forceinline__ uint64_t bytestep64(const uint32_t* lds, uint64_t c, 
     return u64of(t) ^ (c >> 8);
 }
 
-__device__ __forceinline__ uint64_t mul_basis64_lds(uint64_t p, const uint32_t* lds, uint32_t basis_addr) {
-    uint64_t r = 0;
-#pragma unroll 4
-    for (int i = 0; i < 64; i += 2) {
-        const uint4 b = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(lds) + basis_addr + i * 8);
-        r ^= (0ull - ((p >> i) & 1ull)) & (((uint64_t)b.y << 32) | b.x);
-        r ^= (0ull - ((p >> (i + 1)) & 1ull)) & (((uint64_t)b.w << 32) | b.z);
-    }
-    return r;
+// p * x^(128*2^k) through the nibble tables R64_k (16 lookups).
+__device__ __forceinline__ uint64_t mul_r64(uint64_t p, const uint32_t* lds, int k) {
+    const char* R = reinterpret_cast<const char*>(lds) + k64RBase + k * 2048;
+    uint2 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+        v[m] = *reinterpret_cast<const uint2*>(R + m * 128 + (((uint32_t)(p >> (4 * m)) & 15u) << 3));
+    uint32_t lo = xor3(xor3(v[0].x, v[1].x, v[2].x), xor3(v[3].x, v[4].x, v[5].x), xor3(v[6].x, v[7].x, v[8].x));
+    uint32_t hi = xor3(xor3(v[0].y, v[1].y, v[2].y), xor3(v[3].y, v[4].y, v[5].y), xor3(v[6].y, v[7].y, v[8].y));
+    lo = xor3(lo, xor3(v[9].x, v[10].x, v[11].x), xor3(v[12].x, v[13].x, v[14].x)) ^ v[15].x;
+    hi = xor3(hi, xor3(v[9].y, v[10].y, v[11].y), xor3(v[12].y, v[13].y, v[14].y)) ^ v[15].y;
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t mul_basis64(uint64_t p, const uint64_t* basis) {
@@ -834,19 +839,33 @@ __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64
             *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64SBase + base + r * 8) = sv;
         }
     }
-    if (tid < 6 * 64)
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64BasisBase + tid * 8u) =
-            u2of(kc.basis[tid >> 6][tid & 63]);
+    // R64_k[m][v] = (v << 4m) * x^(128*2^k): XOR of the basis words of v's bits.
+    for (uint32_t e = tid; e < 6u * 256u; e += kBlock) {
+        const uint32_t k = e >> 8, m = (e >> 4) & 15u, v = e & 15u;
+        uint64_t r = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & kc.basis[k][4 * m + j];
+        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64RBase + e * 8u) = u2of(r);
+    }
     __syncthreads();
+}
+
+// p * x^(128*d) for d < 2^LOG2 (basis multiplies on the bits of d).
+template <int LOG2>
+__device__ __forceinline__ uint64_t shift64(uint64_t pc, uint32_t d, const uint32_t* lds) {
+#pragma unroll
+    for (int k = 0; k < LOG2; ++k) {
+        const uint64_t m = mul_r64(pc, lds, k);
+        pc = ((d >> k) & 1u) ? m : pc;  // every lane runs every level: no divergence
+    }
+    return pc;
 }
 
 // Shift lane partials by x^(128*d) and XOR-reduce over the G lanes.
 template <int G>
 __device__ __forceinline__ uint64_t group_reduce64(uint64_t pc, uint32_t d, const uint32_t* lds) {
     constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
-#pragma unroll 1
-    for (int k = 0; k < LOG2G; ++k)
-        if ((d >> k) & 1u) pc = mul_basis64_lds(pc, lds, k64BasisBase + 512u * k);
+    pc = shift64<LOG2G>(pc, d, lds);
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) {
         const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)pc, o, 64);
@@ -950,7 +969,11 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
 // the continuous cross-buffer load ring of crc32c_uniform_kernel (B = 1).
 // Register init 0; lane 0 applies the inverted init (~seed0 * x^(8n)) and the
 // final inversion; per-buffer seeds are folded in by crc64_seed_kernel.
-template <int G, int U, int D>
+// V interleaved partials per lane: partial j takes rows r = j (mod V), i.e.
+// lane l plays virtual lane j*G + l of a V*G-lane geometry (row shift
+// x^(8*16*G*V), the kc passed is lane_consts64(G*V)); V independent S chains
+// of U/V steps instead of one of U steps.
+template <int G, int U, int D, int V = 1>
 __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
     build_tables64(lds, kc);
@@ -998,8 +1021,12 @@ __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args arg
         advance();
     }
     const uint64_t padded = (nsteps + S - 1) / S * S;
+    static_assert(U % V == 0 && G * V <= 64, "interleave must divide the step; V*G lanes <= 64");
+    constexpr int LOG2VG = G * V == 64 ? 6 : G * V == 32 ? 5 : G * V == 16 ? 4 : G * V == 8 ? 3 : 2;
     uint64_t slot = 0, step = 0;
-    uint2 pc = make_uint2(0, 0);
+    uint2 pc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) pc[j] = make_uint2(0, 0);
     for (uint64_t s = 0; s < padded; s += S) {
 #pragma unroll
         for (int d = 0; d < S; ++d) {
@@ -1011,12 +1038,22 @@ __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args arg
 #pragma unroll
             for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, ring[d][u], la);
 #pragma unroll
-            for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+            for (int u = 0; u < U; ++u) pc[u % V] = sstep64(lds, pc[u % V], la, c[u]);
             if (++step == spb) {
-                const uint64_t crc = group_reduce64<G>(u64of(pc), (uint32_t)(G - 1 - gl), lds);
+                uint64_t acc = 0;
+#pragma unroll
+                for (int j = 0; j < V; ++j)
+                    acc ^= shift64<LOG2VG>(u64of(pc[j]), (uint32_t)(G * V - 1 - (j * G + gl)), lds);
+#pragma unroll
+                for (int o = G / 2; o > 0; o >>= 1) {
+                    const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);
+                    const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), o, 64);
+                    acc ^= ((uint64_t)hi32 << 32) | lo32;
+                }
                 const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
-                if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = ~(crc ^ args.init_shift);
-                pc = make_uint2(0, 0);
+                if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = ~(acc ^ args.init_shift);
+#pragma unroll
+                for (int j = 0; j < V; ++j) pc[j] = make_uint2(0, 0);
                 step = 0;
                 ++slot;
             }

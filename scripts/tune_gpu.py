@@ -56,8 +56,9 @@ def make(v, lanes):
             if v == "g64":
                 ck.set_stream64_config(0, 0)
             else:
-                _, u, d = v.split(":")
-                ck.set_stream64_config(int(u), int(d))
+                parts = v.split(":")
+                ck.set_stream64_config(int(parts[1]), int(parts[2]))
+                ck.set_stream64_interleave(int(parts[3]) if len(parts) > 3 else 2)
             ck.batch64_strided(buf, nbytes, nbytes, count, out64, stream=stream)
         return f64
     def f():
@@ -88,7 +89,8 @@ for r in range(args.rounds):
                 refs[key] = o
             assert np.array_equal(o, refs[key]), f"variant {v}/G{l} disagrees"
 ck.set_stream_config(0, 0, 0)
-ck.set_stream64_config(8, 1)
+ck.set_stream64_config(4, 3)
+ck.set_stream64_interleave(1)
 ck.set_generic_rows(4)
 ck.set_lanes_per_buffer(0)
 rows = []

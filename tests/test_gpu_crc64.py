@@ -95,15 +95,20 @@ def test_strided(torch_dev, oracle, g):
             assert int(got[i]) == oracle.crc64ecma(datagen.stream_bytes(0x640 + nbytes + i, nbytes), 0x1234), i
 
 
+@pytest.mark.parametrize("v", [1, 2, 4])
 @pytest.mark.parametrize("shape", [(4, 2), (4, 3), (2, 4), (8, 1), None])
 @pytest.mark.parametrize("g", [8, 32, 64])
-def test_streaming_shapes(torch_dev, oracle, shape, g):
-    # The CRC-64 streaming kernel (uniform batches) in every shape, with seed0,
-    # per-buffer seeds and no seed; counts that do not fill whole wave tuples.
+def test_streaming_shapes(torch_dev, oracle, shape, g, v):
+    # The CRC-64 streaming kernel (uniform batches) in every shape and row
+    # interleave, with seed0, per-buffer seeds and no seed; counts that do not
+    # fill whole wave tuples.
     if shape is None:
+        if v != 1:
+            pytest.skip("generic kernel has no interleave")
         ck.set_stream64_config(0, 0)  # generic kernel only
     else:
         ck.set_stream64_config(*shape)
+        ck.set_stream64_interleave(v)
     ck.set_lanes_per_buffer(g)
     try:
         for nbytes, count in ((16 * 64 * 8, 37), (65536, 301), (4096, 1001)):
@@ -121,7 +126,8 @@ def test_streaming_shapes(torch_dev, oracle, shape, g):
                     want = oracle.crc64ecma(datagen.stream_bytes(0x6400 + nbytes + i, nbytes), sd(i))
                     assert int(got[i]) == want, (shape, g, nbytes, i)
     finally:
-        ck.set_stream64_config(8, 1)
+        ck.set_stream64_config(4, 3)
+        ck.set_stream64_interleave(1)
 
 
 def test_full_c2_crc64(torch_dev, oracle):
@@ -137,7 +143,7 @@ def test_full_c2_crc64(torch_dev, oracle):
     try:
         ck.batch64_strided(d, n, n, cnt, b)
     finally:
-        ck.set_stream64_config(8, 1)
+        ck.set_stream64_config(4, 3)
     torch_dev.cuda.synchronize()
     assert torch_dev.equal(a, b)
     got = a.cpu().numpy().view(np.uint64)
