@@ -174,6 +174,21 @@ int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
  * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
 int photon_crc64_set_interleave(int partials);
 
+/* Producers outside device memory.
+ * photon_crc_host_register: make an existing host range (e.g. the iovec
+ * targets of IFile::preadv, fs/filesystem.h:54-70) readable by the kernels in
+ * place (hipHostRegister, mapped); undo with photon_crc_host_unregister.
+ * photon_crc32c_file_strided: h_out[i] = crc32c_extend(record i, nbytes,
+ * seed0) for the records at file offset + i*stride of fd. A reader thread
+ * pread()s 4 KiB-aligned chunks (so an O_DIRECT fd works: the device reads
+ * what the disk DMA'd, the CPU touches no payload byte) into two pinned chunk
+ * buffers while the GPU pipeline checksums the previous chunk. Synchronous;
+ * -EIO if the file ends before the last record, -errno on a read error. */
+int photon_crc_host_register(void* ptr, uint64_t len);
+int photon_crc_host_unregister(void* ptr);
+int photon_crc32c_file_strided(int fd, uint64_t offset, uint64_t stride, uint64_t nbytes, uint64_t count,
+                               uint32_t seed0, uint32_t* h_out);
+
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
  * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),

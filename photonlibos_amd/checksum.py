@@ -366,6 +366,23 @@ def crc32c_combine_series_at(addr, part_size, n_parts):
     return _auto("crc32c_combine_series_auto", _CSER_PTR_FN)(addr, part_size, n_parts)
 
 
+def host_register(addr, nbytes):
+    """Make host memory [addr, addr+nbytes) device-readable in place."""
+    _check(lib().photon_crc_host_register(addr, nbytes))
+
+
+def host_unregister(addr):
+    _check(lib().photon_crc_host_unregister(addr))
+
+
+def file_strided(fd, offset, stride, nbytes, count, seed=0):
+    """CRC32C of `count` records of `nbytes` at offset + i*stride of file descriptor fd
+    (pread into pinned chunks + GPU pipeline). Returns a list of ints."""
+    out = (ctypes.c_uint32 * max(count, 1))()
+    _check(lib().photon_crc32c_file_strided(fd, offset, stride, nbytes, count, seed & 0xFFFFFFFF, out))
+    return list(out)[:count]
+
+
 def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
     """Streaming-kernel shape (B, U, D) for uniform batches; B = 0 disables it."""
     _check(lib().photon_crc_set_stream_config(run_blocks, rows_per_step, steps_in_flight))

@@ -1,0 +1,203 @@
+// file_source.cpp -- producers of checksum input outside device memory
+// (include/photon_crc/crc32c_gpu.h):
+//   photon_crc_host_register / _unregister: make existing host buffers (e.g.
+//       the iovec targets of IFile::preadv, fs/filesystem.h:54-70) readable by
+//       the kernels in place (hipHostRegister, mapped);
+//   photon_crc32c_file_strided: checksum equal-size records of a file. A
+//       reader thread pread()s 4 KiB-aligned chunks (O_DIRECT-compatible) into
+//       two pinned chunk buffers while the GPU pipeline
+//       (photon_crc32c_host_batch_strided) checksums the previous chunk, so
+//       the CPU never touches the payload bytes when the fd is O_DIRECT.
+#include <errno.h>
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+
+#include <photon_crc/crc32c_gpu.h>
+
+#include "internal.h"
+
+namespace {
+
+using pcrc::report_error;
+using pcrc::report_hip_error;
+
+constexpr uint64_t kAlign = 4096;
+constexpr uint64_t kChunk = 64ull << 20;  // payload span per chunk
+constexpr int kReadThreads = 8;           // parallel preads per chunk (page-cache copies are per-core bound)
+
+struct ChunkBufs {
+    std::mutex mu;
+    void* buf[2] = {nullptr, nullptr};
+    uint64_t cap = 0;
+};
+
+ChunkBufs& chunk_bufs() {
+    static ChunkBufs* c = new ChunkBufs;
+    return *c;
+}
+
+// Read [off, off+want_max) of fd into dst, accepting a short read at end of
+// file once at least want_min bytes are in (the 4 KiB-rounded tail of the
+// last chunk may run past EOF). -errno, or -EIO before want_min.
+int read_span(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_max, uint64_t off, std::string* err) {
+    uint64_t got = 0;
+    while (got < want_max) {
+        const ssize_t r = pread(fd, dst + got, want_max - got, (off_t)(off + got));
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            *err = std::string("pread: ") + strerror(errno);
+            return -errno;
+        }
+        got += (uint64_t)r;
+        if (r == 0 || (got >= want_min && got < want_max)) break;
+    }
+    if (got < want_min) {
+        *err = "pread: end of file before the last record";
+        return -EIO;
+    }
+    return 0;
+}
+
+// read_span over kReadThreads 4 KiB-aligned pieces in parallel; only the last
+// piece may end short (at EOF).
+int read_span_parallel(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_max, uint64_t off, std::string* err) {
+    const uint64_t piece = ((want_max / kReadThreads) + kAlign - 1) & ~(kAlign - 1);
+    if (want_max < 4 * kAlign * kReadThreads || piece == 0) return read_span(fd, dst, want_min, want_max, off, err);
+    int rcs[kReadThreads] = {};
+    std::string errs[kReadThreads];
+    std::thread th[kReadThreads];
+    int used = 0;
+    for (uint64_t lo = 0; lo < want_max; lo += piece, ++used) {
+        const uint64_t hi = lo + piece < want_max ? lo + piece : want_max;
+        const bool last = hi == want_max;
+        const uint64_t need = last ? (want_min > lo ? want_min - lo : 0) : hi - lo;
+        th[used] = std::thread([=, &rcs, &errs] { rcs[used] = read_span(fd, dst + lo, need, hi - lo, off + lo, &errs[used]); });
+    }
+    int rc = 0;
+    for (int i = 0; i < used; ++i) {
+        th[i].join();
+        if (rcs[i] && !rc) {
+            rc = rcs[i];
+            *err = errs[i];
+        }
+    }
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int photon_crc_host_register(void* ptr, uint64_t len) {
+    if (!ptr || !len) return report_error(-EINVAL, "null or empty range");
+    hipError_t e = hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipHostRegister");
+}
+
+int photon_crc_host_unregister(void* ptr) {
+    hipError_t e = hipHostUnregister(ptr);
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipHostUnregister");
+}
+
+int photon_crc32c_file_strided(int fd, uint64_t offset, uint64_t stride, uint64_t nbytes, uint64_t count,
+                               uint32_t seed0, uint32_t* h_out) {
+    if (!count) return 0;
+    if (fd < 0 || !h_out || stride < nbytes || !nbytes) return report_error(-EINVAL, "bad arguments");
+    if (photon_crc_device_count() <= 0) return -ENODEV;
+    // Records per chunk; a chunk's read span is rounded out to 4 KiB.
+    uint64_t per = kChunk / stride;
+    if (per == 0) per = 1;
+    if (per > count) per = count;
+    const uint64_t span_max = (per - 1) * stride + nbytes + 2 * kAlign;
+    ChunkBufs& cb = chunk_bufs();
+    std::lock_guard<std::mutex> lk(cb.mu);
+    if (cb.cap < span_max) {
+        for (void*& b : cb.buf)
+            if (b) {
+                (void)hipHostFree(b);
+                b = nullptr;
+            }
+        cb.cap = 0;
+        for (void*& b : cb.buf) {
+            hipError_t e = hipHostMalloc(&b, span_max, hipHostMallocPortable);
+            if (e != hipSuccess) return report_hip_error(e, "hipHostMalloc(chunk)");
+        }
+        cb.cap = span_max;
+    }
+
+    const uint64_t nchunks = (count + per - 1) / per;
+    std::mutex mu;
+    std::condition_variable cv;
+    int ready[2] = {-1, -1};  // chunk index held by each buffer, -1 = free
+    int64_t skew[2] = {0, 0};  // record 0 of the chunk sits at buf + skew
+    int read_rc = 0;
+    std::string read_err;
+    bool stop = false;
+
+    std::thread reader([&] {
+        for (uint64_t c = 0; c < nchunks; ++c) {
+            const int slot = (int)(c & 1);
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return ready[slot] < 0 || stop; });
+                if (stop) return;
+            }
+            const uint64_t first = c * per;
+            const uint64_t k = count - first < per ? count - first : per;
+            const uint64_t lo = offset + first * stride;
+            const uint64_t hi = lo + (k - 1) * stride + nbytes;
+            const uint64_t alo = lo & ~(kAlign - 1);
+            const uint64_t ahi = (hi + kAlign - 1) & ~(kAlign - 1);
+            std::string err;
+            int rc = read_span_parallel(fd, static_cast<uint8_t*>(cb.buf[slot]), hi - alo, ahi - alo, alo, &err);
+            std::unique_lock<std::mutex> g(mu);
+            if (rc) {
+                read_rc = rc;
+                read_err = err;
+                stop = true;
+                cv.notify_all();
+                return;
+            }
+            skew[slot] = (int64_t)(lo - alo);
+            ready[slot] = (int)c;
+            cv.notify_all();
+        }
+    });
+
+    int rc = 0;
+    for (uint64_t c = 0; c < nchunks && !rc; ++c) {
+        const int slot = (int)(c & 1);
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return ready[slot] == (int)c || stop; });
+            if (ready[slot] != (int)c) {
+                rc = read_rc ? read_rc : -EIO;
+                break;
+            }
+        }
+        const uint64_t first = c * per;
+        const uint64_t k = count - first < per ? count - first : per;
+        rc = photon_crc32c_host_batch_strided(static_cast<uint8_t*>(cb.buf[slot]) + skew[slot], stride, nbytes, k,
+                                              seed0, nullptr, h_out + first);
+        std::unique_lock<std::mutex> g(mu);
+        ready[slot] = -1;
+        cv.notify_all();
+    }
+    {
+        std::unique_lock<std::mutex> g(mu);
+        stop = true;
+        cv.notify_all();
+    }
+    reader.join();
+    if (read_rc) return report_error(read_rc, read_err.c_str());
+    return rc;
+}
+
+}  // extern "C"

@@ -13,6 +13,7 @@ for c in c2 c3 c4 c5 c2_crc64; do
 done
 timeout -k 10 300 python bench.py --h2d > $O/bench_h2d.log 2>&1 || { echo "h2d failed"; exit 1; }
 timeout -k 10 300 python bench.py --rpc-batch > $O/bench_rpc.log 2>&1 || { echo "rpc-batch failed"; exit 1; }
+timeout -k 10 300 python bench.py --file-records > $O/bench_file.log 2>&1 || { echo "file-records failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2 -o c2 -- python3 bench.py --no-cpu-baseline > $O/prof_c2.log 2>&1 || { echo "prof failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_c2 -o c2 -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/pmc_c2.log 2>&1 || { echo "pmc failed"; exit 1; }
 bash scripts/pmc_kernel.sh c2 $O/sq_c2 > /dev/null || { echo "sq c2 failed"; exit 1; }

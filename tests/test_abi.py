@@ -76,6 +76,8 @@ def test_device_calls_fail_loudly_without_gpu():
         ck.device_count()
     with pytest.raises(ck.CrcError):
         ck.batch_strided(0x1000, 4096, 4096, 1, 0x2000)
+    with pytest.raises(ck.CrcError):
+        ck.file_strided(0, 0, 4096, 4096, 1)
 
 
 def test_argument_validation():

@@ -212,3 +212,24 @@ def test_device_dispatch_dropin(torch_dev, oracle):
     assert ck.crc32c_combine_series_at(out_d.data_ptr(), ps, np_) == oracle.crc32c(host[:ps * np_])
     ck.set_device_dispatch(False)
     assert ck.crc32c_extend_at(hbuf.ctypes.data, n, 77) == expect
+
+
+def test_extend_device_over_4gib(torch_dev):
+    # One buffer larger than 2^32 bytes (64-bit lengths and offsets end to
+    # end): the split/fold path equals the series + combine_series identity.
+    torch = torch_dev
+    n = (5 << 30) + 4096 * 3
+    dbuf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, n, n, 1, 0x5EED0500)
+    one = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.extend_device(dbuf, n, 0, one)
+    ps = 4096
+    parts = torch.zeros(n // ps, dtype=torch.int32, device="cuda")
+    ck.series_device(dbuf, ps, n // ps, parts)
+    folded = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.combine_series_device(parts, ps, n // ps, folded)
+    torch.cuda.synchronize()
+    assert n % ps == 0
+    assert int(u32(one)[0]) == int(u32(folded)[0])
+    del dbuf
+    torch.cuda.empty_cache()
