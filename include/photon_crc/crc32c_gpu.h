@@ -75,6 +75,32 @@ int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nb
 int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                      uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out);
 
+/* (i-h, many GPUs) The same host-memory batch sharded over the first `ndev`
+ * gfx950 devices (0 = every device) of THIS process -- Photon runs one
+ * process per host, not one per GPU: contiguous slices of the buffer indices,
+ * one host thread per device driving that device's pipeline over its own
+ * host link, results in h_out[count] exactly as the single-device call.
+ * No collective. Synchronous. */
+int photon_crc32c_host_batch_strided_multi(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                           uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out, int ndev);
+
+/* (i-d, many GPUs) Device-resident shards, each on its own device: shard i is
+ * photon_crc32c_batch_strided on `device` (pointers of that device, stream of
+ * that device or NULL). Enqueues every shard and returns (async); the caller's
+ * current device is restored. */
+typedef struct photon_crc_shard {
+    int device;
+    const void* d_base;
+    uint64_t stride;
+    uint64_t nbytes;
+    uint64_t count;
+    uint32_t seed0;
+    const uint32_t* d_seeds;
+    uint32_t* d_out;
+    void* stream;
+} photon_crc_shard;
+int photon_crc32c_batch_strided_shards(const photon_crc_shard* shards, int nshards);
+
 /* (ii) Arbitrary buffers: d_iov[count] (device-resident descriptors); any
  * alignment, any length (0 returns the seed). */
 int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint32_t seed0,
@@ -161,8 +187,9 @@ int photon_crc_set_lanes_per_buffer(int g);
  * the current tables); run_blocks = 0 turns it off again. */
 int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
 
-/* Rows per step of the generic batch kernel (testing / tuning): 2, 4
- * (default) or 8. */
+/* Batch kernel variant (testing / tuning): 2, 4 (default) or 8 = the generic
+ * kernel with that many rows per step; 0 = the fused kernel (four rows per
+ * step with the row shifts folded into the tables). */
 int photon_crc_set_generic_rows(int rows_per_step);
 
 /* The CRC-64 streaming kernel's shape: rows per step U and steps in flight D,

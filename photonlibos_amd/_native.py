@@ -48,6 +48,8 @@ def _declare(L):
     fn("photon_crc32c_batch_strided_sync", ctypes.c_int, vp, u64, u64, u64, u32, vp, vp, vp)
     fn("photon_crc32c_batch_iov", ctypes.c_int, vp, u64, u32, vp, vp, vp)
     fn("photon_crc32c_host_batch_strided", ctypes.c_int, vp, u64, u64, u64, u32, vp, vp)
+    fn("photon_crc32c_host_batch_strided_multi", ctypes.c_int, vp, u64, u64, u64, u32, vp, vp, ctypes.c_int)
+    fn("photon_crc32c_batch_strided_shards", ctypes.c_int, vp, ctypes.c_int)
     fn("photon_crc32c_batch_msg", ctypes.c_int, vp, vp, u64, u32, vp, vp, vp, vp)
     fn("photon_crc32c_combine_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp)
     fn("photon_crc64ecma_batch_strided", ctypes.c_int, vp, u64, u64, u64, u64, vp, vp, vp)

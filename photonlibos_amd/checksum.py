@@ -24,7 +24,8 @@ __all__ = [
     "crc32c_combine", "crc32c_combine_sw", "crc32c_combine_hw",
     "crc32c_combine_series", "crc32c_combine_series_sw", "crc32c_combine_series_hw",
     "crc32c_trim", "crc32c_trim_sw", "crc32c_trim_hw", "is_crc32c_hw_available",
-    "device_count", "set_lanes_per_buffer", "host_batch_strided", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
+    "device_count", "set_lanes_per_buffer", "host_batch_strided", "host_batch_strided_multi", "batch_strided_shards",
+    "Shard", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
     "crc64ecma_combine_series", "crc64ecma_trim",
     "batch64_strided", "batch64_iov", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
@@ -280,6 +281,35 @@ def host_batch_strided(base, stride, nbytes, count, out, seed=0, seeds=None):
                                                   _ptr(seeds), _ptr(out)))
 
 
+def host_batch_strided_multi(base, stride, nbytes, count, out, seed=0, seeds=None, ndev=0):
+    """host_batch_strided sharded over `ndev` devices of this process (0 = all),
+    one host thread per device. Synchronous."""
+    _check(lib().photon_crc32c_host_batch_strided_multi(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFF,
+                                                        _ptr(seeds), _ptr(out), ndev))
+
+
+class Shard(ctypes.Structure):
+    """photon_crc_shard (include/photon_crc/crc32c_gpu.h)."""
+    _fields_ = [("device", ctypes.c_int), ("d_base", ctypes.c_void_p), ("stride", ctypes.c_uint64),
+                ("nbytes", ctypes.c_uint64), ("count", ctypes.c_uint64), ("seed0", ctypes.c_uint32),
+                ("d_seeds", ctypes.c_void_p), ("d_out", ctypes.c_void_p), ("stream", ctypes.c_void_p)]
+
+
+def batch_strided_shards(shards):
+    """shards: list of dicts with Shard's fields (pointers as ints or .data_ptr()
+    objects). Enqueues batch_strided on every shard's device. Async."""
+    arr = (Shard * len(shards))()
+    for a, s in zip(arr, shards):
+        a.device = s.get("device", 0)
+        a.d_base = _ptr(s["d_base"])
+        a.stride, a.nbytes, a.count = s["stride"], s["nbytes"], s["count"]
+        a.seed0 = s.get("seed0", 0) & 0xFFFFFFFF
+        a.d_seeds = _ptr(s.get("d_seeds"))
+        a.d_out = _ptr(s["d_out"])
+        a.stream = _stream(s.get("stream"))
+    _check(lib().photon_crc32c_batch_strided_shards(arr, len(shards)))
+
+
 def batch_iov(iov, count, out, seed=0, seeds=None, stream=None):
     """out[i] = crc32c_extend(iov[i].base, iov[i].len, seed_i). Async."""
     _check(lib().photon_crc32c_batch_iov(_ptr(iov), count, seed & 0xFFFFFFFF, _ptr(seeds), _ptr(out),
@@ -389,7 +419,8 @@ def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
 
 
 def set_generic_rows(u):
-    """Generic batch kernel: rows per step (2, 4, 8)."""
+    """Batch kernel variant: 2, 4 (default), 8 = rows per step of the generic
+    kernel; 0 = the fused 4-row kernel."""
     _check(lib().photon_crc_set_generic_rows(u))
 
 

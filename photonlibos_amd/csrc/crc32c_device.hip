@@ -38,6 +38,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <photon/common/checksum/crc32c.h>
@@ -54,7 +55,10 @@ namespace {
 
 thread_local std::string g_err;
 int g_lanes_override = 0;
-int g_generic_u = 4;  // generic kernel: rows per step (2, 4, 8)
+// Batch kernel: rows per step of the generic kernel (2, 4, 8), or 0 = the
+// fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
+// the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
+int g_generic_u = 4;
 int g_stream_b = 1, g_stream_u = 4, g_stream_d = 3;  // streaming kernel: run blocks, rows/step, steps in flight
 // The streaming kernel is a tuning option: with the conflict-free rotated
 // tables the generic kernel measures faster on every config
@@ -173,6 +177,22 @@ int choose_lanes(uint64_t typical_len) {
     return 4;
 }
 
+FusedConsts make_fused_consts(int g) {
+    FusedConsts c;
+    for (int j = 0; j <= 4; ++j) c.xrow[j] = xpow(8ull * 16ull * (uint64_t)g * (uint64_t)j);
+    for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), c.basis[k]);
+    return c;
+}
+
+const FusedConsts& fused_consts(int g) {
+    static FusedConsts tab[7];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int lg = 2; lg <= 6; ++lg) tab[lg] = make_fused_consts(1 << lg);
+    });
+    return tab[g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2];
+}
+
 int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
     if (a.count == 0) return 0;
     int cus = 0;
@@ -182,8 +202,23 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
     const uint64_t gpw = 64 / g;
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
-    const LaneConsts& kc = lane_consts(g);
     if (grid > (uint64_t)cus) grid = cus;
+    if (g_generic_u == 0) {
+        const FusedConsts& fc = fused_consts(g);
+#define LF(GG) hipLaunchKernelGGL((crc32c_fused_kernel<GG>), dim3(grid), dim3(kBlock), 0, stream, a, fc)
+        switch (g) {
+            case 64: LF(64); break;
+            case 32: LF(32); break;
+            case 16: LF(16); break;
+            case 8: LF(8); break;
+            default: LF(4); break;
+        }
+#undef LF
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "crc32c_fused_kernel launch");
+        return 0;
+    }
+    const LaneConsts& kc = lane_consts(g);
 #define LB(GG, UU) hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc)
 #define LBG(UU)                    \
     switch (g) {                   \
@@ -400,6 +435,7 @@ constexpr int kNumStage = 3;
 constexpr uint64_t kStageBytes = 256ull << 20;
 
 struct HostPipe {
+    std::mutex mu;  // one host-memory batch at a time per device; devices run concurrently
     bool ready = false;
     hipStream_t copy = nullptr, comp = nullptr;
     void* stage[kNumStage] = {};
@@ -409,12 +445,11 @@ struct HostPipe {
     uint64_t out_cap = 0;
 };
 
-std::mutex g_pipe_mu;
-std::vector<HostPipe> g_pipes;
+constexpr int kMaxDevices = 64;
+HostPipe g_pipes[kMaxDevices];
 
-int pipe_for(int dev, HostPipe** out) {
-    if ((int)g_pipes.size() <= dev) g_pipes.resize(dev + 1);
-    HostPipe& p = g_pipes[dev];
+// The device's pipeline, created on first use; the caller holds p.mu.
+int pipe_init(HostPipe& p) {
     if (!p.ready) {
         hipError_t e;
         if ((e = hipStreamCreateWithFlags(&p.copy, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "stream");
@@ -428,7 +463,6 @@ int pipe_for(int dev, HostPipe** out) {
         }
         p.ready = true;
     }
-    *out = &p;
     return 0;
 }
 
@@ -466,8 +500,8 @@ int photon_crc_set_lanes_per_buffer(int g) {
 }
 
 int photon_crc_set_generic_rows(int rows_per_step) {
-    if (rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
-        return fail(-EINVAL, "rows per step must be 2, 4 or 8");
+    if (rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
+        return fail(-EINVAL, "rows per step must be 0 (fused kernel), 2, 4 or 8");
     g_generic_u = rows_per_step;
     return 0;
 }
@@ -542,9 +576,10 @@ int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    std::lock_guard<std::mutex> lk(g_pipe_mu);
-    HostPipe* p = nullptr;
-    int rc = pipe_for(dev, &p);
+    if (dev >= kMaxDevices) return fail(-ENODEV, "device index beyond the pipeline table");
+    HostPipe* p = &g_pipes[dev];
+    std::lock_guard<std::mutex> lk(p->mu);
+    int rc = pipe_init(*p);
     if (rc) return rc;
     hipError_t e;
     if (p->out_cap < count) {
@@ -581,6 +616,63 @@ int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64
     e = hipStreamSynchronize(p->comp);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return 0;
+}
+
+int photon_crc32c_host_batch_strided_multi(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                           uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out, int ndev) {
+    if (!count) return 0;
+    if (!h_base || !h_out || stride < nbytes) return fail(-EINVAL, "bad arguments");
+    int total = 0;
+    hipError_t e = hipGetDeviceCount(&total);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    std::vector<int> devs;
+    for (int d = 0; d < total && d < kMaxDevices; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            devs.push_back(d);
+    }
+    if (devs.empty()) return fail(-ENODEV, "photon_crc: no gfx950 device");
+    if (ndev > 0 && ndev < (int)devs.size()) devs.resize(ndev);
+    const uint64_t nd = devs.size() < count ? devs.size() : count;
+    // Contiguous slices of the buffer indices, one host thread per device, each
+    // driving that device's pipeline over its own host link.
+    std::vector<int> rcs(nd, 0);
+    std::vector<std::string> errs(nd);
+    std::vector<std::thread> th;
+    const uint8_t* src = static_cast<const uint8_t*>(h_base);
+    for (uint64_t k = 0; k < nd; ++k) {
+        const uint64_t lo = count * k / nd, hi = count * (k + 1) / nd;
+        th.emplace_back([&, k, lo, hi] {
+            hipError_t se = hipSetDevice(devs[k]);
+            rcs[k] = se != hipSuccess ? hip_fail(se, "hipSetDevice")
+                                      : photon_crc32c_host_batch_strided(src + lo * stride, stride, nbytes, hi - lo,
+                                                                         seed0, h_seeds ? h_seeds + lo : nullptr,
+                                                                         h_out + lo);
+            if (rcs[k]) errs[k] = g_err;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (uint64_t k = 0; k < nd; ++k)
+        if (rcs[k]) return fail(rcs[k], "device " + std::to_string(devs[k]) + ": " + errs[k]);
+    return 0;
+}
+
+int photon_crc32c_batch_strided_shards(const photon_crc_shard* shards, int nshards) {
+    if (nshards < 0 || (nshards && !shards)) return fail(-EINVAL, "bad shard list");
+    int prev = -1;
+    hipError_t e = hipGetDevice(&prev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    int rc = 0;
+    for (int i = 0; i < nshards && !rc; ++i) {
+        const photon_crc_shard& s = shards[i];
+        if ((e = hipSetDevice(s.device)) != hipSuccess) {
+            rc = hip_fail(e, "hipSetDevice");
+            break;
+        }
+        rc = photon_crc32c_batch_strided(s.d_base, s.stride, s.nbytes, s.count, s.seed0, s.d_seeds, s.d_out, s.stream);
+    }
+    (void)hipSetDevice(prev);
+    return rc;
 }
 
 int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint32_t seed0,

@@ -316,6 +316,276 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
     }
 }
 
+// ----------------------------------------------------------------- fused path
+// Four rows per step with the row shifts folded into the tables. Over a step
+// of rows u = 0..3 (X = x^(8*16*G), the shift of one row of the column):
+//     P <- P * X^4  ^  sum_u crc16(block_u) * X^(3-u)
+// crc16(b) = D(y) where y is the CRC register after the block's first three
+// word steps, so crc16(b_u) * X^(3-u) = E_{3-u}(y_u) with E_j = D * X^j: one
+// 4-lookup table step per block replaces the final D step AND the S step. Per
+// 16 bytes a lane does 12 D + 4 E lookups + 1 S4 lookup (17, down from 20).
+//
+// LDS (152 KiB, one 1024-thread workgroup per CU):
+//   [0, 64K)    row idx (256 B): D at t*32 + r*4, S4 (P -> P*X^4) at 128 + t*32 + r*4
+//   [64K,128K)  row idx (256 B): slot m = 0..6 at m*32 + t*8 + e*4 holds E_{3-(m%4)}
+//   [128K,152K) R_k lane-combine tables (as kRBase above)
+// Lane l: q = (l>>1)&3 (byte rotation), D replica r = (l&1) | ((l>>3)&3)<<1,
+// E replica e = l&1, rotation g = (l>>3)&3. In E-lookup k the lane reads slot
+// m = k + g, i.e. it feeds block (k+g)%4's register through E_{3-((k+g)%4)}:
+// the 32 lanes of a ds_read group hit 32 distinct banks (m%4, t, e) with only
+// two E replicas, and the per-lane slot is the per-lane base g*32 plus the
+// instruction's immediate k*32 (slots 4..6 repeat 0..2 so no wrap is needed).
+// All rows of a buffer are full: the block grid is aligned to the END of the
+// buffer (pad = rows*G - nblocks zero blocks in front of block 0, plus whole
+// zero rows so rows % 4 == 0). Leading zeros do not change a CRC column that
+// starts at 0, so every step is a full fused step and lane l always ends
+// G-1-l blocks before the end.
+constexpr uint32_t kFRegionE = 65536u;
+constexpr uint32_t kFRBase = 131072u;
+constexpr uint32_t kFLdsBytes = kFRBase + kRBytes;           // 155648 B
+
+struct FusedConsts {
+    uint32_t xrow[5];          // X^0..X^4, X = x^(8*16*G) mod P
+    uint32_t basis[6][32];     // basis of x^(128 * 2^k) mod P (lane combine)
+};
+
+struct FusedLane {
+    uint32_t rot;      // 8*q
+    uint32_t off[4];   // D/S: ((i+q)%4)*32 + r*4
+    uint32_t offe[4];  // E:   1<<16 | g*32 + ((i+q)%4)*8 + e*4
+    uint32_t r4;       // r*4 (byte-serial tail, D slice 3)
+    uint32_t g;        // block rotation of the E lookups
+};
+
+__device__ __forceinline__ FusedLane fused_lane(uint32_t lane) {
+    FusedLane f;
+    const uint32_t q = (lane >> 1) & 3u;
+    const uint32_t r = (lane & 1u) | (((lane >> 3) & 3u) << 1);
+    const uint32_t e = lane & 1u;
+    f.g = (lane >> 3) & 3u;
+    f.rot = 8u * q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t t = (i + q) & 3u;
+        f.off[i] = (t << 5) | (r << 2);
+        f.offe[i] = (1u << 16) | (f.g << 5) | (t << 3) | (e << 2);
+    }
+    f.r4 = r << 2;
+    return f;
+}
+
+template <int I, uint32_t TOFF>
+__device__ __forceinline__ uint32_t flook(const uint32_t* lds, uint32_t xr, const FusedLane& a) {
+    return lds_word(lds, __builtin_amdgcn_perm(xr, a.off[I], 0x0C0C0000u | ((4u + I) << 8)) + TOFF);
+}
+
+// E lookup: bytes {offe.b0, xr.b_I, offe.b2 (= 1: region E), 0}; slot offset K*32.
+template <int I, int K>
+__device__ __forceinline__ uint32_t elook(const uint32_t* lds, uint32_t xr, const FusedLane& a) {
+    return lds_word(lds, __builtin_amdgcn_perm(xr, a.offe[I], 0x0C020000u | ((4u + I) << 8)) + 32u * K);
+}
+
+__device__ __forceinline__ uint32_t fdstep(const uint32_t* lds, uint32_t x, const FusedLane& a, uint32_t e) {
+    const uint32_t xr = __builtin_amdgcn_alignbit(x, x, a.rot);
+    return xor3(xor3(flook<0, 0>(lds, xr, a), flook<1, 0>(lds, xr, a), flook<2, 0>(lds, xr, a)),
+                flook<3, 0>(lds, xr, a), e);
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t festep(const uint32_t* lds, uint32_t x, const FusedLane& a, uint32_t e) {
+    const uint32_t xr = __builtin_amdgcn_alignbit(x, x, a.rot);
+    return xor3(xor3(elook<0, K>(lds, xr, a), elook<1, K>(lds, xr, a), elook<2, K>(lds, xr, a)),
+                elook<3, K>(lds, xr, a), e);
+}
+
+__device__ __forceinline__ uint32_t fsstep(const uint32_t* lds, uint32_t p, const FusedLane& a) {
+    const uint32_t pr = __builtin_amdgcn_alignbit(p, p, a.rot);
+    return xor3(xor3(flook<0, kSOff>(lds, pr, a), flook<1, kSOff>(lds, pr, a), flook<2, kSOff>(lds, pr, a)),
+                flook<3, kSOff>(lds, pr, a), 0u);
+}
+
+__device__ __forceinline__ uint32_t fbytestep(const uint32_t* lds, uint32_t c, uint8_t b, const FusedLane& a) {
+    const uint32_t x = (c ^ b) & 0xffu;
+    return lds_word(lds, (x << 8) + 3u * 32u + a.r4) ^ (c >> 8);
+}
+
+// One fused step over the 4 rows w[0..3] of this lane's column.
+__device__ __forceinline__ uint32_t fused_step(const uint32_t* lds, uint32_t p, const uint4 (&w)[4],
+                                               const FusedLane& a) {
+    uint32_t y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        uint32_t c = fdstep(lds, w[u].x, a, w[u].y);
+        c = fdstep(lds, c, a, w[u].z);
+        y[u] = fdstep(lds, c, a, w[u].w);
+    }
+    // z[k] = y[(k+g)%4]: rotate the four registers by g (two select levels).
+    uint32_t h[4], z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h[k] = (a.g & 1u) ? y[(k + 1) & 3] : y[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = (a.g & 2u) ? h[(k + 2) & 3] : h[k];
+    uint32_t s = fsstep(lds, p, a);
+    s = festep<0>(lds, z[0], a, s);
+    s = festep<1>(lds, z[1], a, s);
+    s = festep<2>(lds, z[2], a, s);
+    return festep<3>(lds, z[3], a, s);
+}
+
+__device__ __forceinline__ void build_tables_fused(uint32_t* lds, const FusedConsts& kc) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t = tid >> 8, b = tid & 255u;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & kc.basis[k][8 * t + j];
+        lds[kFRBase / 4 + k * 1024 + t * 256 + b] = r;
+    }
+    const uint32_t v = b << (8 * t);
+    uint32_t ev[4];
+    ev[0] = mulmod(v, 0x82f63b78u);  // D: v * x^32
+#pragma unroll
+    for (int j = 1; j < 4; ++j) ev[j] = mulmod(ev[0], kc.xrow[j]);
+    const uint32_t sv = mulmod(v, kc.xrow[4]);
+    const uint32_t base = ((b << 8) + (t << 5)) >> 2;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        lds[base + r] = ev[0];
+        lds[base + kSOff / 4 + r] = sv;
+    }
+    const uint32_t ebase = (kFRegionE + (b << 8) + (t << 3)) >> 2;
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+        const uint32_t val = ev[3 - (m & 3)];
+        lds[ebase + m * 8] = val;
+        lds[ebase + m * 8 + 1] = val;
+    }
+    __syncthreads();
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_reduce_f(uint32_t pc, uint32_t d, const uint32_t* lds) {
+    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
+#pragma unroll
+    for (int k = 0; k < LOG2G; ++k) {
+        const uint32_t* R = lds + kFRBase / 4 + k * 1024;
+        const uint32_t m = xor3(xor3(R[pc & 0xffu], R[256 + ((pc >> 8) & 0xffu)], R[512 + ((pc >> 16) & 0xffu)]),
+                                R[768 + (pc >> 24)], 0u);
+        pc = ((d >> k) & 1u) ? m : pc;
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
+    return pc;
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc32c_fused_kernel(BatchArgs args, FusedConsts kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kFLdsBytes / 4];
+    build_tables_fused(lds, kc);
+
+    constexpr int GPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = wave_id();
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const FusedLane la = fused_lane(lane);
+
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.count; wv += nwaves) {
+        const uint64_t bi = wv * GPW + grp;
+        const bool active = bi < args.count;
+        const uint8_t* p = nullptr;
+        uint64_t n = 0;
+        uint32_t seed = args.seed0;
+        if (active) {
+            if (args.iov) {
+                p = static_cast<const uint8_t*>(args.iov[bi].base);
+                n = args.iov[bi].len;
+            } else {
+                p = args.base + bi * args.stride;
+                n = args.nbytes;
+            }
+            if (args.seeds) seed = args.seeds[bi];
+        }
+
+        uint32_t crc;
+        if (n < 64) {
+            crc = seed;
+            if (gl == 0)
+                for (uint64_t k = 0; k < n; ++k) crc = fbytestep(lds, crc, load8(p + k), la);
+        } else {
+            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+            const uint8_t* e = p + n;
+            const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
+            const int s0 = (int)(p - a0);
+            const int64_t nb = (int64_t)((uint64_t)(eb - a0) >> 4);  // >= 3
+            const int64_t rows = (nb + G - 1) / G;
+            const int64_t steps = (rows + 3) / 4;
+            const int64_t pad = rows * G - nb;                   // zero blocks before block 0
+            const int64_t zr = steps * 4 - rows;                 // zero rows before that
+            // Block index of this lane in grid row R: (R - zr)*G + gl - pad.
+            const int64_t b0 = (int64_t)gl - pad - zr * G;
+
+            // First two steps: blocks may precede block 0 (zeros) or be blocks
+            // 0/1 (masked head + seed).
+            auto load_checked = [&](int64_t s, uint4 (&w)[4]) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t bidx = b0 + (4 * s + u) * G;
+                    uint4 v = make_uint4(0, 0, 0, 0);
+                    if (bidx >= 0) {
+                        v = load16(a0 + 16 * bidx);
+                        if (bidx < 2) {
+                            const int off = (int)bidx * 16;
+                            v.x = head_word(v.x, off, s0, seed);
+                            v.y = head_word(v.y, off + 4, s0, seed);
+                            v.z = head_word(v.z, off + 8, s0, seed);
+                            v.w = head_word(v.w, off + 12, s0, seed);
+                        }
+                    }
+                    w[u] = v;
+                }
+            };
+            const uint8_t* lp = a0 + 16 * b0;  // grid row 0 of this lane (may precede a0)
+            auto load_step = [&](int64_t s, uint4 (&w)[4]) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) w[u] = load16(lp + (4 * s + u) * (16 * G));
+            };
+
+            // Double-buffered: the next step's 4 rows are in flight while this
+            // one is reduced (deeper rings measured slower: more VGPRs, same HBM).
+            uint32_t pc = 0;
+            {
+                uint4 cur[4];
+                load_checked(0, cur);
+                int64_t s = 0;
+                if (steps > 1) {
+                    uint4 nxt[4];
+                    load_checked(1, nxt);
+                    pc = fused_step(lds, pc, cur, la);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+                    s = 1;
+                }
+                for (; s + 1 < steps; ++s) {
+                    uint4 nxt[4];
+                    load_step(s + 1, nxt);
+                    pc = fused_step(lds, pc, cur, la);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+                }
+                pc = fused_step(lds, pc, cur, la);
+            }
+
+            crc = group_reduce_f<G>(pc, G - 1 - gl, lds);
+            if (gl == 0)
+                for (const uint8_t* q = eb; q < e; ++q) crc = fbytestep(lds, crc, load8(q), la);
+        }
+        if (active && gl == 0) args.out[bi] = crc;
+    }
+}
+
 // ------------------------------------------------------------ streaming path
 // Uniform batches: base and stride 16-byte aligned, nbytes = R*16*B*G with
 // R % U == 0. A row is B*G consecutive 16-byte blocks; load b of a row is the

@@ -78,6 +78,10 @@ def test_device_calls_fail_loudly_without_gpu():
         ck.batch_strided(0x1000, 4096, 4096, 1, 0x2000)
     with pytest.raises(ck.CrcError):
         ck.file_strided(0, 0, 4096, 4096, 1)
+    with pytest.raises(ck.CrcError):
+        ck.host_batch_strided_multi(0x1000, 4096, 4096, 1, 0x2000)
+    with pytest.raises(ck.CrcError):
+        ck.batch_strided_shards([dict(device=0, d_base=0x1000, stride=4096, nbytes=4096, count=1, d_out=0x2000)])
 
 
 def test_argument_validation():

@@ -30,6 +30,12 @@ def _reset_lanes():
     yield
     ck.set_lanes_per_buffer(0)
     ck.set_stream_config(0, 0, 0)
+    ck.set_generic_rows(4)
+
+
+# Batch kernel variants: 4 = the generic kernel (default), 0 = the fused
+# 4-row kernel (a tuning option).
+VARIANTS = [4, 0]
 
 
 STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (0, 0, 0)]
@@ -71,15 +77,18 @@ def test_golden_512(torch_dev, golden_in):
     assert list(got) == golden_in["crc32c"]
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("g", [0, 4, 64])
-def test_alphabet_lengths_0_4096(torch_dev, ref_vectors, g):
+def test_alphabet_lengths_0_4096(torch_dev, ref_vectors, g, variant):
+    ck.set_generic_rows(variant)
     ck.set_lanes_per_buffer(g)
     d = to_dev(torch_dev, ALPHA)
     got = run_iov(torch_dev, d, [0] * 4097, list(range(4097)))
     assert list(got) == ref_vectors["alphabet_crc32c"]
 
 
-def test_reference_random_vectors(torch_dev, ref_vectors):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_reference_random_vectors(torch_dev, ref_vectors, variant):
     # Outputs of the reference's own crc.cpp on seeded data, with misaligned
     # starts (1..15) and non-zero seeds, lengths 1 .. 1 MiB.
     rv = ref_vectors
@@ -92,13 +101,16 @@ def test_reference_random_vectors(torch_dev, ref_vectors):
     for o, n, st in zip(offs, rv["rand_len"], rv["rand_stream"]):
         host[o:o + n] = datagen.stream_bytes(st, n)
     d = to_dev(torch_dev, host)
-    for g in (0, 8, 32):
+    ck.set_generic_rows(variant)
+    for g in (0, 4, 8, 16, 32, 64):
         ck.set_lanes_per_buffer(g)
         got = run_iov(torch_dev, d, offs, rv["rand_len"], seeds=rv["rand_seed"])
         assert list(got) == rv["rand_crc32c"], g
 
 
-def test_every_length_and_alignment(torch_dev, oracle):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_every_length_and_alignment(torch_dev, oracle, variant):
+    ck.set_generic_rows(variant)
     host = datagen.stream_bytes(0x1234, 1 << 16)
     d = to_dev(torch_dev, host)
     rnd = random.Random(1)
@@ -113,10 +125,12 @@ def test_every_length_and_alignment(torch_dev, oracle):
     assert list(got) == want
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("g", [4, 8, 16, 32, 64])
 @pytest.mark.parametrize("nbytes,stride", [(64, 64), (100, 112), (1000, 1000), (4096, 4096), (8192, 8192),
                                            (65536, 65536), (65536 + 7, 65536 + 16), (300000, 300001)])
-def test_strided_all_lane_groups(torch_dev, oracle, g, nbytes, stride):
+def test_strided_all_lane_groups(torch_dev, oracle, g, nbytes, stride, variant):
+    ck.set_generic_rows(variant)
     ck.set_lanes_per_buffer(g)
     count = max(3, min(97, (8 << 20) // stride))
     host = datagen.stream_bytes(g * 1000 + nbytes, stride * count + 64)
@@ -179,7 +193,10 @@ def test_full_c2_4gib(torch_dev, oracle):
     ck.set_stream_config(1, 4, 3)  # the streaming kernel
     c = run_strided(torch_dev, d, nbytes, nbytes, count)
     ck.set_stream_config(0, 0, 0)
-    assert np.array_equal(a, b) and np.array_equal(a, c)
+    ck.set_generic_rows(0)  # the fused kernel
+    e = run_strided(torch_dev, d, nbytes, nbytes, count)
+    ck.set_generic_rows(4)
+    assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, e)
     rnd = random.Random(2)
     for i in [0, 1, count - 1] + [rnd.randrange(count) for _ in range(61)]:
         assert a[i] == oracle.crc32c(datagen.stream_bytes(0x5EED0001 + i, nbytes)), i
@@ -314,3 +331,30 @@ def test_host_batch_pipeline(torch_dev, oracle):
     h = host.numpy()
     for i in list(range(0, count, 97)) + [count - 1]:
         assert got[i] == oracle.crc32c(h[i * stride:i * stride + nbytes], i), i
+    # The same batch sharded over this process's devices (all; then one)
+    # gives the same CRCs (every device visible here takes a slice).
+    for ndev in (0, 1):
+        out2 = torch_dev.zeros(count, dtype=torch_dev.int32, pin_memory=True)
+        ck.host_batch_strided_multi(host, stride, nbytes, count, out2, seeds=seeds, ndev=ndev)
+        assert np.array_equal(out2.numpy(), out.numpy()), ndev
+
+
+def test_device_shards(torch_dev, oracle):
+    # photon_crc32c_batch_strided_shards: two shards (halves, different seeds)
+    # enqueued on the device(s); equal to one batch per half.
+    nbytes, count = 4096, 1000
+    d = torch_dev.empty(nbytes * count, dtype=torch_dev.uint8, device="cuda")
+    ck.fill_splitmix(d, nbytes, nbytes, count, 0x5EED0001)
+    out = torch_dev.zeros(count, dtype=torch_dev.int32, device="cuda")
+    half = count // 2
+    ck.batch_strided_shards([
+        dict(device=0, d_base=d.data_ptr(), stride=nbytes, nbytes=nbytes, count=half, seed0=0,
+             d_out=out.data_ptr()),
+        dict(device=0, d_base=d.data_ptr() + half * nbytes, stride=nbytes, nbytes=nbytes, count=count - half,
+             seed0=0xABCDEF01, d_out=out.data_ptr() + 4 * half),
+    ])
+    torch_dev.cuda.synchronize()
+    got = u32(out)
+    for i in (0, 1, half - 1, half, count - 1):
+        want = oracle.crc32c(datagen.stream_bytes(0x5EED0001 + i, nbytes), 0 if i < half else 0xABCDEF01)
+        assert got[i] == want, i
