@@ -55,6 +55,8 @@ def parse(argv=None):
                     help="untimed steps; the first ~10 back-to-back launches run slower while clocks settle")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--h2d", action="store_true", help="host-memory end-to-end rate (for DESIGN.md)")
+    ap.add_argument("--h2d-devices", type=int, default=1,
+                    help="with --h2d: shard the host batch over this many devices of ONE process (0 = all)")
     ap.add_argument("--file-records", action="store_true", help="file records through the pread pipeline (DESIGN.md)")
     ap.add_argument("--rpc-batch", action="store_true", help="CheckedMessage batch over pinned host payloads (DESIGN.md)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
@@ -235,12 +237,17 @@ def run_h2d(args, stream):
     del dev
     torch.cuda.synchronize()
     out = torch.zeros(cnt, dtype=torch.int32, pin_memory=True)
-    step = lambda: ck.host_batch_strided(host, n, n, cnt, out)  # noqa: E731
+    ndev = args.h2d_devices
+    if ndev == 1:
+        step = lambda: ck.host_batch_strided(host, n, n, cnt, out)  # noqa: E731
+    else:
+        step = lambda: ck.host_batch_strided_multi(host, n, n, cnt, out, ndev=ndev)  # noqa: E731
+    used = torch.cuda.device_count() if ndev <= 0 else min(ndev, torch.cuda.device_count())
     steps = max(2, min(args.steps, 10))
     elapsed, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
     ok = ck.crc32c_hw(host[:n].numpy().tobytes()) == int(out[0].item()) & 0xFFFFFFFF
     print(json.dumps({"metric": "GiB/s CRC32C host-resident (pinned) end to end: H2D + kernel + D2H",
-                      "value": round(n * cnt * steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
+                      "value": round(n * cnt * steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": used,
                       "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 3), "self_check": ok,
                       "config": {"workload": cfg["workload"].replace("device-resident", "pinned host memory")}}))
 

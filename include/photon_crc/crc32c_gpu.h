@@ -201,6 +201,11 @@ int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
  * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
 int photon_crc64_set_interleave(int partials);
 
+/* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
+ * each lane reads two consecutive 16-byte blocks per row, one row shift per
+ * 32 bytes (lanes per buffer <= 32; overrides the interleave). */
+int photon_crc64_set_run_blocks(int blocks);
+
 /* Producers outside device memory.
  * photon_crc_host_register: make an existing host range (e.g. the iovec
  * targets of IFile::preadv, fs/filesystem.h:54-70) readable by the kernels in

@@ -424,6 +424,11 @@ def set_generic_rows(u):
     _check(lib().photon_crc_set_generic_rows(u))
 
 
+def set_stream64_run_blocks(b):
+    """CRC-64 streaming kernel: 16-byte blocks per lane run (1, 2)."""
+    _check(lib().photon_crc64_set_run_blocks(b))
+
+
 def set_stream64_interleave(v):
     """CRC-64 streaming kernel: interleaved row partials per lane (1, 2, 4)."""
     _check(lib().photon_crc64_set_interleave(v))

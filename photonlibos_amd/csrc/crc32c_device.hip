@@ -284,10 +284,17 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
 
 // CRC-64 streaming kernel shape (rows per step, steps in flight, interleaved
 // partials per lane).
-int g_stream64_u = 4, g_stream64_d = 3, g_stream64_v = 1;
+int g_stream64_u = 4, g_stream64_d = 3, g_stream64_v = 1, g_stream64_b = 1;
 
 template <int G, int U, int D>
 void launch_uniform64_v(const Uniform64Args& a, dim3 grid, hipStream_t st) {
+    if constexpr (G <= 32) {
+        if (g_stream64_b == 2) {
+            hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, 1, 2>), grid, dim3(kBlock), 0, st, a,
+                               lane_consts64(2 * G));
+            return;
+        }
+    }
     constexpr int V2 = (G <= 32 && U % 2 == 0) ? 2 : 1;
     constexpr int V4 = (G <= 16 && U % 4 == 0) ? 4 : V2;
     if (g_stream64_v >= 4)
@@ -305,6 +312,9 @@ bool launch_uniform64_g(const Uniform64Args& a, dim3 grid, hipStream_t st) {
     else if (u == 4 && d == 3) launch_uniform64_v<G, 4, 3>(a, grid, st);
     else if (u == 2 && d == 4) launch_uniform64_v<G, 2, 4>(a, grid, st);
     else if (u == 8 && d == 1) launch_uniform64_v<G, 8, 1>(a, grid, st);
+    else if (u == 2 && d == 2) launch_uniform64_v<G, 2, 2>(a, grid, st);
+    else if (u == 2 && d == 3) launch_uniform64_v<G, 2, 3>(a, grid, st);
+    else if (u == 4 && d == 1) launch_uniform64_v<G, 4, 1>(a, grid, st);
     else return false;
     return true;
 }
@@ -313,7 +323,8 @@ int try_launch_uniform64(const uint8_t* base, uint64_t stride, uint64_t nbytes, 
                          const uint64_t* seeds, uint64_t* out, hipStream_t stream) {
     if (!g_stream64_enabled || count == 0) return 1;
     const int g = choose_lanes(nbytes);
-    const uint64_t row = 16ull * g;
+    const int b = (g_stream64_b == 2 && g <= 32) ? 2 : 1;
+    const uint64_t row = 16ull * g * b;
     if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
     const uint64_t rows = nbytes / row;
     if (rows % (uint64_t)g_stream64_u) return 1;
@@ -520,6 +531,12 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
     return 0;
 }
 
+int photon_crc64_set_run_blocks(int blocks) {
+    if (blocks != 1 && blocks != 2) return fail(-EINVAL, "run blocks must be 1 or 2");
+    g_stream64_b = blocks;
+    return 0;
+}
+
 int photon_crc64_set_interleave(int partials) {
     if (partials != 1 && partials != 2 && partials != 4) return fail(-EINVAL, "interleave must be 1, 2 or 4");
     g_stream64_v = partials;
@@ -532,7 +549,7 @@ int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight) {
         g_stream64_enabled = false;
         return 0;
     }
-    if (!((u == 4 && (d == 2 || d == 3)) || (u == 2 && d == 4) || (u == 8 && d == 1)))
+    if (!((u == 4 && (d >= 1 && d <= 3)) || (u == 2 && (d >= 2 && d <= 4)) || (u == 8 && d == 1)))
         return fail(-EINVAL, "unsupported CRC-64 (rows_per_step, steps_in_flight)");
     g_stream64_enabled = true;
     g_stream64_u = u;

@@ -55,7 +55,12 @@ def make(v, lanes):
             ck.set_lanes_per_buffer(lanes)
             if v == "g64":
                 ck.set_stream64_config(0, 0)
+            elif v.startswith("s64b2"):
+                parts = v.split(":")
+                ck.set_stream64_config(int(parts[1]), int(parts[2]))
+                ck.set_stream64_run_blocks(2)
             else:
+                ck.set_stream64_run_blocks(1)
                 parts = v.split(":")
                 ck.set_stream64_config(int(parts[1]), int(parts[2]))
                 ck.set_stream64_interleave(int(parts[3]) if len(parts) > 3 else 2)
@@ -91,6 +96,7 @@ for r in range(args.rounds):
 ck.set_stream_config(0, 0, 0)
 ck.set_stream64_config(4, 3)
 ck.set_stream64_interleave(1)
+ck.set_stream64_run_blocks(1)
 ck.set_generic_rows(4)
 ck.set_lanes_per_buffer(0)
 rows = []

@@ -95,20 +95,23 @@ def test_strided(torch_dev, oracle, g):
             assert int(got[i]) == oracle.crc64ecma(datagen.stream_bytes(0x640 + nbytes + i, nbytes), 0x1234), i
 
 
-@pytest.mark.parametrize("v", [1, 2, 4])
-@pytest.mark.parametrize("shape", [(4, 2), (4, 3), (2, 4), (8, 1), None])
+@pytest.mark.parametrize("v", [1, 2, 4, "b2"])
+@pytest.mark.parametrize("shape", [(4, 2), (4, 3), (2, 4), (8, 1), (4, 1), (2, 2), (2, 3), None])
 @pytest.mark.parametrize("g", [8, 32, 64])
 def test_streaming_shapes(torch_dev, oracle, shape, g, v):
     # The CRC-64 streaming kernel (uniform batches) in every shape and row
     # interleave, with seed0, per-buffer seeds and no seed; counts that do not
-    # fill whole wave tuples.
+    # fill whole wave tuples. v = "b2": runs of two blocks per lane.
     if shape is None:
         if v != 1:
             pytest.skip("generic kernel has no interleave")
         ck.set_stream64_config(0, 0)  # generic kernel only
     else:
         ck.set_stream64_config(*shape)
-        ck.set_stream64_interleave(v)
+        if v == "b2":
+            ck.set_stream64_run_blocks(2)
+        else:
+            ck.set_stream64_interleave(v)
     ck.set_lanes_per_buffer(g)
     try:
         for nbytes, count in ((16 * 64 * 8, 37), (65536, 301), (4096, 1001)):
@@ -128,6 +131,7 @@ def test_streaming_shapes(torch_dev, oracle, shape, g, v):
     finally:
         ck.set_stream64_config(4, 3)
         ck.set_stream64_interleave(1)
+        ck.set_stream64_run_blocks(1)
 
 
 def test_full_c2_crc64(torch_dev, oracle):
