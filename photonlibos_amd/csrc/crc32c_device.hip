@@ -16,18 +16,21 @@
 // U blocks a lane holds are reduced in parallel and only the cheap shift is
 // on the loop-carried chain. All GF(2) products by constants are byte-sliced
 // LDS table lookups (no carry-less multiply on CDNA4, no MFMA: this is GF(2)):
-//   D tables: x -> x * x^32 mod P, 4 byte slices, replicated 32x so that lane
-//             l always hits bank l%32 (conflict-free random lookups), 128 KiB;
-//   S tables: P -> P * x^(8*16*G) mod P, 4 slices, 4 replicas, 16 KiB.
+//   D tables: x -> x * x^32 mod P and S tables: P -> P * x^(8*16*G) mod P,
+//             4 byte slices x 8 replicas each, 64 KiB together; lanes take
+//             the slices in a per-lane rotated order so the 32 lanes of a
+//             ds_read group always hit 32 distinct banks (crc32c_kernels.h).
 // At the end lane l multiplies its partial by x^(128*d_l), d_l = number of
-// 16-byte blocks between its last block and the end (constant-basis GF(2)
-// multiplies on the bits of d_l), and the group XOR-reduces with __shfl_xor.
+// 16-byte blocks between its last block and the end (byte-sliced R_k tables
+// of x^(128*2^k) on the bits of d_l), and the group XOR-reduces with
+// __shfl_xor.
 // Unaligned heads use zero-prefix invariance (crc.md:24-32): the leading
 // bytes of the first aligned block are masked to 0 and the seed is XORed into
 // the first four data bytes (init-value linearity), so every load is an
 // aligned 16-byte load. Ragged tails (<16 B) are finished byte-serially.
-// Uniform batches (aligned, equal length, whole rows) take a streaming kernel
-// whose load ring runs continuously across buffer boundaries.
+// Options (tuning, parity-tested, off by default because they measured
+// slower): a streaming kernel whose load ring runs continuously across buffer
+// boundaries, and a fused kernel with the row shifts folded into the tables.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>

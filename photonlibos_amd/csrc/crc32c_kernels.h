@@ -781,14 +781,46 @@ __device__ __forceinline__ uint32_t shift_bytes_tab(uint32_t crc, uint64_t n, co
     return crc;
 }
 
+// x^(8n) mod P: product of the x^(8*2^i) entries over the set bits of n.
+__device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
+    uint32_t k = kOne;
+    for (int i = 0; n; ++i, n >>= 1)
+        if (n & 1) k = mulmod(k, t.x8pow2[i]);
+    return k;
+}
+
+// One thread per message. The segments' lengths and CRCs are loaded 8 at a
+// time before the (dependent) fold, and the shift constant x^(8*len) is
+// recomputed only when the length changes (messages of equal-size segments
+// pay one mulmod per segment).
 __global__ void crc32c_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_t* msg_start, uint64_t nmsg,
                                        const uint32_t* seg_crc, uint32_t seed0, const uint32_t* seeds,
                                        uint32_t* out, PowTable pt) {
     const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= nmsg) return;
+    const uint64_t s0 = msg_start[m], s1 = msg_start[m + 1];
     uint32_t acc = seeds ? seeds[m] : seed0;
-    for (uint64_t s = msg_start[m]; s < msg_start[m + 1]; ++s)
-        acc = shift_bytes_tab(acc, iov[s].len, pt) ^ seg_crc[s];
+    uint64_t klen = 0;
+    uint32_t k = kOne;  // x^(8*klen)
+    for (uint64_t s = s0; s < s1; s += 8) {
+        uint64_t len[8];
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (s + j < s1) {
+                len[j] = iov[s + j].len;
+                c[j] = seg_crc[s + j];
+            }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (s + j < s1) {
+                if (len[j] != klen) {
+                    k = xpow8_tab(len[j], pt);
+                    klen = len[j];
+                }
+                acc = mulmod(acc, k) ^ c[j];
+            }
+    }
     out[m] = acc;
 }
 
