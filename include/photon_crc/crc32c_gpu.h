@@ -172,6 +172,23 @@ int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t
 int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint64_t seed0,
                                const uint64_t* d_seeds, uint64_t* d_out, void* stream);
 
+/* CRC-64/ECMA forms of the CRC32C calls above (crc64ecma.h:20-87):
+ *   combine_batch: d_out[i] = crc64ecma_combine(d_crc1[i], d_crc2[i], d_len2[i])
+ *                  (crc1 == 0 -> crc2, as the reference);
+ *   batch_msg_n:   d_out[m] = crc64ecma_extend chained over message m's
+ *                  segments from seed_m (e.g. an OSS object's iovector,
+ *                  ecosystem/oss.h:217 expected_crc64); d_seg_out[s] = each
+ *                  segment's crc64ecma(seg, 0); nseg == d_msg_start[nmsg];
+ *   extend_device: *d_out = crc64ecma_extend(d_data, nbytes, seed) for ONE
+ *                  long device buffer (split, run in parallel, folded). */
+int photon_crc64ecma_combine_batch(const uint64_t* d_crc1, const uint64_t* d_crc2, const uint32_t* d_len2,
+                                   uint64_t count, uint64_t* d_out, void* stream);
+int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                                 uint64_t nseg, uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_seg_out,
+                                 uint64_t* d_out, void* stream);
+int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,
+                                   void* stream);
+
 /* Synchronous convenience: photon_crc32c_batch_strided + stream sync. */
 int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                      uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream);

@@ -28,7 +28,7 @@ __all__ = [
     "Shard", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
     "crc64ecma_combine_series", "crc64ecma_trim",
-    "batch64_strided", "batch64_iov", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
+    "batch64_strided", "batch64_iov", "combine64_batch", "batch64_msg_n", "extend64_device", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
 _CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
@@ -338,6 +338,24 @@ def batch64_iov(iov, count, out, seed=0, seeds=None, stream=None):
     """out[i] = crc64ecma_extend(iov[i].base, iov[i].len, seed_i) (uint64 out). Async."""
     _check(lib().photon_crc64ecma_batch_iov(_ptr(iov), count, seed & 0xFFFFFFFFFFFFFFFF, _ptr(seeds), _ptr(out),
                                             _stream(stream)))
+
+
+def combine64_batch(crc1, crc2, len2, count, out, stream=None):
+    """out[i] = crc64ecma_combine(crc1[i], crc2[i], len2[i]) (uint64 crcs, uint32 lengths). Async."""
+    _check(lib().photon_crc64ecma_combine_batch(_ptr(crc1), _ptr(crc2), _ptr(len2), count, _ptr(out),
+                                                _stream(stream)))
+
+
+def batch64_msg_n(iov, msg_start, nmsg, nseg, seg_out, out, seed=0, seeds=None, stream=None):
+    """out[m] = crc64ecma_extend chained over message m's segments (uint64). Async."""
+    _check(lib().photon_crc64ecma_batch_msg_n(_ptr(iov), _ptr(msg_start), nmsg, nseg, seed & 0xFFFFFFFFFFFFFFFF,
+                                              _ptr(seeds), _ptr(seg_out), _ptr(out), _stream(stream)))
+
+
+def extend64_device(data, nbytes, out, seed=0, stream=None):
+    """*out = crc64ecma_extend(data, nbytes, seed) for one long device buffer. Async."""
+    _check(lib().photon_crc64ecma_extend_device(_ptr(data), nbytes, seed & 0xFFFFFFFFFFFFFFFF, _ptr(out),
+                                                _stream(stream)))
 
 
 def combine_batch(crc1, crc2, len2, count, out, stream=None):

@@ -143,6 +143,19 @@ const PowTable& pow_table() {
     return t;
 }
 
+const PowTable64& pow_table64() {
+    static PowTable64 t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        uint64_t v = xpow64(8);
+        for (int i = 0; i < 64; ++i) {
+            t.x8pow2[i] = v;
+            v = mulmod64(v, v);
+        }
+    });
+    return t;
+}
+
 // x^(8*part*2^i): powers of K = x^(8*part) for the combine_series kernel.
 PowTable part_pow_table(uint64_t part) {
     PowTable t;
@@ -774,6 +787,80 @@ int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, ui
     a.out = d_out;
     a.seed0 = seed0;
     return launch_batch64(a, 65536, static_cast<hipStream_t>(stream));
+}
+
+int photon_crc64ecma_combine_batch(const uint64_t* d_crc1, const uint64_t* d_crc2, const uint32_t* d_len2,
+                                   uint64_t count, uint64_t* d_out, void* stream) {
+    if (!count) return 0;
+    if (!d_crc1 || !d_crc2 || !d_len2 || !d_out) return fail(-EINVAL, "null argument");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    hipLaunchKernelGGL(crc64_combine_kernel, dim3((count + 255) / 256), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_crc1, d_crc2, d_len2, count, d_out, pow_table64());
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "crc64_combine_kernel launch");
+}
+
+int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                                 uint64_t nseg, uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_seg_out,
+                                 uint64_t* d_out, void* stream) {
+    if (!nmsg) return 0;
+    if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    Batch64Args a{};
+    a.iov = d_iov;
+    a.count = nseg;
+    a.out = d_seg_out;
+    a.seed0 = 0;
+    int rc = launch_batch64(a, 8192, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(crc64_msg_fold_kernel, dim3((nmsg + 255) / 256), dim3(256), 0, st, d_iov, d_msg_start, nmsg,
+                       d_seg_out, seed0, d_seeds, d_out, pow_table64());
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "crc64_msg_fold_kernel launch");
+}
+
+int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,
+                                   void* stream) {
+    if (!d_out || (!d_data && nbytes)) return fail(-EINVAL, "null buffer or output");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // Pieces as photon_crc32c_extend_device: >= 16 KiB, 4 KiB multiples, <= 4096.
+    uint64_t piece = (nbytes + 4095) / 4096;
+    piece = (piece + 4095) & ~4095ull;
+    if (piece < (16u << 10)) piece = 16u << 10;
+    const uint64_t k = nbytes ? (nbytes + piece - 1) / piece : 1;
+    if (k == 1)  // (nbytes == 0 gives the seed, as crc64ecma_extend does)
+        return photon_crc64ecma_batch_strided(d_data, nbytes, nbytes, 1, seed, nullptr, d_out, stream);
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    void* scratch = nullptr;
+    hipError_t e = hipMallocAsync(&scratch, k * sizeof(photon_crc_iovec) + k * 8, st);
+    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    auto* iov = static_cast<photon_crc_iovec*>(scratch);
+    auto* crcs = reinterpret_cast<uint64_t*>(iov + k);
+    hipLaunchKernelGGL(crc32c_split_kernel, dim3((k + 255) / 256), dim3(256), 0, st,
+                       static_cast<const uint8_t*>(d_data), nbytes, piece, k, iov);
+    e = hipGetLastError();
+    int rc = e == hipSuccess ? 0 : hip_fail(e, "split kernel launch");
+    if (!rc) {
+        Batch64Args a{};
+        a.iov = iov;
+        a.count = k;
+        a.out = crcs;
+        a.seed0 = 0;
+        rc = launch_batch64(a, piece, st);
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(crc64_fold_pieces_kernel, dim3(1), dim3(1024), 0, st, crcs, k, piece,
+                           nbytes - (k - 1) * piece, seed, nbytes, xpow64(8 * piece), d_out, pow_table64());
+        e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "crc64_fold_pieces_kernel launch");
+    }
+    e = hipFreeAsync(scratch, st);
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    return rc;
 }
 
 int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,

@@ -1393,4 +1393,95 @@ __global__ void crc64_seed_kernel(uint64_t* out, uint64_t count, const uint64_t*
     out[i] ^= mul_basis64(seeds[i], sc.basis);
 }
 
+
+// ---------------------------------------------- CRC-64 combine / fold / extend
+// crc64ecma_combine(c1, c2, len2) = c1 ? c2 ^ c1 * x^(8*len2) : c2
+// (crc.cpp crc64ecma_combine_sw: the inverted-CRC combine is linear). A
+// message's CRC chained over its segments (crc64ecma_extend, seg after seg)
+// is therefore acc = seed; acc = acc * x^(8*len_s) ^ crc64ecma(seg_s, 0).
+struct PowTable64 {
+    uint64_t x8pow2[64];  // x^(8 * 2^i) mod P64
+};
+
+constexpr uint64_t kOne64 = 1ull << 63;
+
+__device__ __forceinline__ uint64_t xpow8_tab64(uint64_t n, const PowTable64& t) {
+    uint64_t k = kOne64;
+    for (int i = 0; n; ++i, n >>= 1)
+        if (n & 1) k = mulmod64(k, t.x8pow2[i]);
+    return k;
+}
+
+__global__ void crc64_combine_kernel(const uint64_t* c1, const uint64_t* c2, const uint32_t* l2, uint64_t n,
+                                     uint64_t* out, PowTable64 pt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = c1[i], b = c2[i];
+    out[i] = a ? b ^ mulmod64(a, xpow8_tab64(l2[i], pt)) : b;
+}
+
+// One thread per message (as crc32c_msg_fold_kernel).
+__global__ void crc64_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_t* msg_start, uint64_t nmsg,
+                                      const uint64_t* seg_crc, uint64_t seed0, const uint64_t* seeds,
+                                      uint64_t* out, PowTable64 pt) {
+    const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= nmsg) return;
+    const uint64_t s0 = msg_start[m], s1 = msg_start[m + 1];
+    uint64_t acc = seeds ? seeds[m] : seed0;
+    uint64_t klen = 0, k = kOne64;
+    for (uint64_t s = s0; s < s1; s += 4) {
+        uint64_t len[4], c[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (s + j < s1) {
+                len[j] = iov[s + j].len;
+                c[j] = seg_crc[s + j];
+            }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (s + j < s1) {
+                if (len[j] != klen) {
+                    k = xpow8_tab64(len[j], pt);
+                    klen = len[j];
+                }
+                acc = mulmod64(acc, k) ^ c[j];
+            }
+    }
+    out[m] = acc;
+}
+
+// One long buffer split into k pieces of `piece` bytes (the last one
+// last_len): out = sum_i crc_i * x^(8 * bytes after piece i) ^ seed * x^(8n)
+// (the seed term only for seed != 0: combine's shortcut). One 1024-thread
+// block; thread t folds a contiguous run of pieces by Horner with
+// K = x^(8*piece), shifts it past the rest, then a block XOR reduction.
+__global__ __launch_bounds__(1024) void crc64_fold_pieces_kernel(const uint64_t* crcs, uint64_t k, uint64_t piece,
+                                                                 uint64_t last_len, uint64_t seed, uint64_t nbytes,
+                                                                 uint64_t kpiece, uint64_t* out, PowTable64 pt) {
+    __shared__ uint64_t red[1024];
+    const uint32_t t = threadIdx.x;
+    const uint64_t per = (k + 1023) / 1024;
+    const uint64_t lo = t * per, hi = lo + per < k ? lo + per : k;
+    uint64_t acc = 0;
+    if (lo < hi) {
+        // pieces lo..hi-1, all full-size except possibly piece k-1 (which is
+        // then the run's last): Horner over the full pieces, last one appended.
+        for (uint64_t i = lo; i < hi; ++i) {
+            const bool last = i == k - 1;
+            acc = last ? mulmod64(acc, xpow8_tab64(last_len, pt)) ^ crcs[i] : mulmod64(acc, kpiece) ^ crcs[i];
+        }
+        // acc = sum crc_i * x^(8 * bytes from the end of piece i to the end of
+        // the run); shift it past the bytes after the run.
+        if (hi < k) acc = mulmod64(acc, xpow8_tab64((k - 1 - hi) * piece + last_len, pt));
+    }
+    red[t] = acc;
+    __syncthreads();
+    for (uint32_t o = 512; o > 0; o >>= 1) {
+        if (t < o) red[t] ^= red[t + o];
+        __syncthreads();
+    }
+    if (t == 0) *out = red[0] ^ (seed ? mulmod64(seed, xpow8_tab64(nbytes, pt)) : 0ull);
+}
+
+
 }  // namespace pcrc

@@ -153,3 +153,63 @@ def test_full_c2_crc64(torch_dev, oracle):
     got = a.cpu().numpy().view(np.uint64)
     for i in range(0, cnt, 4099):
         assert int(got[i]) == oracle.crc64ecma(d[i * n:(i + 1) * n].cpu().numpy())
+
+
+def test_combine64_batch_reference_triples(torch_dev, ref_vectors):
+    # photon_crc64ecma_combine_batch vs the reference's own crc64ecma_combine_sw
+    # outputs (ref_vectors.json c64_*), shortcuts included.
+    rv = ref_vectors
+    n = len(rv["c64_crc1"])
+    t = lambda a, dt: torch_dev.from_numpy(np.asarray(a, dt).view(  # noqa: E731
+        np.int64 if dt == np.uint64 else np.int32)).cuda()
+    out = torch_dev.zeros(n, dtype=torch_dev.int64, device="cuda")
+    ck.combine64_batch(t(rv["c64_crc1"], np.uint64), t(rv["c64_crc2"], np.uint64), t(rv["c64_len2"], np.uint32),
+                       n, out)
+    torch_dev.cuda.synchronize()
+    assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == rv["c64_comb_sw"]
+
+
+def test_msg64_scatter_gather(torch_dev, oracle):
+    # Messages of ragged, misaligned, empty segments (and empty messages):
+    # photon_crc64ecma_batch_msg_n == crc64ecma_extend chained over the segments.
+    rnd = random.Random(64)
+    host = datagen.stream_bytes(0x64, 1 << 20)
+    d = torch_dev.from_numpy(host.copy()).cuda()
+    iov, start, segs = [], [0], []
+    for m in range(300):
+        k = rnd.choice([0, 1, 2, 3, 8, 28])
+        for _ in range(k):
+            n = rnd.choice([0, 1, 7, 63, 64, 100, 4096, 8192, 20000])
+            o = rnd.randrange(0, (1 << 20) - n)
+            iov.append((d.data_ptr() + o, n))
+            segs.append((o, n))
+        start.append(len(iov))
+    nseg, nmsg = len(iov), len(start) - 1
+    seeds = [rnd.getrandbits(64) if m % 3 else 0 for m in range(nmsg)]
+    d_iov = torch_dev.from_numpy(np.asarray(iov, np.uint64).view(np.int64)).cuda()
+    d_start = torch_dev.from_numpy(np.asarray(start, np.uint64).view(np.int64)).cuda()
+    d_seeds = torch_dev.from_numpy(np.asarray(seeds, np.uint64).view(np.int64)).cuda()
+    seg_out = torch_dev.zeros(max(nseg, 1), dtype=torch_dev.int64, device="cuda")
+    out = torch_dev.zeros(nmsg, dtype=torch_dev.int64, device="cuda")
+    ck.batch64_msg_n(d_iov, d_start, nmsg, nseg, seg_out, out, seeds=d_seeds)
+    torch_dev.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64)
+    for m in range(nmsg):
+        acc = seeds[m]
+        for o, n in segs[start[m]:start[m + 1]]:
+            acc = oracle.crc64ecma(host[o:o + n], acc)
+        assert int(got[m]) == acc, m
+
+
+@pytest.mark.parametrize("nbytes", [0, 1, 4095, 16384, 16389, 1 << 20, (1 << 20) + 3, (64 << 20) + 7])
+def test_extend64_device_single_buffer(torch_dev, oracle, nbytes):
+    # photon_crc64ecma_extend_device: one long buffer split into pieces,
+    # checksummed in parallel and folded; unaligned start, seeds 0 and not.
+    d = torch_dev.empty(nbytes + 32, dtype=torch_dev.uint8, device="cuda")
+    ck.fill_splitmix(d, nbytes + 32, nbytes + 32, 1, 0x6465)
+    host = d.cpu().numpy()
+    out = torch_dev.zeros(1, dtype=torch_dev.int64, device="cuda")
+    for seed in (0, 0x0123456789ABCDEF):
+        ck.extend64_device(d.data_ptr() + 5, nbytes, out, seed=seed)
+        torch_dev.cuda.synchronize()
+        assert int(out.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(host[5:5 + nbytes], seed), seed
