@@ -154,7 +154,7 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
 
 /* Route the drop-in entry points to the device when handed device memory:
  * with on != 0, crc32c_auto / crc32c_series_auto / crc32c_combine_series_auto
- * (crc.cpp:126-134) point to wrappers that ask HIP whether the data pointer
+ * (crc.cpp:126-134) and crc64ecma_auto point to wrappers that ask HIP whether the data pointer
  * is device memory (hipMemoryTypeDevice) and, if so, run the calls above
  * synchronously on that pointer's device (legacy default stream), else call
  * the host engine. Off (the default, also at load time) restores the host

@@ -404,6 +404,14 @@ def crc32c_extend_at(addr, nbytes, crc=0):
     return _auto("crc32c_auto", _CRC_PTR_FN)(addr, nbytes, crc & 0xFFFFFFFF)
 
 
+_CRC64_PTR_FN = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64)
+
+
+def crc64ecma_extend_at(addr, nbytes, crc=0):
+    """crc64ecma_extend through the crc64ecma_auto pointer on a raw address."""
+    return _auto("crc64ecma_auto", _CRC64_PTR_FN)(addr, nbytes, crc & 0xFFFFFFFFFFFFFFFF)
+
+
 def crc32c_series_at(addr, part_size, n_parts, out_addr):
     """crc32c_series through crc32c_series_auto on raw addresses."""
     _auto("crc32c_series_auto", _SERIES_PTR_FN)(addr, part_size, n_parts, out_addr)

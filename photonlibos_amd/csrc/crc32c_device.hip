@@ -45,6 +45,7 @@
 #include <vector>
 
 #include <photon/common/checksum/crc32c.h>
+#include <photon/common/checksum/crc64ecma.h>
 
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "crc32c_kernels.h"
@@ -1019,6 +1020,7 @@ std::mutex g_dispatch_mu;
 std::atomic<int> g_dispatch_err{0};
 bool g_dispatch_on = false;
 uint32_t (*g_host_crc)(const uint8_t*, size_t, uint32_t) = nullptr;
+uint64_t (*g_host_crc64)(const uint8_t*, size_t, uint64_t) = nullptr;
 void (*g_host_series)(const uint8_t*, uint32_t, uint32_t, uint32_t*) = nullptr;
 uint32_t (*g_host_cseries)(uint32_t*, uint32_t, uint32_t) = nullptr;
 
@@ -1112,6 +1114,18 @@ uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
     return rc ? 0 : r;
 }
 
+uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
+    const int dev = n ? device_of(p) : -1;
+    if (dev < 0) return g_host_crc64(p, n, crc);
+    DeviceScope scope(dev);
+    uint64_t r = 0;
+    int rc = with_scratch(8, &r, 8, [&](void* d) {
+        return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), nullptr);
+    });
+    if (rc) routed_failure("crc64ecma_extend", rc);
+    return rc ? 0 : r;
+}
+
 }  // namespace
 }  // namespace pcrc
 
@@ -1125,11 +1139,14 @@ extern "C" int photon_crc_set_device_dispatch(int on) {
         crc32c_auto = dispatch_crc;
         crc32c_series_auto = dispatch_series;
         crc32c_combine_series_auto = dispatch_combine_series;
+        g_host_crc64 = crc64ecma_auto;
+        crc64ecma_auto = dispatch_crc64;
         g_dispatch_on = true;
     } else if (!on && g_dispatch_on) {
         crc32c_auto = g_host_crc;
         crc32c_series_auto = g_host_series;
         crc32c_combine_series_auto = g_host_cseries;
+        crc64ecma_auto = g_host_crc64;
         g_dispatch_on = false;
     }
     return g_dispatch_err.exchange(0) ? -EIO : 0;

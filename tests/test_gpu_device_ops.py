@@ -210,6 +210,10 @@ def test_device_dispatch_dropin(torch_dev, oracle):
     assert list(u32(out_d)) == exp_parts
     # combine_series on a device array
     assert ck.crc32c_combine_series_at(out_d.data_ptr(), ps, np_) == oracle.crc32c(host[:ps * np_])
+    # CRC-64: crc64ecma_auto routes device pointers too
+    e64 = oracle.crc64ecma(host, 0xFEEDFACECAFEBEEF)
+    assert ck.crc64ecma_extend_at(dbuf.data_ptr(), n, 0xFEEDFACECAFEBEEF) == e64
+    assert ck.crc64ecma_extend_at(hbuf.ctypes.data, n, 0xFEEDFACECAFEBEEF) == e64
     ck.set_device_dispatch(False)
     assert ck.crc32c_extend_at(hbuf.ctypes.data, n, 77) == expect
 
