@@ -181,6 +181,10 @@ int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, ui
  *                  segment's crc64ecma(seg, 0); nseg == d_msg_start[nmsg];
  *   extend_device: *d_out = crc64ecma_extend(d_data, nbytes, seed) for ONE
  *                  long device buffer (split, run in parallel, folded). */
+/* photon_crc32c_host_batch_strided for CRC-64/ECMA: host (e.g. an OSS
+ * upload's) buffers through the same chunked H2D + kernel + D2H pipeline. */
+int photon_crc64ecma_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                        uint64_t seed0, const uint64_t* h_seeds, uint64_t* h_out);
 int photon_crc64ecma_combine_batch(const uint64_t* d_crc1, const uint64_t* d_crc2, const uint32_t* d_len2,
                                    uint64_t count, uint64_t* d_out, void* stream);
 int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,

@@ -468,9 +468,9 @@ struct HostPipe {
     hipStream_t copy = nullptr, comp = nullptr;
     void* stage[kNumStage] = {};
     hipEvent_t copied[kNumStage] = {}, consumed[kNumStage] = {};
-    uint32_t* d_out = nullptr;
-    uint32_t* d_seeds = nullptr;
-    uint64_t out_cap = 0;
+    void* d_out = nullptr;    // CRC words of the batch
+    void* d_seeds = nullptr;
+    uint64_t out_cap = 0;     // bytes
 };
 
 constexpr int kMaxDevices = 64;
@@ -601,8 +601,17 @@ int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64
     return 0;
 }
 
-int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
-                                     uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out) {
+}  // extern "C"
+
+namespace pcrc {
+namespace {
+
+// The host-memory pipeline for CRC word type T (uint32_t CRC-32C, uint64_t
+// CRC-64/ECMA); `device_batch` is the matching strided device batch.
+template <typename T>
+int host_batch_impl(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count, T seed0, const T* h_seeds,
+                    T* h_out,
+                    int (*device_batch)(const void*, uint64_t, uint64_t, uint64_t, T, const T*, T*, void*)) {
     if (!count) return 0;
     if (!h_base || !h_out || stride < nbytes) return fail(-EINVAL, "bad arguments");
     const uint64_t pitch = (nbytes + 255) & ~uint64_t(255);
@@ -616,17 +625,20 @@ int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64
     int rc = pipe_init(*p);
     if (rc) return rc;
     hipError_t e;
-    if (p->out_cap < count) {
+    const uint64_t bytes = count * sizeof(T);
+    if (p->out_cap < bytes) {
         if (p->d_out) (void)hipFree(p->d_out);
         if (p->d_seeds) (void)hipFree(p->d_seeds);
         p->d_out = p->d_seeds = nullptr;
         p->out_cap = 0;
-        if ((e = hipMalloc(&p->d_out, count * 4)) != hipSuccess) return hip_fail(e, "hipMalloc(out)");
-        if ((e = hipMalloc(&p->d_seeds, count * 4)) != hipSuccess) return hip_fail(e, "hipMalloc(seeds)");
-        p->out_cap = count;
+        if ((e = hipMalloc(&p->d_out, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(out)");
+        if ((e = hipMalloc(&p->d_seeds, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(seeds)");
+        p->out_cap = bytes;
     }
+    T* d_out = static_cast<T*>(p->d_out);
+    T* d_seeds = static_cast<T*>(p->d_seeds);
     if (h_seeds) {
-        e = hipMemcpyAsync(p->d_seeds, h_seeds, count * 4, hipMemcpyHostToDevice, p->comp);
+        e = hipMemcpyAsync(d_seeds, h_seeds, bytes, hipMemcpyHostToDevice, p->comp);
         if (e != hipSuccess) return hip_fail(e, "seeds H2D");
     }
     const uint64_t per_chunk = kStageBytes / pitch;
@@ -640,16 +652,33 @@ int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64
         if (e != hipSuccess) return hip_fail(e, "hipMemcpy2DAsync H2D");
         if ((e = hipEventRecord(p->copied[slot], p->copy)) != hipSuccess) return hip_fail(e, "record");
         if ((e = hipStreamWaitEvent(p->comp, p->copied[slot], 0)) != hipSuccess) return hip_fail(e, "wait");
-        rc = photon_crc32c_batch_strided(p->stage[slot], pitch, nbytes, k, seed0, h_seeds ? p->d_seeds + first : nullptr,
-                                         p->d_out + first, p->comp);
+        rc = device_batch(p->stage[slot], pitch, nbytes, k, seed0, h_seeds ? d_seeds + first : nullptr, d_out + first,
+                          p->comp);
         if (rc) return rc;
         if ((e = hipEventRecord(p->consumed[slot], p->comp)) != hipSuccess) return hip_fail(e, "record");
     }
-    e = hipMemcpyAsync(h_out, p->d_out, count * 4, hipMemcpyDeviceToHost, p->comp);
+    e = hipMemcpyAsync(h_out, d_out, bytes, hipMemcpyDeviceToHost, p->comp);
     if (e != hipSuccess) return hip_fail(e, "out D2H");
     e = hipStreamSynchronize(p->comp);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return 0;
+}
+
+}  // namespace
+}  // namespace pcrc
+
+extern "C" {
+
+int photon_crc32c_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                     uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out) {
+    return host_batch_impl<uint32_t>(h_base, stride, nbytes, count, seed0, h_seeds, h_out,
+                                     &photon_crc32c_batch_strided);
+}
+
+int photon_crc64ecma_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                        uint64_t seed0, const uint64_t* h_seeds, uint64_t* h_out) {
+    return host_batch_impl<uint64_t>(h_base, stride, nbytes, count, seed0, h_seeds, h_out,
+                                     &photon_crc64ecma_batch_strided);
 }
 
 int photon_crc32c_host_batch_strided_multi(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,

@@ -213,3 +213,19 @@ def test_extend64_device_single_buffer(torch_dev, oracle, nbytes):
         ck.extend64_device(d.data_ptr() + 5, nbytes, out, seed=seed)
         torch_dev.cuda.synchronize()
         assert int(out.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(host[5:5 + nbytes], seed), seed
+
+
+def test_host_batch64_pipeline(torch_dev, oracle):
+    # CRC-64 host-memory pipeline: pinned host batch, odd stride, seeds.
+    nbytes, stride, count = 65536 + 8, 65536 + 24, 4500
+    host = torch_dev.empty(stride * count, dtype=torch_dev.uint8, pin_memory=True)
+    host.numpy()[:] = np.resize(datagen.stream_bytes(0xC64, 1 << 20), stride * count)
+    seeds = torch_dev.from_numpy((np.arange(count, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)).view(
+        np.int64)).pin_memory()
+    out = torch_dev.zeros(count, dtype=torch_dev.int64, pin_memory=True)
+    ck.host_batch64_strided(host, stride, nbytes, count, out, seeds=seeds)
+    got = out.numpy().view(np.uint64)
+    h = host.numpy()
+    sd = seeds.numpy().view(np.uint64)
+    for i in list(range(0, count, 211)) + [count - 1]:
+        assert int(got[i]) == oracle.crc64ecma(h[i * stride:i * stride + nbytes], int(sd[i])), i
