@@ -181,6 +181,19 @@ int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, ui
  *                  segment's crc64ecma(seg, 0); nseg == d_msg_start[nmsg];
  *   extend_device: *d_out = crc64ecma_extend(d_data, nbytes, seed) for ONE
  *                  long device buffer (split, run in parallel, folded). */
+/* Same layout as CRC64ECMA_Component {uint64_t crc; uint64_t size;}
+ * (common/checksum/crc64ecma.h:68-71). */
+typedef struct photon_crc64_component {
+    uint64_t crc;
+    uint64_t size;
+} photon_crc64_component;
+
+/* d_out[i] = crc64ecma_trim(d_all[i], d_prefix[i], d_suffix[i])
+ * (crc64ecma.h:73-87); inconsistent sizes give 0 and count in *d_nerr. */
+int photon_crc64ecma_trim_batch(const photon_crc64_component* d_all, const photon_crc64_component* d_prefix,
+                                const photon_crc64_component* d_suffix, uint64_t count, uint64_t* d_out,
+                                uint32_t* d_nerr, void* stream);
+
 /* photon_crc32c_host_batch_strided for CRC-64/ECMA: host (e.g. an OSS
  * upload's) buffers through the same chunked H2D + kernel + D2H pipeline. */
 int photon_crc64ecma_host_batch_strided(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,

@@ -55,6 +55,7 @@ def _declare(L):
     fn("photon_crc64ecma_batch_strided", ctypes.c_int, vp, u64, u64, u64, u64, vp, vp, vp)
     fn("photon_crc64ecma_batch_iov", ctypes.c_int, vp, u64, u64, vp, vp, vp)
     fn("photon_crc64ecma_host_batch_strided", ctypes.c_int, vp, u64, u64, u64, u64, vp, vp)
+    fn("photon_crc64ecma_trim_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp, vp)
     fn("photon_crc64ecma_combine_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp)
     fn("photon_crc64ecma_batch_msg_n", ctypes.c_int, vp, vp, u64, u64, u64, vp, vp, vp, vp)
     fn("photon_crc64ecma_extend_device", ctypes.c_int, vp, u64, u64, vp, vp)

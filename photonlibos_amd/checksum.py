@@ -28,7 +28,7 @@ __all__ = [
     "Shard", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
     "crc64ecma_combine_series", "crc64ecma_trim",
-    "batch64_strided", "batch64_iov", "combine64_batch", "batch64_msg_n", "host_batch64_strided", "extend64_device", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
+    "batch64_strided", "batch64_iov", "combine64_batch", "trim64_batch", "batch64_msg_n", "host_batch64_strided", "extend64_device", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
 _CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
@@ -344,6 +344,13 @@ def host_batch64_strided(base, stride, nbytes, count, out, seed=0, seeds=None):
     """CRC-64/ECMA host-memory batch (chunked H2D + kernel + D2H). Synchronous."""
     _check(lib().photon_crc64ecma_host_batch_strided(_ptr(base), stride, nbytes, count, seed & 0xFFFFFFFFFFFFFFFF,
                                                      _ptr(seeds), _ptr(out)))
+
+
+def trim64_batch(all_, prefix, suffix, count, out, nerr=None, stream=None):
+    """out[i] = crc64ecma_trim(all_[i], prefix[i], suffix[i]); arrays of 16-byte
+    {crc, size} components (device). Async."""
+    _check(lib().photon_crc64ecma_trim_batch(_ptr(all_), _ptr(prefix), _ptr(suffix), count, _ptr(out), _ptr(nerr),
+                                             _stream(stream)))
 
 
 def combine64_batch(crc1, crc2, len2, count, out, stream=None):

@@ -157,6 +157,19 @@ const PowTable64& pow_table64() {
     return t;
 }
 
+const PowTable64& rshift_table64() {
+    static PowTable64 t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        uint64_t v = xpow64_inv(8);
+        for (int i = 0; i < 64; ++i) {
+            t.x8pow2[i] = v;
+            v = mulmod64(v, v);
+        }
+    });
+    return t;
+}
+
 // x^(8*part*2^i): powers of K = x^(8*part) for the combine_series kernel.
 PowTable part_pow_table(uint64_t part) {
     PowTable t;
@@ -830,6 +843,20 @@ int photon_crc64ecma_combine_batch(const uint64_t* d_crc1, const uint64_t* d_crc
                        static_cast<hipStream_t>(stream), d_crc1, d_crc2, d_len2, count, d_out, pow_table64());
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "crc64_combine_kernel launch");
+}
+
+int photon_crc64ecma_trim_batch(const photon_crc64_component* d_all, const photon_crc64_component* d_prefix,
+                                const photon_crc64_component* d_suffix, uint64_t count, uint64_t* d_out,
+                                uint32_t* d_nerr, void* stream) {
+    if (!count) return 0;
+    if (!d_all || !d_prefix || !d_suffix || !d_out) return fail(-EINVAL, "null argument");
+    int cus = 0;
+    int dev = current_device(&cus);
+    if (dev < 0) return dev;
+    hipLaunchKernelGGL(crc64_trim_kernel, dim3((count + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       d_all, d_prefix, d_suffix, count, d_out, d_nerr, pow_table64(), rshift_table64());
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "crc64_trim_kernel launch");
 }
 
 int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,

@@ -1420,6 +1420,26 @@ __global__ void crc64_combine_kernel(const uint64_t* c1, const uint64_t* c2, con
     out[i] = a ? b ^ mulmod64(a, xpow8_tab64(l2[i], pt)) : b;
 }
 
+// crc64ecma_trim per element (do_crc_trim, crc.cpp:442-456, with
+// T = CRC64ECMA_Component): 64-bit size check; shifts by the 32-bit lengths
+// crc_apply_shifts takes; combine's crc1 == 0 shortcut.
+__global__ void crc64_trim_kernel(const photon_crc64_component* all, const photon_crc64_component* pre,
+                                  const photon_crc64_component* suf, uint64_t n, uint64_t* out, uint32_t* nerr,
+                                  PowTable64 lsh, PowTable64 rsh) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const photon_crc64_component a = all[i], p = pre[i], s = suf[i];
+    if (a.size < p.size + s.size) {
+        out[i] = 0;
+        if (nerr) atomicAdd(nerr, 1u);
+        return;
+    }
+    uint64_t crc = a.crc;
+    if (p.size && p.crc) crc ^= mulmod64(p.crc, xpow8_tab64((uint32_t)(a.size - p.size), lsh));
+    if (s.size) crc = mulmod64(crc ^ s.crc, xpow8_tab64((uint32_t)s.size, rsh));
+    out[i] = crc;
+}
+
 // One thread per message (as crc32c_msg_fold_kernel).
 __global__ void crc64_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_t* msg_start, uint64_t nmsg,
                                       const uint64_t* seg_crc, uint64_t seed0, const uint64_t* seeds,

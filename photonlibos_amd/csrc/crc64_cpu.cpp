@@ -2,12 +2,14 @@
 // (include/photon/common/checksum/crc64ecma.h; reference crc64ecma.h:20-87,
 // crc.cpp:119-122, 511-669): same names, C++ linkage, inversion convention,
 // combine/trim semantics (incl. the reference's 32-bit length arguments).
-// Both engines are slicing-by-8 tables here (results identical to the
-// reference's crc64ecma_sw and SSE/PCLMUL paths; its AVX-512 path disagrees
-// with them for long inputs, SURVEY.md §0.4, and is not reproduced).
+// crc64ecma_sw is slicing-by-8 tables, crc64ecma_hw PCLMUL folding (tables
+// without PCLMUL); results identical to the reference's crc64ecma_sw and
+// SSE/PCLMUL paths (its AVX-512 path disagrees with them for long inputs,
+// SURVEY.md §0.4, and is not reproduced).
 #include <photon/common/checksum/crc64ecma.h>
 
 #include <errno.h>
+#include <immintrin.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -85,16 +87,78 @@ uint64_t trim64(CRC64ECMA_Component all, CRC64ECMA_Component prefix, CRC64ECMA_C
     return crc;
 }
 
+// ---------------------------------------------------------- PCLMUL folding
+// The hw engine (the reference's crc64ecma_hw is PCLMUL-based too,
+// crc.cpp:511-669): fold 16-byte states with carry-less multiplies, finish
+// the last state with the table engine.
+//
+// A 16-byte little-endian block is the reflected 128-bit polynomial
+// S = S_hi * x^64 + S_lo with S_hi in the low qword. Moving S forward by d
+// bits: S * x^d = S_hi * x^(64+d) + S_lo * x^d, and a carry-less product of
+// two reflected 64-bit values is x * (their product) in reflected 128-bit
+// form, so the constants are x^(63+d) and x^(d-1) mod P (both reflected, as
+// xpow64 returns them). The message so far is congruent to the state modulo
+// P, so the register is (S * x^64 mod P) = the table engine run over the 16
+// bytes of S from register 0.
+struct Fold64 {
+    uint64_t k1_lo, k1_hi;  // d = 128: x^191, x^127
+    uint64_t k4_lo, k4_hi;  // d = 512: x^575, x^511
+};
+Fold64 g_fold;
+bool g_have_pclmul = false;
+
+__attribute__((target("pclmul,sse4.1"))) inline __m128i fold16(__m128i s, __m128i k) {
+    return _mm_xor_si128(_mm_clmulepi64_si128(s, k, 0x00), _mm_clmulepi64_si128(s, k, 0x11));
+}
+
+__attribute__((target("pclmul,sse4.1"))) uint64_t engine64_clmul(const uint8_t* p, size_t n, uint64_t c) {
+    if (n < 128) return engine64(p, n, c);
+    const __m128i k1 = _mm_set_epi64x((long long)g_fold.k1_hi, (long long)g_fold.k1_lo);
+    const __m128i k4 = _mm_set_epi64x((long long)g_fold.k4_hi, (long long)g_fold.k4_lo);
+    auto ld = [](const uint8_t* q) { return _mm_loadu_si128(reinterpret_cast<const __m128i*>(q)); };
+    // Four interleaved states (blocks i, i+4, ...), the register folded into
+    // the first 8 message bytes (init linearity).
+    __m128i s0 = _mm_xor_si128(ld(p), _mm_cvtsi64_si128((long long)c));
+    __m128i s1 = ld(p + 16), s2 = ld(p + 32), s3 = ld(p + 48);
+    p += 64;
+    n -= 64;
+    for (; n >= 64; p += 64, n -= 64) {
+        s0 = _mm_xor_si128(fold16(s0, k4), ld(p));
+        s1 = _mm_xor_si128(fold16(s1, k4), ld(p + 16));
+        s2 = _mm_xor_si128(fold16(s2, k4), ld(p + 32));
+        s3 = _mm_xor_si128(fold16(s3, k4), ld(p + 48));
+    }
+    __m128i s = _mm_xor_si128(fold16(s0, k1), s1);
+    s = _mm_xor_si128(fold16(s, k1), s2);
+    s = _mm_xor_si128(fold16(s, k1), s3);
+    for (; n >= 16; p += 16, n -= 16) s = _mm_xor_si128(fold16(s, k1), ld(p));
+    uint8_t tail[16];
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(tail), s);
+    return engine64(p, n, engine64(tail, 16, 0));
+}
+
+void build_fold() {
+    g_fold.k1_lo = pcrc::xpow64(191);
+    g_fold.k1_hi = pcrc::xpow64(127);
+    g_fold.k4_lo = pcrc::xpow64(575);
+    g_fold.k4_hi = pcrc::xpow64(511);
+    g_have_pclmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+}
+
+uint64_t engine64_hw(const uint8_t* p, size_t n, uint64_t c) {
+    return g_have_pclmul ? engine64_clmul(p, n, c) : engine64(p, n, c);
+}
+
 }  // namespace
 
 uint64_t crc64ecma_sw(const uint8_t* buffer, size_t nbytes, uint64_t crc) { return ~engine64(buffer, nbytes, ~crc); }
-uint64_t crc64ecma_hw(const uint8_t* buffer, size_t nbytes, uint64_t crc) { return ~engine64(buffer, nbytes, ~crc); }
+uint64_t crc64ecma_hw(const uint8_t* buffer, size_t nbytes, uint64_t crc) { return ~engine64_hw(buffer, nbytes, ~crc); }
 
 void crc64ecma_series_sw(const uint8_t* buffer, uint32_t part_size, uint32_t n_parts, uint64_t* crc_parts) {
     for (uint32_t i = 0; i < n_parts; ++i) crc_parts[i] = crc64ecma_sw(buffer + (size_t)i * part_size, part_size, 0);
 }
 void crc64ecma_series_hw(const uint8_t* buffer, uint32_t part_size, uint32_t n_parts, uint64_t* crc_parts) {
-    crc64ecma_series_sw(buffer, part_size, n_parts, crc_parts);
+    for (uint32_t i = 0; i < n_parts; ++i) crc_parts[i] = crc64ecma_hw(buffer + (size_t)i * part_size, part_size, 0);
 }
 
 uint64_t crc64ecma_combine_sw(uint64_t crc1, uint64_t crc2, uint32_t len2) { return combine64(crc1, crc2, len2); }
@@ -121,6 +185,7 @@ uint64_t (*crc64ecma_trim_auto)(CRC64ECMA_Component, CRC64ECMA_Component, CRC64E
 
 __attribute__((constructor(101))) static void photon_crc64_cpu_init() {
     build64();
+    build_fold();
     crc64ecma_auto = crc64ecma_hw;
     crc64ecma_series_auto = crc64ecma_series_hw;
     crc64ecma_combine_auto = crc64ecma_combine_hw;

@@ -229,3 +229,29 @@ def test_host_batch64_pipeline(torch_dev, oracle):
     sd = seeds.numpy().view(np.uint64)
     for i in list(range(0, count, 211)) + [count - 1]:
         assert int(got[i]) == oracle.crc64ecma(h[i * stride:i * stride + nbytes], int(sd[i])), i
+
+
+def test_trim64_batch_reference_vectors(torch_dev, ref_vectors, oracle):
+    # photon_crc64ecma_trim_batch vs the reference's crc64ecma_trim_sw outputs
+    # (ref_vectors t64_*; same buffer as tests/test_crc64_dropin.py), plus the
+    # error path and the shortcuts.
+    rv = ref_vectors
+    buf = datagen.stream_bytes(0x5EEDB064, 5100)
+    x = rv["t64_all"][0]
+    cases = []
+    for l1, l3 in zip(rv["t64_l1"], rv["t64_l3"]):
+        c1 = oracle.crc64ecma(buf[:l1])
+        c3 = oracle.crc64ecma(buf[5100 - l3:]) if l3 else 0
+        cases.append(((x, 5100), (c1, l1), (c3, l3)))
+    want = list(rv["t64_sw"])
+    cases += [((123, 10), (1, 6), (2, 6)),          # EINVAL: 0 and counted
+              ((0xDEAD, 100), (0, 0), (0, 0)),       # nothing to trim
+              ((0xDEAD, 100), (0, 40), (0x12, 60))]  # prefix.crc == 0 shortcut
+    want += [0, ck.crc64ecma_trim((0xDEAD, 100), (0, 0), (0, 0)), ck.crc64ecma_trim((0xDEAD, 100), (0, 40), (0x12, 60))]
+    arr = [torch_dev.from_numpy(np.asarray([c[k] for c in cases], np.uint64).view(np.int64)).cuda() for k in range(3)]
+    out = torch_dev.zeros(len(cases), dtype=torch_dev.int64, device="cuda")
+    nerr = torch_dev.zeros(1, dtype=torch_dev.int32, device="cuda")
+    ck.trim64_batch(*arr, len(cases), out, nerr)
+    torch_dev.cuda.synchronize()
+    assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == want
+    assert int(nerr.item()) == 1
