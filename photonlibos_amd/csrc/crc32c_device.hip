@@ -223,12 +223,13 @@ const FusedConsts& fused_consts(int g) {
     return tab[g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2];
 }
 
-int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream) {
+// lanes: 0 = by typical_len (choose_lanes), else the lane-group size.
+int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, int lanes = 0) {
     if (a.count == 0) return 0;
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const int g = choose_lanes(typical_len);
+    const int g = lanes ? lanes : choose_lanes(typical_len);
     const uint64_t gpw = 64 / g;
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
@@ -779,9 +780,14 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
     return photon_crc32c_batch_msg_n(d_iov, d_msg_start, nmsg, nseg, seed0, d_seeds, d_seg_out, d_out, stream);
 }
 
-int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
-                              uint64_t nseg, uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out,
-                              uint32_t* d_out, void* stream) {
+}  // extern "C"
+
+// Messages with an explicit lane-group size (0 = automatic): segments in host
+// memory read by the kernels over the host link go faster with wide groups
+// (longer contiguous requests), see checked_batch.cpp.
+int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg, uint64_t nseg,
+                          uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
+                          void* stream, int lanes) {
     if (!nmsg) return 0;
     if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -791,7 +797,7 @@ int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_m
     a.count = nseg;
     a.out = d_seg_out;
     a.seed0 = 0;
-    int rc = launch_batch(a, 8192, st);
+    int rc = launch_batch(a, 8192, st, lanes);
     if (rc) return rc;
     const int bs = 256;
     hipLaunchKernelGGL(crc32c_msg_fold_kernel, dim3((nmsg + bs - 1) / bs), dim3(bs), 0, st, d_iov, d_msg_start,
@@ -799,6 +805,14 @@ int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_m
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "crc32c_msg_fold_kernel launch");
     return 0;
+}
+
+extern "C" {
+
+int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
+                              uint64_t nseg, uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out,
+                              uint32_t* d_out, void* stream) {
+    return pcrc::batch_msg_lanes(d_iov, d_msg_start, nmsg, nseg, seed0, d_seeds, d_seg_out, d_out, stream, 0);
 }
 
 int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,

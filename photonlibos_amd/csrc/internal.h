@@ -1,10 +1,18 @@
 // internal.h -- shared by the translation units of libphoton_checksum.so.
 #pragma once
 #include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <photon_crc/crc32c_gpu.h>
 
 namespace pcrc {
 // Record the text returned by photon_crc_last_error() on this thread and
 // return `code` (report_hip_error: -EIO with the HIP error string).
 int report_error(int code, const char* what);
 int report_hip_error(hipError_t e, const char* what);
+// photon_crc32c_batch_msg_n with an explicit lane-group size (0 = automatic;
+// 4, 8, 16, 32 or 64).
+int batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg, uint64_t nseg,
+                    uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out, void* stream,
+                    int lanes);
 }  // namespace pcrc
