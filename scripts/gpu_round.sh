@@ -6,7 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 O=gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; exit 1; }
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; exit 1; }
 for c in c2 c3 c4 c5 c2_crc64; do
   timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $O/bench_$c.log 2>&1 || { echo "bench $c failed"; exit 1; }
