@@ -7,7 +7,8 @@ MI355X through the C-ABI engine (libphoton_checksum.so).
 One "step" = one pass of the hot path over one batch (BASELINE.json configs):
   c2 (default, configs[1]): 65,536 x 64 KiB random buffers, device-resident
   c3: 1,048,576 x 4 KiB        c4: 32,768 x 1 MiB per GPU (the 8-GPU config's shard)
-  c5: 65,536 messages x 8 non-contiguous 8 KiB segments (per-segment CRC + combine)
+  c5: 65,536 messages x 8 non-contiguous 8 KiB segments, per-message CRC (chained extend)
+  c5_seg: the same with every segment's own CRC written too
   --h2d: the c2 batch starting and ending in pinned host memory (chunked
          H2D + kernel + D2H); reported in DESIGN.md, never as `value`.
 Multi-GPU: one process per GPU (torchrun); every rank checksums its own
@@ -40,8 +41,11 @@ CONFIGS = {
                workload="C3: 1048576 x 4 KiB RPC-payload buffers, device-resident, per GPU"),
     "c4": dict(kind="strided", nbytes=1 << 20, count=32768,
                workload="C4 shard: 32768 x 1 MiB buffers per GPU (256K x 1 MiB over 8 GPUs)"),
-    "c5": dict(kind="msg", nbytes=8192, count=65536, nseg=8,
-               workload="C5: 65536 messages x 8 non-contiguous 8 KiB segments, per-segment CRC + combine"),
+    "c5": dict(kind="msg", nbytes=8192, count=65536, nseg=8, seg_out=False,
+               workload="C5: 65536 messages x 8 non-contiguous 8 KiB segments, per-message CRC "
+                        "(Crc32Hasher: crc32c_extend chained over the segments = per-segment CRC + combine)"),
+    "c5_seg": dict(kind="msg", nbytes=8192, count=65536, nseg=8, seg_out=True,
+                   workload="C5 shape, per-segment CRCs also written (segment kernel + fold kernel)"),
     "c2_crc64": dict(kind="strided64", nbytes=65536, count=65536,
                      workload="C2 shape, CRC-64/ECMA (next row): 65536 x 64 KiB, device-resident, per GPU"),
 }
@@ -147,8 +151,8 @@ class Workload:
         elif c["kind"] == "strided64":
             ck.batch64_strided(self.payload, c["nbytes"], c["nbytes"], c["count"], self.out, stream=self.stream)
         else:
-            ck.batch_msg_n(self.iov, self.start, c["count"], c["count"] * c["nseg"], self.seg_out, self.out,
-                           stream=self.stream)
+            ck.batch_msg_n(self.iov, self.start, c["count"], c["count"] * c["nseg"],
+                           self.seg_out if c.get("seg_out") else None, self.out, stream=self.stream)
 
     def self_check(self):
         """Spot-check results against the product's own host engine (crc32c_hw

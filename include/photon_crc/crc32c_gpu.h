@@ -110,8 +110,9 @@ int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint3
  * [d_msg_start[m], d_msg_start[m+1]) of d_iov (d_msg_start has nmsg+1
  * entries, d_msg_start[nmsg] = total segments). d_out[m] = the chained
  * crc32c_extend over the message's segments starting from seed_m.
- * d_seg_out (total segments entries) receives each segment's own CRC32C
- * (seed 0); it is required (it is the combine kernel's input). */
+ * d_seg_out (total segments entries), if non-NULL, receives each segment's
+ * own CRC32C (seed 0); with NULL the segments are chained through the seed
+ * (the faster form when there are many short messages). */
 int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
                             uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
                             void* stream);
@@ -234,6 +235,14 @@ int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
 /* Interleaved row partials per lane in the CRC-64 streaming kernel (testing /
  * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
 int photon_crc64_set_interleave(int partials);
+
+/* Message batches (photon_crc32c_batch_msg[_n], the CheckedMessage batch),
+ * testing / tuning: 0 = automatic (default: one kernel with a lane group per
+ * message, chained through the seed, when no per-segment CRCs are requested
+ * and there are >= 4096 wavefronts' worth of short messages; else parallel
+ * segment CRCs + a fold kernel), 1 = always the one-kernel form, 2 = always
+ * the two-kernel form. */
+int photon_crc_set_msg_mode(int mode);
 
 /* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
  * each lane reads two consecutive 16-byte blocks per row, one row shift per

@@ -66,6 +66,7 @@ def _declare(L):
     fn("photon_crc_set_generic_rows", ctypes.c_int, ctypes.c_int)
     fn("photon_crc64_set_interleave", ctypes.c_int, ctypes.c_int)
     fn("photon_crc64_set_run_blocks", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc_set_msg_mode", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_host_register", ctypes.c_int, vp, u64)
     fn("photon_crc_host_unregister", ctypes.c_int, vp)
     fn("photon_crc32c_file_strided", ctypes.c_int, ctypes.c_int, u64, u64, u64, u64, u32, vp)

@@ -463,6 +463,11 @@ def set_generic_rows(u):
     _check(lib().photon_crc_set_generic_rows(u))
 
 
+def set_msg_mode(mode):
+    """Message batches: 0 automatic, 1 one fused kernel, 2 segment + fold kernels."""
+    _check(lib().photon_crc_set_msg_mode(mode))
+
+
 def set_stream64_run_blocks(b):
     """CRC-64 streaming kernel: 16-byte blocks per lane run (1, 2)."""
     _check(lib().photon_crc64_set_run_blocks(b))

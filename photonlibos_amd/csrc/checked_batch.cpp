@@ -131,7 +131,6 @@ struct photon_crc_msg_batch {
     // device side
     photon_crc_iovec* d_iov = nullptr;
     uint64_t* d_start = nullptr;
-    uint32_t* d_seg = nullptr;
     uint32_t* d_out = nullptr;
     hipEvent_t done_ev = nullptr;
     uint64_t nmsg = 0, nseg = 0;
@@ -146,7 +145,7 @@ void free_batch(photon_crc_msg_batch* b) {
     if (b->done_ev) (void)hipEventDestroy(b->done_ev);
     for (void* p : {(void*)b->h_iov, (void*)b->h_start, (void*)b->h_expect, (void*)b->h_out})
         if (p) (void)hipHostFree(p);
-    for (void* p : {(void*)b->d_iov, (void*)b->d_start, (void*)b->d_seg, (void*)b->d_out})
+    for (void* p : {(void*)b->d_iov, (void*)b->d_start, (void*)b->d_out})
         if (p) (void)hipFree(p);
     delete b;
 }
@@ -277,7 +276,6 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
     hm((void**)&b->h_out, M * 4);
     dm((void**)&b->d_iov, S * sizeof(photon_crc_iovec));
     dm((void**)&b->d_start, (M + 1) * 8);
-    dm((void**)&b->d_seg, S * 4);
     dm((void**)&b->d_out, M * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -338,7 +336,7 @@ int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*do
         if (b->nseg) e = hipMemcpyAsync(b->d_iov, b->h_iov, b->nseg * sizeof(photon_crc_iovec), hipMemcpyHostToDevice, st);
         if (e == hipSuccess) e = hipMemcpyAsync(b->d_start, b->h_start, (b->nmsg + 1) * 8, hipMemcpyHostToDevice, st);
         if (e != hipSuccess) return report_hip_error(e, "hipMemcpyAsync(descriptors)");
-        rc = pcrc::batch_msg_lanes(b->d_iov, b->d_start, b->nmsg, b->nseg, 0, nullptr, b->d_seg, b->d_out, stream,
+        rc = pcrc::batch_msg_lanes(b->d_iov, b->d_start, b->nmsg, b->nseg, 0, nullptr, nullptr, b->d_out, stream,
                                    lanes_for(b->host_bytes, b->total_bytes));
         if (rc) return rc;
         e = hipMemcpyAsync(b->h_out, b->d_out, b->nmsg * 4, hipMemcpyDeviceToHost, st);

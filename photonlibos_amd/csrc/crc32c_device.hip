@@ -63,6 +63,7 @@ int g_lanes_override = 0;
 // fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
 // the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
 int g_generic_u = 4;
+int g_msg_mode = 0;  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
 int g_stream_b = 1, g_stream_u = 4, g_stream_d = 3;  // streaming kernel: run blocks, rows/step, steps in flight
 // The streaming kernel is a tuning option: with the conflict-free rotated
 // tables the generic kernel measures faster on every config
@@ -250,7 +251,8 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
         return 0;
     }
     const LaneConsts& kc = lane_consts(g);
-#define LB(GG, UU) hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc)
+#define LB(GG, UU) \
+    hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc, pow_table())
 #define LBG(UU)                    \
     switch (g) {                   \
         case 64: LB(64, UU); break; \
@@ -562,6 +564,12 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
     return 0;
 }
 
+int photon_crc_set_msg_mode(int mode) {
+    if (mode < 0 || mode > 2) return fail(-EINVAL, "message mode must be 0 (auto), 1 (fused) or 2 (two kernels)");
+    g_msg_mode = mode;
+    return 0;
+}
+
 int photon_crc64_set_run_blocks(int blocks) {
     if (blocks != 1 && blocks != 2) return fail(-EINVAL, "run blocks must be 1 or 2");
     g_stream64_b = blocks;
@@ -770,7 +778,7 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
                             uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
                             void* stream) {
     if (!nmsg) return 0;
-    if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
+    if (!d_iov || !d_msg_start || !d_out) return fail(-EINVAL, "null argument");
     hipStream_t st = static_cast<hipStream_t>(stream);
     uint64_t nseg = 0;
     hipError_t e = hipMemcpyAsync(&nseg, d_msg_start + nmsg, sizeof(nseg), hipMemcpyDeviceToHost, st);
@@ -789,7 +797,7 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
                           uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
                           void* stream, int lanes) {
     if (!nmsg) return 0;
-    if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
+    if (!d_iov || !d_msg_start || !d_out) return fail(-EINVAL, "null argument");
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e;
     BatchArgs a{};
@@ -797,14 +805,60 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
     a.count = nseg;
     a.out = d_seg_out;
     a.seed0 = 0;
+    // One kernel (a group per message) when there are enough messages to fill
+    // the chip and messages are short; else segment CRCs in parallel + a fold
+    // kernel (few, long messages).
+    const int g = lanes ? lanes : choose_lanes(8192);
+    const uint64_t gpw = 64 / (uint64_t)g;
+    // (With per-segment CRCs requested the fused form folds with a multiply per
+    // segment on one lane and measured slower than the fold kernel, so it is
+    // automatic only for the seed-chained form.)
+    const bool fused = g_msg_mode == 1 ||
+                       (g_msg_mode == 0 && !d_seg_out && nmsg >= 4096 * gpw && nseg <= 64 * nmsg);
+    if (fused) {
+        int cus = 0;
+        int dev = current_device(&cus);
+        if (dev < 0) return dev;
+        a.msg_start = d_msg_start;
+        a.nmsg = nmsg;
+        a.msg_out = d_out;
+        a.seeds = d_seeds;
+        a.seed0 = seed0;
+        uint64_t grid = ((nmsg + gpw - 1) / gpw + kWaves - 1) / kWaves;
+        if (grid > (uint64_t)cus) grid = cus;
+        const LaneConsts& kc = lane_consts(g);
+#define LM(GG) \
+    hipLaunchKernelGGL((crc32c_batch_kernel<GG, 4, true>), dim3(grid), dim3(kBlock), 0, st, a, kc, pow_table())
+        switch (g) {
+            case 64: LM(64); break;
+            case 32: LM(32); break;
+            case 16: LM(16); break;
+            case 8: LM(8); break;
+            default: LM(4); break;
+        }
+#undef LM
+        e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "crc32c_batch_kernel<msg> launch");
+    }
+    void* scratch = nullptr;  // segment CRCs the caller did not ask for
+    if (!d_seg_out && nseg) {
+        e = hipMallocAsync(&scratch, nseg * 4, st);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+        a.out = static_cast<uint32_t*>(scratch);
+    }
     int rc = launch_batch(a, 8192, st, lanes);
-    if (rc) return rc;
-    const int bs = 256;
-    hipLaunchKernelGGL(crc32c_msg_fold_kernel, dim3((nmsg + bs - 1) / bs), dim3(bs), 0, st, d_iov, d_msg_start,
-                       nmsg, d_seg_out, seed0, d_seeds, d_out, pow_table());
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "crc32c_msg_fold_kernel launch");
-    return 0;
+    if (!rc) {
+        const int bs = 256;
+        hipLaunchKernelGGL(crc32c_msg_fold_kernel, dim3((nmsg + bs - 1) / bs), dim3(bs), 0, st, d_iov, d_msg_start,
+                           nmsg, a.out, seed0, d_seeds, d_out, pow_table());
+        e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "crc32c_msg_fold_kernel launch");
+    }
+    if (scratch) {
+        e = hipFreeAsync(scratch, st);
+        if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    }
+    return rc;
 }
 
 extern "C" {

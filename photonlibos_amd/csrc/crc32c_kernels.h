@@ -49,6 +49,12 @@ struct BatchArgs {
     const uint32_t* seeds;     // optional
     uint32_t* out;
     uint32_t seed0;
+    // Message mode (crc32c_batch_kernel<G, U, true>): unit m = message m,
+    // segments iov[msg_start[m] .. msg_start[m+1]); out[] = per-segment CRCs
+    // (seed 0), msg_out[m] = the chained CRC from seed_m (seeds[m] or seed0).
+    const uint64_t* msg_start;
+    uint64_t nmsg;
+    uint32_t* msg_out;
 };
 
 __device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_addr) {
@@ -222,11 +228,89 @@ __device__ __forceinline__ uint32_t wave_id() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+// x^(8 * 2^i) mod P, i < 64 (shift-by-bytes constants).
+struct PowTable {
+    uint32_t x8pow2[64];  // x^(8 * 2^i) mod P
+};
+
+// x^(8n) mod P: product of the x^(8*2^i) entries over the set bits of n.
+__device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
+    uint32_t k = kOne;
+    for (int i = 0; n; ++i, n >>= 1)
+        if (n & 1) k = mulmod(k, t.x8pow2[i]);
+    return k;
+}
+
 // -------------------------------------------------------------- generic path
 // Any pointer, any length, any seed; one group of G lanes per buffer.
 // U rows per step per lane, the next U rows' loads in flight.
-template <int G, int U = 4>
-__global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc) {
+// CRC-32C of one buffer (seed applied) by a group of G lanes; the result is
+// valid on the group's first lane (gl == 0).
+template <int G, int U>
+__device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_t* p, uint64_t n, uint32_t seed,
+                                               uint32_t gl, const LaneAddr& la) {
+    uint32_t crc;
+    if (n < 64) {
+        // Tiny buffer: byte-serial on the group's first lane.
+        crc = seed;
+        if (gl == 0)
+            for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
+    } else {
+        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+        const uint8_t* e = p + n;
+        const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
+        const int s0 = (int)(p - a0);
+        const uint64_t nb = (uint64_t)(eb - a0) >> 4;  // >= 3 blocks since n >= 64
+        const uint64_t full = nb / G;                   // rows where every lane has a block
+        const uint64_t rows = (nb + G - 1) / G;
+        const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);  // blocks in the last row, 1..G
+        const uint8_t* lp = a0 + 16 * gl;               // this lane's block in row 0
+
+        // Row 0 (holds the head: masked leading bytes + seed).
+        uint32_t pc = 0;
+        if (gl < nb) {
+            uint4 w = load16(lp);
+            if (gl < 2) {
+                const int off = (int)gl * 16;
+                w.x = head_word(w.x, off, s0, seed);
+                w.y = head_word(w.y, off + 4, s0, seed);
+                w.z = head_word(w.z, off + 8, s0, seed);
+                w.w = head_word(w.w, off + 12, s0, seed);
+            }
+            pc = crc16(lds, w, la);
+        }
+        // Full rows 1..full-1: U rows per step, the next U in flight.
+        uint64_t row = 1;
+        if (row + U <= full) {
+            uint4 cur[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
+            for (; row + 2 * U <= full; row += U) {
+                uint4 nxt[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+                pc = column_step<U>(lds, pc, cur, la);
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            }
+            pc = column_step<U>(lds, pc, cur, la);
+            row += U;
+        }
+        for (; row < full; ++row) pc = column_step1(lds, pc, load16(lp + row * (16 * G)), la);
+        // Partial last row.
+        if (full >= 1 && full < rows && full * G + gl < nb)
+            pc = column_step1(lds, pc, load16(lp + full * (16 * G)), la);
+
+        crc = group_reduce<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds);
+        // Ragged tail (< 16 bytes) after the last aligned block.
+        if (gl == 0)
+            for (const uint8_t* q = eb; q < e; ++q) crc = bytestep(lds, crc, load8(q), la);
+    }
+    return crc;
+}
+
+template <int G, int U = 4, bool MSG = false>
+__global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     build_tables(lds, kc);
 
@@ -238,6 +322,50 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
     const LaneAddr la = lane_addr(lane);
 
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    if constexpr (MSG) {
+        // One group per message: its segments one after the other, each CRC
+        // (seed 0) stored, and folded on the first lane: acc = acc*x^(8 len) ^ crc
+        // (crc32c_combine, crc.cpp:393-405), the shift constant reused while
+        // the segment length repeats. No second kernel.
+        for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.nmsg; wv += nwaves) {
+            const uint64_t m = wv * GPW + grp;
+            const bool active = m < args.nmsg;
+            uint64_t s0 = 0, s1 = 0;
+            uint32_t acc = args.seed0;
+            if (active) {
+                s0 = args.msg_start[m];
+                s1 = args.msg_start[m + 1];
+                if (args.seeds) acc = args.seeds[m];
+            }
+            if (!args.out) {
+                // No per-segment CRCs wanted: chain through the seed
+                // (crc32c_extend(seg, n, acc), Crc32Hasher::extend_hash).
+                for (uint64_t sg = s0; sg < s1; ++sg) {
+                    const uint32_t seed = (uint32_t)__shfl((int)acc, (int)(threadIdx.x & 63u & ~(uint32_t)(G - 1)), 64);
+                    acc = buffer_crc<G, U>(lds, static_cast<const uint8_t*>(args.iov[sg].base), args.iov[sg].len,
+                                           seed, gl, la);
+                }
+            } else {
+                uint64_t klen = 0;
+                uint32_t k = kOne;
+                for (uint64_t sg = s0; sg < s1; ++sg) {
+                    const uint8_t* p = static_cast<const uint8_t*>(args.iov[sg].base);
+                    const uint64_t n = args.iov[sg].len;
+                    const uint32_t c = buffer_crc<G, U>(lds, p, n, 0u, gl, la);
+                    if (gl == 0) {
+                        args.out[sg] = c;
+                        if (n != klen) {
+                            k = xpow8_tab(n, pt);
+                            klen = n;
+                        }
+                        acc = mulmod(acc, k) ^ c;
+                    }
+                }
+            }
+            if (active && gl == 0) args.msg_out[m] = acc;
+        }
+        return;
+    }
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.count; wv += nwaves) {
         const uint64_t bi = wv * GPW + grp;
         const bool active = bi < args.count;
@@ -255,63 +383,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             if (args.seeds) seed = args.seeds[bi];
         }
 
-        uint32_t crc;
-        if (n < 64) {
-            // Tiny buffer: byte-serial on the group's first lane.
-            crc = seed;
-            if (gl == 0)
-                for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
-        } else {
-            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
-            const uint8_t* e = p + n;
-            const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
-            const int s0 = (int)(p - a0);
-            const uint64_t nb = (uint64_t)(eb - a0) >> 4;  // >= 3 blocks since n >= 64
-            const uint64_t full = nb / G;                   // rows where every lane has a block
-            const uint64_t rows = (nb + G - 1) / G;
-            const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);  // blocks in the last row, 1..G
-            const uint8_t* lp = a0 + 16 * gl;               // this lane's block in row 0
-
-            // Row 0 (holds the head: masked leading bytes + seed).
-            uint32_t pc = 0;
-            if (gl < nb) {
-                uint4 w = load16(lp);
-                if (gl < 2) {
-                    const int off = (int)gl * 16;
-                    w.x = head_word(w.x, off, s0, seed);
-                    w.y = head_word(w.y, off + 4, s0, seed);
-                    w.z = head_word(w.z, off + 8, s0, seed);
-                    w.w = head_word(w.w, off + 12, s0, seed);
-                }
-                pc = crc16(lds, w, la);
-            }
-            // Full rows 1..full-1: U rows per step, the next U in flight.
-            uint64_t row = 1;
-            if (row + U <= full) {
-                uint4 cur[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
-                for (; row + 2 * U <= full; row += U) {
-                    uint4 nxt[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                    pc = column_step<U>(lds, pc, cur, la);
-#pragma unroll
-                    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-                }
-                pc = column_step<U>(lds, pc, cur, la);
-                row += U;
-            }
-            for (; row < full; ++row) pc = column_step1(lds, pc, load16(lp + row * (16 * G)), la);
-            // Partial last row.
-            if (full >= 1 && full < rows && full * G + gl < nb)
-                pc = column_step1(lds, pc, load16(lp + full * (16 * G)), la);
-
-            crc = group_reduce<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds);
-            // Ragged tail (< 16 bytes) after the last aligned block.
-            if (gl == 0)
-                for (const uint8_t* q = eb; q < e; ++q) crc = bytestep(lds, crc, load8(q), la);
-        }
+        const uint32_t crc = buffer_crc<G, U>(lds, p, n, seed, gl, la);
         if (active && gl == 0) args.out[bi] = crc;
     }
 }
@@ -771,9 +843,6 @@ __global__ void crc32c_seed_kernel(uint32_t* out, uint64_t count, const uint32_t
 
 // Per-message fold of per-segment CRCs: acc = seed; acc = acc*x^(8 len)+crc.
 // (Crc32Hasher::extend_hash, rpc/serialize.h:244-252, equals this fold.)
-struct PowTable {
-    uint32_t x8pow2[64];  // x^(8 * 2^i) mod P
-};
 
 __device__ __forceinline__ uint32_t shift_bytes_tab(uint32_t crc, uint64_t n, const PowTable& t) {
     for (int i = 0; n; ++i, n >>= 1)
@@ -781,13 +850,6 @@ __device__ __forceinline__ uint32_t shift_bytes_tab(uint32_t crc, uint64_t n, co
     return crc;
 }
 
-// x^(8n) mod P: product of the x^(8*2^i) entries over the set bits of n.
-__device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
-    uint32_t k = kOne;
-    for (int i = 0; n; ++i, n >>= 1)
-        if (n & 1) k = mulmod(k, t.x8pow2[i]);
-    return k;
-}
 
 // One thread per message. The segments' lengths and CRCs are loaded 8 at a
 // time before the (dependent) fold, and the shift constant x^(8*len) is

@@ -31,6 +31,12 @@ def _reset_lanes():
     ck.set_lanes_per_buffer(0)
     ck.set_stream_config(0, 0, 0)
     ck.set_generic_rows(4)
+    ck.set_msg_mode(0)
+
+
+# Message batch forms: 0 automatic, 1 one fused kernel (a lane group per
+# message), 2 segment kernel + fold kernel.
+MSG_MODES = [0, 1, 2]
 
 
 # Batch kernel variants: 4 = the generic kernel (default), 0 = the fused
@@ -211,8 +217,10 @@ def _pool_messages(nmsg, nseg, seglen, seed):
     return perm
 
 
+@pytest.mark.parametrize("mode", MSG_MODES)
 @pytest.mark.parametrize("nmsg,nseg,seglen", [(512, 8, 8192), (64, 28, 4096)])
-def test_msg_scatter_gather(torch_dev, oracle, nmsg, nseg, seglen):
+def test_msg_scatter_gather(torch_dev, oracle, nmsg, nseg, seglen, mode):
+    ck.set_msg_mode(mode)
     slots = nmsg * nseg
     d = torch_dev.empty(slots * seglen, dtype=torch_dev.uint8, device="cuda")
     ck.fill_splitmix(d, seglen, seglen, slots, 0x5EED0005)
@@ -242,8 +250,12 @@ def test_msg_scatter_gather(torch_dev, oracle, nmsg, nseg, seglen):
     assert np.array_equal(u32(out2), got)
 
 
-def test_msg_ragged_segments(torch_dev, oracle):
+@pytest.mark.parametrize("mode", MSG_MODES)
+@pytest.mark.parametrize("g", [0, 4, 64])
+def test_msg_ragged_segments(torch_dev, oracle, mode, g):
     # Generic iovectors: odd lengths, odd addresses, empty segments, empty messages.
+    ck.set_msg_mode(mode)
+    ck.set_lanes_per_buffer(g)
     rnd = random.Random(3)
     host = datagen.stream_bytes(77, 1 << 20)
     d = to_dev(torch_dev, host)
@@ -265,8 +277,11 @@ def test_msg_ragged_segments(torch_dev, oracle):
     seg_out = torch_dev.zeros(max(len(iov), 1), dtype=torch_dev.int32, device="cuda")
     out = torch_dev.zeros(len(msgs), dtype=torch_dev.int32, device="cuda")
     ck.batch_msg(d_iov, d_start, len(msgs), seg_out, out, seeds=to_dev(torch_dev, seeds.view(np.int32)))
+    out_ns = torch_dev.zeros(len(msgs), dtype=torch_dev.int32, device="cuda")
+    ck.batch_msg(d_iov, d_start, len(msgs), None, out_ns, seeds=to_dev(torch_dev, seeds.view(np.int32)))
     torch_dev.cuda.synchronize()
     got = u32(out)
+    assert np.array_equal(u32(out_ns), got)
     for m, parts in enumerate(msgs):
         assert got[m] == oracle.extend_chain(parts, int(seeds[m])), m
 
@@ -358,3 +373,45 @@ def test_device_shards(torch_dev, oracle):
     for i in (0, 1, half - 1, half, count - 1):
         want = oracle.crc32c(datagen.stream_bytes(0x5EED0001 + i, nbytes), 0 if i < half else 0xABCDEF01)
         assert got[i] == want, i
+
+
+def test_msg_many_messages_fused_vs_two_kernels(torch_dev, oracle):
+    # Enough messages for the automatic one-kernel form (>= 4096 waves of
+    # groups): ragged messages of 0..6 segments at random offsets; the fused
+    # and two-kernel forms agree on every message and segment, a sample
+    # matches the oracle.
+    rnd = random.Random(11)
+    host = datagen.stream_bytes(0x11, 1 << 20)
+    d = to_dev(torch_dev, host)
+    nmsg = 40000
+    iov, start, msgs = [], [0], []
+    for m in range(nmsg):
+        parts = []
+        for _ in range(rnd.choice([0, 1, 3, 6])):
+            n = rnd.choice([0, 5, 64, 200, 1500, 3000])
+            o = rnd.randrange(len(host) - n)
+            iov.append([d.data_ptr() + o, n])
+            parts.append((o, n))
+        start.append(len(iov))
+        msgs.append(parts)
+    seeds = np.array([rnd.getrandbits(32) for _ in range(nmsg)], np.uint32)
+    d_iov = to_dev(torch_dev, np.array(iov, np.uint64).view(np.int64))
+    d_start = to_dev(torch_dev, np.array(start, np.uint64).view(np.int64))
+    d_seeds = to_dev(torch_dev, seeds.view(np.int32))
+    res = {}
+    for mode in (1, 2, 0):
+        ck.set_msg_mode(mode)
+        seg_out = torch_dev.zeros(len(iov), dtype=torch_dev.int32, device="cuda")
+        out = torch_dev.zeros(nmsg, dtype=torch_dev.int32, device="cuda")
+        ck.batch_msg_n(d_iov, d_start, nmsg, len(iov), seg_out, out, seeds=d_seeds)
+        # without per-segment CRCs (the seed-chained form when fused)
+        out_ns = torch_dev.zeros(nmsg, dtype=torch_dev.int32, device="cuda")
+        ck.batch_msg_n(d_iov, d_start, nmsg, len(iov), None, out_ns, seeds=d_seeds)
+        torch_dev.cuda.synchronize()
+        res[mode] = (u32(out).copy(), u32(seg_out).copy())
+        assert np.array_equal(u32(out_ns), res[mode][0]), mode
+    assert np.array_equal(res[1][0], res[2][0]) and np.array_equal(res[1][1], res[2][1])
+    assert np.array_equal(res[0][0], res[1][0])
+    for m in list(range(0, nmsg, 97)) + [nmsg - 1]:
+        parts = [host[o:o + n] for o, n in msgs[m]]
+        assert res[1][0][m] == oracle.extend_chain(parts, int(seeds[m])), m
