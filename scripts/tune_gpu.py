@@ -82,7 +82,9 @@ variants = [(v, int(l)) for v in args.variants.split(",") for l in args.lanes.sp
 refs = {}
 res = {f"{v}/G{l}": [] for v, l in variants}
 for r in range(args.rounds):
-    for v, l in variants:
+    # alternate the order every round (the first launches after a switch can
+    # run at a different clock; do not always hand that to the same variant)
+    for v, l in (variants if r % 2 == 0 else variants[::-1]):
         ms = timed(make(v, l))
         res[f"{v}/G{l}"].append(ms)
         if v != "read":
