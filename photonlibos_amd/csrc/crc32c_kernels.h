@@ -1353,7 +1353,10 @@ __device__ __forceinline__ uint2 crc_run64(const uint32_t* lds, const uint4 (&w)
 // dwordx4 loads, lane stride 32 B) so the row shift (8 S lookups) is paid
 // once per 32 bytes: 40 instead of 48 lookups per 32 B. The lane then plays
 // the 2G-lane geometry's blocks 2l, 2l+1 (kc = lane_consts64(2G)).
-template <int G, int U, int D, int V = 1, int B = 1>
+// ABL != 0 only in bench-only ablation builds (probes.hip); results are then
+// NOT CRCs: 1 = no S (row-shift) lookups, 2 = one D step per block instead of
+// two, 4 = no table lookups at all.
+template <int G, int U, int D, int V = 1, int B = 1, int ABL = 0>
 __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
     build_tables64(lds, kc);
@@ -1422,9 +1425,22 @@ __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args arg
             advance();
             uint2 c[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) c[u] = crc_run64<B>(lds, ring[d][u], la);
+            for (int u = 0; u < U; ++u) {
+                if constexpr (ABL & 4) {
+                    c[u] = make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w);
+                } else if constexpr (ABL & 2) {
+                    c[u] = dstep64(lds, make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w),
+                                   la);
+                } else {
+                    c[u] = crc_run64<B>(lds, ring[d][u], la);
+                }
+            }
 #pragma unroll
-            for (int u = 0; u < U; ++u) pc[u % V] = sstep64(lds, pc[u % V], la, c[u]);
+            for (int u = 0; u < U; ++u) {
+                if constexpr (ABL & 1) pc[u % V] = make_uint2((pc[u % V].x ^ (pc[u % V].y << 1)) ^ c[u].x,
+                                                              (pc[u % V].y ^ (pc[u % V].x >> 1)) ^ c[u].y);
+                else pc[u % V] = sstep64(lds, pc[u % V], la, c[u]);
+            }
             if (++step == spb) {
                 uint64_t acc = 0;
 #pragma unroll

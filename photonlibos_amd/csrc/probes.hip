@@ -103,6 +103,34 @@ int probe_crc_ablate(const void* base, uint64_t nbytes, uint64_t count, uint32_t
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// The CRC-64 streaming kernel (G=32, U=4, D=3) with parts of the arithmetic
+// removed: 1 no S lookups, 2 one D step per block, 4 no lookups (and sums).
+int probe_crc64_ablate(const void* base, uint64_t nbytes, uint64_t count, uint64_t* out, int abl, int cus,
+                       void* stream) {
+    using namespace pcrc;
+    constexpr int G = 32;
+    LaneConsts64 kc;
+    kc.kshift = xpow64(8ull * 16ull * G);
+    for (int k = 0; k < 6; ++k)
+        for (int i = 0; i < 64; ++i) kc.basis[k][i] = mulmod64(1ull << i, xpow64(128ull << k));
+    Uniform64Args a{static_cast<const uint8_t*>(base), nbytes, nbytes / (16ull * G), count, out, 0};
+    const uint64_t waves = (count + 1) / 2;
+    uint64_t grid = (waves + 15) / 16;
+    if (grid > (uint64_t)cus) grid = cus;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+#define AB64(X) hipLaunchKernelGGL((crc64_uniform_kernel<G, 4, 3, 1, 1, X>), dim3(grid), dim3(kBlock), 0, s, a, kc)
+    switch (abl) {
+        case 1: AB64(1); break;
+        case 2: AB64(2); break;
+        case 3: AB64(3); break;
+        case 4: AB64(4); break;
+        case 5: AB64(5); break;
+        default: AB64(0); break;
+    }
+#undef AB64
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 int probe_read_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink, int blocks,
                     int u, int nt, void* stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
