@@ -55,3 +55,23 @@ def test_cpp_rpc_batch_example():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 wrong verdicts" in r.stdout
+
+
+def test_host_engines_under_asan(tmp_path):
+    # Host code only (no GPU sanitizer on this pool): the drop-in engines
+    # compiled with -fsanitize=address,undefined and driven at every length
+    # and misalignment.
+    import shutil
+    gxx = shutil.which("g++")
+    if not gxx:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "asan_host_engines")
+    src = [os.path.join(ROOT, "tests", "cpp", "asan_host_engines.cpp"),
+           os.path.join(ROOT, "photonlibos_amd", "csrc", "crc32c_cpu.cpp"),
+           os.path.join(ROOT, "photonlibos_amd", "csrc", "crc64_cpu.cpp")]
+    subprocess.run([gxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", "-I" + os.path.join(ROOT, "include")] + src + ["-o", exe],
+                   check=True, timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "asan64: 0 mismatches" in r.stdout
