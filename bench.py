@@ -219,6 +219,23 @@ def cpu_baseline(cfg, seconds):
             "kind": "port", "sample": f"{len(bufs)} x {n} B, oracle slicing-by-8, 1 thread"}
 
 
+def cpu_reference_c1(seconds):
+    """config C1 (1024 x 4 KiB, the reference's CPU-runnable
+    case) with Photon's own crc32c() on 1 thread and on 16 threads, beside the
+    main baseline. Empty when the reference build is absent."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return {}
+    out = {}
+    for threads in (1, max(1, min(16, os.cpu_count() or 1))):
+        r = subprocess.run([harness, "bench", "1024", "4096", str(threads), str(seconds)],
+                           capture_output=True, text=True, timeout=seconds * 4 + 60)
+        if r.returncode == 0:
+            out[f"threads_{threads}"] = round(json.loads(r.stdout.strip().splitlines()[-1])["gib_per_s"], 3)
+    return {"unit": "GiB/s", "workload": "C1: 1024 x 4 KiB random buffers (cache-resident), Photon crc32c()",
+            **out} if out else {}
+
+
 def load_traffic(path, config):
     if path is None:
         path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
@@ -405,6 +422,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            res["cpu_reference_c1"] = cpu_reference_c1(min(5.0, args.cpu_seconds))
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
