@@ -1,0 +1,148 @@
+"""Randomised parity: many random shapes through every CRC32C / CRC-64 device
+entry point and engine variant, checked bit-exactly against the pinned
+oracle (tests/_oracle.py). Seeds are fixed, so a failure reproduces."""
+import random
+
+import numpy as np
+import pytest
+
+from photonlibos_amd import checksum as ck
+from photonlibos_amd import datagen
+
+pytestmark = pytest.mark.gpu
+
+POOL = 4 << 20
+
+
+@pytest.fixture(scope="module")
+def dev_pool():
+    import torch
+    assert torch.cuda.is_available()
+    host = datagen.stream_bytes(0xF022, POOL)
+    return torch, host, torch.from_numpy(host.copy()).cuda()
+
+
+@pytest.fixture(autouse=True)
+def _reset():
+    yield
+    ck.set_lanes_per_buffer(0)
+    ck.set_generic_rows(4)
+    ck.set_stream_config(0, 0, 0)
+    ck.set_msg_mode(0)
+
+
+ENGINES = [  # (lanes, generic rows, streaming shape)
+    (0, 4, None), (4, 4, None), (8, 2, None), (16, 8, None), (32, 4, None), (64, 4, None),
+    (0, 0, None), (8, 0, None), (64, 0, None),           # fused kernel
+    (8, 4, (1, 4, 3)), (32, 4, (2, 2, 3)),               # streaming kernel (uniform batches only)
+]
+
+
+def _lengths(rnd, k):
+    out = []
+    for _ in range(k):
+        r = rnd.random()
+        out.append(rnd.randrange(0, 80) if r < 0.3 else rnd.randrange(80, 5000) if r < 0.8
+                   else rnd.randrange(5000, 300000))
+    return out
+
+
+@pytest.mark.parametrize("round_", range(4))
+def test_fuzz_iov_batches(dev_pool, oracle, round_):
+    torch, host, d = dev_pool
+    rnd = random.Random(1000 + round_)
+    for lanes, rows, stream in ENGINES:
+        ck.set_lanes_per_buffer(lanes)
+        ck.set_generic_rows(rows)
+        ck.set_stream_config(*(stream or (0, 0, 0)))
+        lens = _lengths(rnd, 120)
+        offs = [rnd.randrange(0, POOL - n) for n in lens]
+        seeds = [rnd.getrandbits(32) if rnd.random() < 0.7 else 0 for _ in lens]
+        iov = np.zeros((len(lens), 2), np.uint64)
+        iov[:, 0] = np.uint64(d.data_ptr()) + np.asarray(offs, np.uint64)
+        iov[:, 1] = np.asarray(lens, np.uint64)
+        d_iov = torch.from_numpy(iov.view(np.int64)).cuda()
+        d_seeds = torch.from_numpy(np.asarray(seeds, np.uint32).view(np.int32)).cuda()
+        out = torch.zeros(len(lens), dtype=torch.int32, device="cuda")
+        ck.batch_iov(d_iov, len(lens), out, seeds=d_seeds)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        for k, (o, n, s) in enumerate(zip(offs, lens, seeds)):
+            assert got[k] == oracle.crc32c(host[o:o + n], s), (lanes, rows, stream, o, n, s)
+
+
+@pytest.mark.parametrize("round_", range(3))
+def test_fuzz_strided_batches(dev_pool, oracle, round_):
+    torch, host, d = dev_pool
+    rnd = random.Random(2000 + round_)
+    for lanes, rows, stream in ENGINES:
+        ck.set_lanes_per_buffer(lanes)
+        ck.set_generic_rows(rows)
+        ck.set_stream_config(*(stream or (0, 0, 0)))
+        aligned = rnd.random() < 0.5
+        nbytes = rnd.choice([4096, 8192, 65536, 16 * 64 * 4]) if aligned else rnd.randrange(1, 70000)
+        stride = nbytes if aligned else nbytes + rnd.randrange(0, 64)
+        count = max(1, min(rnd.randrange(1, 300), (POOL - 64) // stride))
+        base = 0 if aligned else rnd.randrange(0, 16)
+        seed0 = rnd.getrandbits(32)
+        out = torch.zeros(count, dtype=torch.int32, device="cuda")
+        ck.batch_strided(d.data_ptr() + base, stride, nbytes, count, out, seed=seed0)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        for i in range(count):
+            o = base + i * stride
+            assert got[i] == oracle.crc32c(host[o:o + nbytes], seed0), (lanes, rows, stream, nbytes, stride, i)
+
+
+@pytest.mark.parametrize("round_", range(3))
+def test_fuzz_messages(dev_pool, oracle, round_):
+    torch, host, d = dev_pool
+    rnd = random.Random(3000 + round_)
+    for mode in (0, 1, 2):
+        for lanes in (0, 8, 64):
+            ck.set_msg_mode(mode)
+            ck.set_lanes_per_buffer(lanes)
+            nmsg = rnd.randrange(1, 400)
+            iov, start, msgs = [], [0], []
+            for _ in range(nmsg):
+                parts = []
+                for n in _lengths(rnd, rnd.choice([0, 1, 2, 5, 12])):
+                    n = min(n, 40000)
+                    o = rnd.randrange(0, POOL - n)
+                    iov.append((d.data_ptr() + o, n))
+                    parts.append(host[o:o + n])
+                start.append(len(iov))
+                msgs.append(parts)
+            seeds = [rnd.getrandbits(32) for _ in range(nmsg)]
+            d_iov = torch.from_numpy(np.asarray(iov or [(0, 0)], np.uint64).view(np.int64)).cuda()
+            d_start = torch.from_numpy(np.asarray(start, np.uint64).view(np.int64)).cuda()
+            d_seeds = torch.from_numpy(np.asarray(seeds, np.uint32).view(np.int32)).cuda()
+            out = torch.zeros(nmsg, dtype=torch.int32, device="cuda")
+            seg = torch.zeros(max(len(iov), 1), dtype=torch.int32, device="cuda") if rnd.random() < 0.5 else None
+            ck.batch_msg_n(d_iov, d_start, nmsg, len(iov), seg, out, seeds=d_seeds)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint32)
+            for m, parts in enumerate(msgs):
+                assert got[m] == oracle.extend_chain(parts, seeds[m]), (mode, lanes, m)
+
+
+@pytest.mark.parametrize("round_", range(2))
+def test_fuzz_crc64(dev_pool, oracle, round_):
+    torch, host, d = dev_pool
+    rnd = random.Random(4000 + round_)
+    for lanes in (0, 8, 32, 64):
+        ck.set_lanes_per_buffer(lanes)
+        lens = _lengths(rnd, 80)
+        offs = [rnd.randrange(0, POOL - n) for n in lens]
+        seeds = [rnd.getrandbits(64) for _ in lens]
+        iov = np.zeros((len(lens), 2), np.uint64)
+        iov[:, 0] = np.uint64(d.data_ptr()) + np.asarray(offs, np.uint64)
+        iov[:, 1] = np.asarray(lens, np.uint64)
+        d_iov = torch.from_numpy(iov.view(np.int64)).cuda()
+        d_seeds = torch.from_numpy(np.asarray(seeds, np.uint64).view(np.int64)).cuda()
+        out = torch.zeros(len(lens), dtype=torch.int64, device="cuda")
+        ck.batch64_iov(d_iov, len(lens), out, seeds=d_seeds)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64)
+        for k, (o, n, s) in enumerate(zip(offs, lens, seeds)):
+            assert int(got[k]) == oracle.crc64ecma(host[o:o + n], s), (lanes, o, n)
