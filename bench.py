@@ -63,6 +63,7 @@ def parse(argv=None):
                     help="with --h2d: shard the host batch over this many devices of ONE process (0 = all)")
     ap.add_argument("--file-records", action="store_true", help="file records through the pread pipeline (DESIGN.md)")
     ap.add_argument("--rpc-batch", action="store_true", help="CheckedMessage batch over pinned host payloads (DESIGN.md)")
+    ap.add_argument("--rpc-latency", action="store_true", help="submit+wait latency of small CheckedMessage batches")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -325,6 +326,49 @@ def run_rpc_batch(args, stream):
         alloc.dealloc(a)
 
 
+def run_rpc_latency(args, stream):
+    """Latency of one CheckedMessage batch submit + wait (descriptors H2D,
+    kernel(s), verdicts D2H) for 1..4096 messages of 8 x 8 KiB segments in
+    pinned host memory, against Photon's own crc32c_extend chain on one core
+    for the same messages (the drop-in host engine). Median of 50. DESIGN.md."""
+    from photonlibos_amd.checked import MessageBatch, PinnedAlloc
+    n, nseg = 8192, 8
+    alloc = PinnedAlloc()
+    region = 64 << 20
+    per_region = region // n
+    maxmsg = 4096
+    regions = [alloc.alloc(region) for _ in range((maxmsg * nseg + per_region - 1) // per_region)]
+    for r, a in enumerate(regions):
+        ck.fill_splitmix(a, n, n, per_region, 0x5EED0001 + r * per_region, stream=stream)
+    torch.cuda.synchronize()
+    addr = [regions[s // per_region] + (s % per_region) * n for s in range(maxmsg * nseg)]
+    rows = []
+    for k in (1, 16, 256, 4096):
+        batch = MessageBatch(k, k * nseg)
+        for m in range(k):
+            batch.add([(addr[m * nseg + j], n) for j in range(nseg)])
+        ts = []
+        for _ in range(55):
+            t0 = time.perf_counter()
+            batch.submit(stream.cuda_stream)
+            batch.wait()
+            ts.append(time.perf_counter() - t0)
+        gpu_us = float(np.median(ts[5:])) * 1e6
+        row = {"messages": k, "payload_bytes": k * nseg * n, "gpu_submit_wait_us": round(gpu_us, 1)}
+        harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+        if os.path.exists(harness):  # Photon's crc32c() over the same byte count, one core
+            r = subprocess.run([harness, "bench", str(k * nseg), str(n), "1", "1"], capture_output=True, text=True,
+                               timeout=120)
+            if r.returncode == 0:
+                row["photon_cpu_1core_us"] = round(json.loads(r.stdout.strip().splitlines()[-1])["best_s"] * 1e6, 1)
+        rows.append(row)
+        batch.close()
+    for a in regions:
+        alloc.dealloc(a)
+    print(json.dumps({"metric": "CheckedMessage batch latency (submit + wait), 8 x 8 KiB messages in pinned host memory",
+                      "rows": rows}))
+
+
 def run_file_records(args):
     """§8(f) row 4: CRC32C of the 4 KiB records of a 1 GiB file (page-cache
     hot, buffered pread into pinned chunks + GPU pipeline), end to end.
@@ -375,6 +419,10 @@ def main():
     if args.rpc_batch:
         if rank == 0:
             run_rpc_batch(args, stream)
+        return
+    if args.rpc_latency:
+        if rank == 0:
+            run_rpc_latency(args, stream)
         return
     if args.file_records:
         if rank == 0:

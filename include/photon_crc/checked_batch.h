@@ -75,6 +75,8 @@ int64_t photon_crc_pinned_release(void);
 typedef struct photon_crc_msg_batch photon_crc_msg_batch;
 
 #define PHOTON_CRC_BATCH_TRUSTED 1u /* skip the per-segment accessibility check */
+#define PHOTON_CRC_BATCH_STAGED 2u  /* copy descriptors H2D and verdicts D2H instead of
+                                       the kernels reading / writing the pinned staging */
 
 /* A batch on the current device with room for max_messages messages and
  * max_segments segments in total (bodies count as segments). NULL on error. */
@@ -89,9 +91,11 @@ void photon_crc_msg_batch_destroy(photon_crc_msg_batch* b);
 int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec* iov, uint32_t iovcnt,
                                  const void* body, uint64_t body_length, uint32_t expected);
 
-/* Launch the whole batch on `stream` (NULL = default stream): descriptors go
- * H2D from pinned staging, the kernels read the segments in place, results
- * come back D2H. If `done` is non-NULL it is called once the results are on
+/* Launch the whole batch on `stream` (NULL = default stream): the kernels
+ * read the descriptors from pinned staging and the segments in place, and
+ * write the verdict CRCs to pinned memory (one launch; with
+ * PHOTON_CRC_BATCH_STAGED the descriptors are copied H2D and the results
+ * D2H around it). If `done` is non-NULL it is called once the results are on
  * the host, from a HIP runtime thread (it may call photon::semaphore::signal,
  * thread/thread.h:511-520); it must not call HIP. A completed batch may be
  * submitted again (its payloads re-read, e.g. after they were refilled);

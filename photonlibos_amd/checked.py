@@ -45,6 +45,7 @@ class PinnedAlloc:
 
 
 TRUSTED = 1
+STAGED = 2  # descriptors H2D / verdicts D2H instead of zero-copy staging
 
 
 class MessageBatch:

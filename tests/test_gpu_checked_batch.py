@@ -52,11 +52,12 @@ def _expected(alloc, oracle, segs, body):
     return oracle.extend_chain(data, 0)
 
 
-def test_validate_batch_matches_oracle(torch_dev, oracle):
+@pytest.mark.parametrize("flags", [0, 2])  # zero-copy staging (default) / STAGED copies
+def test_validate_batch_matches_oracle(torch_dev, oracle, flags):
     rng = random.Random(11)
     alloc = PinnedAlloc()
     msgs, blocks = _messages(alloc, rng, 300, 9, 20000)
-    b = MessageBatch(512, 4096)
+    b = MessageBatch(512, 4096, flags)
     exp = [_expected(alloc, oracle, s, body) for s, body in msgs]
     bad = set(rng.sample(range(len(msgs)), 17))
     for i, (segs, body) in enumerate(msgs):
@@ -83,7 +84,8 @@ def test_validate_batch_matches_oracle(torch_dev, oracle):
     assert alloc.release() == slab
 
 
-def test_payload_corruption_detected(torch_dev, oracle):
+@pytest.mark.parametrize("flags", [0, 2])
+def test_payload_corruption_detected(torch_dev, oracle, flags):
     rng = random.Random(12)
     alloc = PinnedAlloc()
     msgs, blocks = _messages(alloc, rng, 64, 8, 8192)
@@ -94,7 +96,7 @@ def test_payload_corruption_detected(torch_dev, oracle):
             a, n = body if not any(n for _, n in segs) else next((a, n) for a, n in segs if n)
             v = alloc.view(a, n)
             v[rng.randrange(n)] ^= 1 << rng.randrange(8)
-    b = MessageBatch(64, 1024)
+    b = MessageBatch(64, 1024, flags)
     for i, (segs, body) in enumerate(msgs):
         b.add(segs, body, exp[i])
     b.submit()
