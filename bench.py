@@ -278,8 +278,8 @@ def run_rpc_batch(args, stream):
     """§8(f) row 1: CheckedMessage validation batched over RPC payloads held in
     pinned host memory (the pinned IOAlloc pool), C5 shape: 65536 messages x 8
     non-contiguous 8 KiB segments. One step = submit + wait of the whole batch
-    (descriptors H2D, kernels reading the payload in place over the host link,
-    verdicts D2H). Reported in DESIGN.md, never as `value`."""
+    (kernels reading descriptors and payload in place over the host link and
+    writing the verdicts to pinned memory). Reported in DESIGN.md, never as `value`."""
     from photonlibos_amd.checked import MessageBatch, PinnedAlloc
     cfg = CONFIGS["c5"]
     n, cnt, nseg = cfg["nbytes"], cfg["count"], cfg["nseg"]
@@ -316,7 +316,7 @@ def run_rpc_batch(args, stream):
     elapsed, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
     nbytes = n * slots
     print(json.dumps({"metric": "GiB/s CRC32C CheckedMessage batch validation, payload in pinned host memory "
-                                "(descriptors H2D + zero-copy kernels + verdicts D2H)",
+                                "(zero-copy: descriptors, payload and verdicts in pinned memory)",
                       "value": round(nbytes * steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": 1,
                       "steps": steps, "ms_per_step": round(elapsed / steps * 1e3, 3),
                       "add_us_per_message_python": round(add_s / cnt * 1e6, 2), "self_check": all(check),
@@ -327,10 +327,10 @@ def run_rpc_batch(args, stream):
 
 
 def run_rpc_latency(args, stream):
-    """Latency of one CheckedMessage batch submit + wait (descriptors H2D,
-    kernel(s), verdicts D2H) for 1..4096 messages of 8 x 8 KiB segments in
-    pinned host memory, against Photon's own crc32c_extend chain on one core
-    for the same messages (the drop-in host engine). Median of 50. DESIGN.md."""
+    """Latency of one CheckedMessage batch submit + wait (zero-copy descriptors
+    and verdicts, one launch) for 1..4096 messages of 8 x 8 KiB segments in
+    pinned host memory, beside Photon's own crc32c() on one core over the same
+    byte count (oracle/_ref harness, when built). Median of 50. DESIGN.md."""
     from photonlibos_amd.checked import MessageBatch, PinnedAlloc
     n, nseg = 8192, 8
     alloc = PinnedAlloc()
