@@ -133,6 +133,7 @@ struct photon_crc_msg_batch {
     photon_crc_iovec* d_iov = nullptr;
     uint64_t* d_start = nullptr;
     uint32_t* d_out = nullptr;
+    uint32_t* d_seg = nullptr;  // segment CRCs of the two-kernel form (device memory)
     hipEvent_t done_ev = nullptr;
     uint64_t nmsg = 0, nseg = 0;
     uint64_t host_bytes = 0, total_bytes = 0;  // payload in host memory / all (lane choice)
@@ -149,6 +150,7 @@ void free_batch(photon_crc_msg_batch* b) {
     if (!b->zero_copy)
         for (void* p : {(void*)b->d_iov, (void*)b->d_start, (void*)b->d_out})
             if (p) (void)hipFree(p);
+    if (b->d_seg) (void)hipFree(b->d_seg);
     delete b;
 }
 
@@ -274,7 +276,7 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
         if (e != hipSuccess) return;
         // Zero-copy: the kernels read the descriptors from and write the
         // verdicts to the pinned staging directly (no H2D / D2H copies: one
-        // launch per submit: 57 -> 44 us for one message).
+        // launch per submit).
         e = b->zero_copy ? hipHostGetDevicePointer(p, host, 0) : hipMalloc(p, n);
     };
     hm((void**)&b->h_iov, S * sizeof(photon_crc_iovec));
@@ -284,6 +286,7 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
     dm((void**)&b->d_iov, b->h_iov, S * sizeof(photon_crc_iovec));
     dm((void**)&b->d_start, b->h_start, (M + 1) * 8);
     dm((void**)&b->d_out, b->h_out, M * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&b->d_seg, S * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         report_hip_error(e, "photon_crc_msg_batch_create");
@@ -347,7 +350,7 @@ int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*do
             if (e != hipSuccess) return report_hip_error(e, "hipMemcpyAsync(descriptors)");
         }
         rc = pcrc::batch_msg_lanes(b->d_iov, b->d_start, b->nmsg, b->nseg, 0, nullptr, nullptr, b->d_out, stream,
-                                   lanes_for(b->host_bytes, b->total_bytes));
+                                   lanes_for(b->host_bytes, b->total_bytes), b->d_seg);
         if (rc) return rc;
         if (!b->zero_copy) {
             e = hipMemcpyAsync(b->h_out, b->d_out, b->nmsg * 4, hipMemcpyDeviceToHost, st);

@@ -795,7 +795,7 @@ int photon_crc32c_batch_msg(const photon_crc_iovec* d_iov, const uint64_t* d_msg
 // (longer contiguous requests), see checked_batch.cpp.
 int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg, uint64_t nseg,
                           uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out,
-                          void* stream, int lanes) {
+                          void* stream, int lanes, uint32_t* seg_scratch) {
     if (!nmsg) return 0;
     if (!d_iov || !d_msg_start || !d_out) return fail(-EINVAL, "null argument");
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -841,7 +841,9 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
         return e == hipSuccess ? 0 : hip_fail(e, "crc32c_batch_kernel<msg> launch");
     }
     void* scratch = nullptr;  // segment CRCs the caller did not ask for
-    if (!d_seg_out && nseg) {
+    if (!d_seg_out && nseg && seg_scratch) {
+        a.out = seg_scratch;
+    } else if (!d_seg_out && nseg) {
         e = hipMallocAsync(&scratch, nseg * 4, st);
         if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
         a.out = static_cast<uint32_t*>(scratch);

@@ -12,7 +12,9 @@ int report_error(int code, const char* what);
 int report_hip_error(hipError_t e, const char* what);
 // photon_crc32c_batch_msg_n with an explicit lane-group size (0 = automatic;
 // 4, 8, 16, 32 or 64).
+// seg_scratch (nseg words, optional): where the two-kernel form keeps the
+// segment CRCs when d_seg_out is NULL (else stream-ordered scratch is used).
 int batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg, uint64_t nseg,
                     uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out, void* stream,
-                    int lanes);
+                    int lanes, uint32_t* seg_scratch = nullptr);
 }  // namespace pcrc
