@@ -49,6 +49,7 @@
 
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "crc32c_kernels.h"
+#include "crc64_kernels.h"
 #include "gf2.h"
 #include "internal.h"
 

@@ -1024,562 +1024,4 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint
     sink[tid] = acc;
 }
 
-// ============================================================ CRC-64/ECMA
-// Same column algorithm at 64 bits (reference crc64ecma_sw, crc.cpp:119-122:
-// reflected poly 0xC96C5795D7870F42, register inverted in and out). Values
-// are kept as two 32-bit halves (uint2: .x = low, .y = high); 64-bit table
-// entries are read with ds_read_b64 (bank = (addr/4) mod 64, lane groups of
-// 32 lanes, 2 banks per lane). LDS holds
-//   D64: x -> x * x^64 mod P64, 8 byte slices x 256 x 4 replicas,
-//        layout [idx][slice t][lane%4] (256 B per index)             64 KiB
-//   S64: P -> P * x^(8*16*G), same layout, at +64 KiB                   64 KiB
-//   lane-combine tables x^(128*2^k), k < 6, nibble-sliced              12 KiB
-// Conflict-free lookups with only 4 replicas: lane l takes its 8 slices in
-// the rotated order t = (i + q) % 8, q = (l/4) % 8, so in every lookup
-// instruction i the 32 lanes of a group hit 32 distinct (t, replica) bank
-// pairs. The rotation is applied to the looked-up VALUE (two v_perm_b32 with
-// per-lane selectors: byte i of x_rot = byte (i+q)%8 of x), so the address
-// of lookup i is ONE v_perm_b32 {off_i.byte0, x_rot.byte i, 0 | off_i.byte2, 0}
-// with off_i = ((i+q)%8)*32 + (l%4)*8 (+ 1<<16, selected for S).
-constexpr uint32_t k64SBase = 65536u;
-// Lane-combine tables R64_k: p -> p * x^(128*2^k), k < 6, NIBBLE-sliced
-// (16 positions x 16 values x 8 B = 2 KiB per k): used once per buffer.
-constexpr uint32_t k64RBase = 131072u;
-constexpr uint32_t k64LdsBytes = k64RBase + 6u * 16u * 16u * 8u;  // 143360 B
-
-struct LaneConsts64 {
-    uint64_t kshift;           // x^(8*16*G) mod P64
-    uint64_t basis[6][64];     // basis of x^(128 * 2^k)
-};
-
-struct SeedConsts64 {
-    uint64_t basis[64];        // basis of x^(8 * nbytes) mod P64
-};
-
-struct Batch64Args {
-    const uint8_t* base;
-    uint64_t stride;
-    uint64_t nbytes;
-    const photon_crc_iovec* iov;
-    uint64_t count;
-    const uint64_t* seeds;
-    uint64_t* out;
-    uint64_t seed0;
-};
-
-struct Uniform64Args {
-    const uint8_t* base;
-    uint64_t stride;
-    uint64_t rows;             // nbytes / (16*G)
-    uint64_t count;
-    uint64_t* out;
-    uint64_t init_shift;       // (~seed0) * x^(8*nbytes): the inverted init's contribution
-};
-
-__device__ __forceinline__ uint2 lds_u2(const uint32_t* lds, uint32_t byte_addr) {
-    return *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + byte_addr);
-}
-
-__device__ __forceinline__ uint2 xor2(uint2 a, uint2 b) { return make_uint2(a.x ^ b.x, a.y ^ b.y); }
-
-struct LaneAddr64 {
-    uint32_t rot_lo, rot_hi;   // v_perm selectors rotating a 64-bit value right by 8q bits
-    uint32_t off[8];           // off_i = ((i+q)%8)*32 + (lane%4)*8 | 1<<16
-    uint32_t r8;               // (lane%4)*8, for the byte-serial tail
-};
-
-__device__ __forceinline__ LaneAddr64 lane_addr64(uint32_t lane) {
-    LaneAddr64 a;
-    const uint32_t q = (lane >> 2) & 7u, r = lane & 3u;
-    // perm(hi, lo, sel): source bytes 0-3 = lo, 4-7 = hi; result byte i = byte (i+q)%8.
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        lo |= ((i + q) & 7u) << (8 * i);
-        hi |= ((i + 4 + q) & 7u) << (8 * i);
-    }
-    a.rot_lo = lo;
-    a.rot_hi = hi;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a.off[i] = (((i + q) & 7u) << 5) | (r << 3) | (1u << 16);
-    a.r8 = r << 3;
-    return a;
-}
-
-__device__ __forceinline__ uint2 rot64(uint2 x, const LaneAddr64& a) {
-    return make_uint2(__builtin_amdgcn_perm(x.y, x.x, a.rot_lo), __builtin_amdgcn_perm(x.y, x.x, a.rot_hi));
-}
-
-// Lookup i (0..7) of the rotated value's byte i; TS = 0 for D64, 1 for S64.
-template <int I, int TS>
-__device__ __forceinline__ uint2 look64(const uint32_t* lds, uint2 xr, const LaneAddr64& a) {
-    const uint32_t half = I < 4 ? xr.x : xr.y;
-    const uint32_t sel = (TS ? 0x0C020000u : 0x0C0C0000u) | ((4u + (I & 3)) << 8);
-    return lds_u2(lds, __builtin_amdgcn_perm(half, a.off[I], sel));
-}
-
-// Table product of x (8 lookups) XORed with e: 4 v_bitop3 per half.
-template <int TS>
-__device__ __forceinline__ uint2 step64(const uint32_t* lds, uint2 x, const LaneAddr64& a, uint2 e) {
-    const uint2 xr = rot64(x, a);
-    const uint2 l0 = look64<0, TS>(lds, xr, a), l1 = look64<1, TS>(lds, xr, a);
-    const uint2 l2 = look64<2, TS>(lds, xr, a), l3 = look64<3, TS>(lds, xr, a);
-    const uint2 l4 = look64<4, TS>(lds, xr, a), l5 = look64<5, TS>(lds, xr, a);
-    const uint2 l6 = look64<6, TS>(lds, xr, a), l7 = look64<7, TS>(lds, xr, a);
-    return make_uint2(xor3(xor3(l0.x, l1.x, l2.x), xor3(l3.x, l4.x, l5.x), xor3(l6.x, l7.x, e.x)),
-                      xor3(xor3(l0.y, l1.y, l2.y), xor3(l3.y, l4.y, l5.y), xor3(l6.y, l7.y, e.y)));
-}
-
-// x * x^64 mod P64 (^ e).
-__device__ __forceinline__ uint2 dstep64(const uint32_t* lds, uint2 x, const LaneAddr64& a,
-                                         uint2 e = make_uint2(0, 0)) {
-    return step64<0>(lds, x, a, e);
-}
-
-// P * x^(8*16*G) mod P64 (^ e).
-__device__ __forceinline__ uint2 sstep64(const uint32_t* lds, uint2 p, const LaneAddr64& a,
-                                         uint2 e = make_uint2(0, 0)) {
-    return step64<1>(lds, p, a, e);
-}
-
-// CRC register (init 0) after a 16-byte block.
-__device__ __forceinline__ uint2 crc16_64(const uint32_t* lds, uint4 w, const LaneAddr64& a) {
-    return dstep64(lds, dstep64(lds, make_uint2(w.x, w.y), a, make_uint2(w.z, w.w)), a);
-}
-
-__device__ __forceinline__ uint64_t u64of(uint2 v) { return ((uint64_t)v.y << 32) | v.x; }
-__device__ __forceinline__ uint2 u2of(uint64_t v) { return make_uint2((uint32_t)v, (uint32_t)(v >> 32)); }
-
-// Byte-serial step: D64 slice 7 = (b << 56) * x^64 = b * x^8, the classic byte table.
-__device__ __forceinline__ uint64_t bytestep64(const uint32_t* lds, uint64_t c, uint8_t b, const LaneAddr64& a) {
-    const uint2 t = lds_u2(lds, ((uint32_t)((c ^ b) & 0xffu) << 8) + 7u * 32u + a.r8);
-    return u64of(t) ^ (c >> 8);
-}
-
-// p * x^(128*2^k) through the nibble tables R64_k (16 lookups).
-__device__ __forceinline__ uint64_t mul_r64(uint64_t p, const uint32_t* lds, int k) {
-    const char* R = reinterpret_cast<const char*>(lds) + k64RBase + k * 2048;
-    uint2 v[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m)
-        v[m] = *reinterpret_cast<const uint2*>(R + m * 128 + (((uint32_t)(p >> (4 * m)) & 15u) << 3));
-    uint32_t lo = xor3(xor3(v[0].x, v[1].x, v[2].x), xor3(v[3].x, v[4].x, v[5].x), xor3(v[6].x, v[7].x, v[8].x));
-    uint32_t hi = xor3(xor3(v[0].y, v[1].y, v[2].y), xor3(v[3].y, v[4].y, v[5].y), xor3(v[6].y, v[7].y, v[8].y));
-    lo = xor3(lo, xor3(v[9].x, v[10].x, v[11].x), xor3(v[12].x, v[13].x, v[14].x)) ^ v[15].x;
-    hi = xor3(hi, xor3(v[9].y, v[10].y, v[11].y), xor3(v[12].y, v[13].y, v[14].y)) ^ v[15].y;
-    return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t mul_basis64(uint64_t p, const uint64_t* basis) {
-    uint64_t r = 0;
-#pragma unroll 4
-    for (int i = 0; i < 64; ++i) r ^= (0ull - ((p >> i) & 1ull)) & basis[i];
-    return r;
-}
-
-// Words at byte offset `off` of the first 16-byte blocks: zero the bytes
-// before the data start s0, XOR the (already inverted) 64-bit init into data
-// bytes s0..s0+7.
-__device__ __forceinline__ uint64_t head_word64(uint64_t w, int off, int s0, uint64_t init) {
-    const int k = s0 - off;
-    if (k >= 8) return 0ull;
-    if (k > 0) w &= ~0ull << (8 * k);
-    if (k >= 0) w ^= init << (8 * k);
-    else if (k > -8) w ^= init >> (8 * -k);
-    return w;
-}
-
-__device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64& kc) {
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t e = tid; e < 2048u; e += kBlock) {
-        const uint32_t t = e >> 8, b = e & 255u;
-        const uint64_t v = (uint64_t)b << (8 * t);
-        const uint2 dv = u2of(mulmod64(v, kPoly64 /* x^64 mod P64 = the reflected polynomial */));
-        const uint2 sv = u2of(mulmod64(v, kc.kshift));
-        const uint32_t base = (b << 8) + (t << 5);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + base + r * 8) = dv;
-            *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64SBase + base + r * 8) = sv;
-        }
-    }
-    // R64_k[m][v] = (v << 4m) * x^(128*2^k): XOR of the basis words of v's bits.
-    for (uint32_t e = tid; e < 6u * 256u; e += kBlock) {
-        const uint32_t k = e >> 8, m = (e >> 4) & 15u, v = e & 15u;
-        uint64_t r = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & kc.basis[k][4 * m + j];
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64RBase + e * 8u) = u2of(r);
-    }
-    __syncthreads();
-}
-
-// p * x^(128*d) for d < 2^LOG2 (basis multiplies on the bits of d).
-template <int LOG2>
-__device__ __forceinline__ uint64_t shift64(uint64_t pc, uint32_t d, const uint32_t* lds) {
-#pragma unroll
-    for (int k = 0; k < LOG2; ++k) {
-        const uint64_t m = mul_r64(pc, lds, k);
-        pc = ((d >> k) & 1u) ? m : pc;  // every lane runs every level: no divergence
-    }
-    return pc;
-}
-
-// Shift lane partials by x^(128*d) and XOR-reduce over the G lanes.
-template <int G>
-__device__ __forceinline__ uint64_t group_reduce64(uint64_t pc, uint32_t d, const uint32_t* lds) {
-    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
-    pc = shift64<LOG2G>(pc, d, lds);
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)pc, o, 64);
-        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(pc >> 32), o, 64);
-        pc ^= ((uint64_t)hi32 << 32) | lo32;
-    }
-    return pc;
-}
-
-// Any pointer / length / seed (iovec batches, ragged and unaligned buffers).
-template <int G>
-__global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
-    build_tables64(lds, kc);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & (G - 1);
-    const uint32_t grp = lane / G;
-    constexpr int GPW = 64 / G;
-    constexpr int U = 4;
-    const LaneAddr64 la = lane_addr64(lane);
-
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave_id(); wv * GPW < args.count; wv += nwaves) {
-        const uint64_t bi = wv * GPW + grp;
-        const bool active = bi < args.count;
-        const uint8_t* p = nullptr;
-        uint64_t n = 0, seed = args.seed0;
-        if (active) {
-            if (args.iov) {
-                p = static_cast<const uint8_t*>(args.iov[bi].base);
-                n = args.iov[bi].len;
-            } else {
-                p = args.base + bi * args.stride;
-                n = args.nbytes;
-            }
-            if (args.seeds) seed = args.seeds[bi];
-        }
-        const uint64_t init = ~seed;  // crc.cpp:119-122: register starts at ~crc
-        uint64_t reg;
-        if (n < 64) {
-            reg = init;
-            if (gl == 0)
-                for (uint64_t k = 0; k < n; ++k) reg = bytestep64(lds, reg, load8(p + k), la);
-        } else {
-            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
-            const uint8_t* e = p + n;
-            const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
-            const int s0 = (int)(p - a0);
-            const uint64_t nb = (uint64_t)(eb - a0) >> 4;
-            const uint64_t full = nb / G;
-            const uint64_t rows = (nb + G - 1) / G;
-            const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);
-            const uint8_t* lp = a0 + 16 * gl;
-            uint2 pc = make_uint2(0, 0);
-            // Row 0 (head: masked leading bytes + inverted init).
-            if (gl < nb) {
-                uint4 w = load16(lp);
-                if (gl < 2) {
-                    const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
-                    const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
-                    w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-                }
-                pc = crc16_64(lds, w, la);
-            }
-            uint64_t row = 1;
-            if (row + U <= full) {
-                uint4 cur[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
-                for (; row + 2 * U <= full; row += U) {
-                    uint4 nxt[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                    uint2 c[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, cur[u], la);
-#pragma unroll
-                    for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
-#pragma unroll
-                    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-                }
-                uint2 c[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, cur[u], la);
-#pragma unroll
-                for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
-                row += U;
-            }
-            for (; row < full; ++row) pc = sstep64(lds, pc, la, crc16_64(lds, load16(lp + row * (16 * G)), la));
-            if (full >= 1 && full < rows && full * G + gl < nb)
-                pc = sstep64(lds, pc, la, crc16_64(lds, load16(lp + full * (16 * G)), la));
-            reg = group_reduce64<G>(u64of(pc), (rlast + G - 1 - gl) & (G - 1), lds);
-            if (gl == 0)
-                for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
-        }
-        if (active && gl == 0) args.out[bi] = ~reg;
-    }
-}
-
-// Uniform batches (aligned base and stride, nbytes = R*16*G with R % U == 0):
-// the continuous cross-buffer load ring of crc32c_uniform_kernel (B = 1).
-// Register init 0; lane 0 applies the inverted init (~seed0 * x^(8n)) and the
-// final inversion; per-buffer seeds are folded in by crc64_seed_kernel.
-// V interleaved partials per lane: partial j takes rows r = j (mod V), i.e.
-// lane l plays virtual lane j*G + l of a V*G-lane geometry (row shift
-// x^(8*16*G*V), the kc passed is lane_consts64(G*V)); V independent S chains
-// of U/V steps instead of one of U steps.
-// CRC register (init 0) after a run of B consecutive 16-byte blocks.
-template <int B>
-__device__ __forceinline__ uint2 crc_run64(const uint32_t* lds, const uint4 (&w)[B], const LaneAddr64& a) {
-    uint2 c = dstep64(lds, make_uint2(w[0].x, w[0].y), a, make_uint2(w[0].z, w[0].w));
-#pragma unroll
-    for (int b = 1; b < B; ++b) {
-        c = dstep64(lds, c, a, make_uint2(w[b].x, w[b].y));
-        c = dstep64(lds, c, a, make_uint2(w[b].z, w[b].w));
-    }
-    return dstep64(lds, c, a);
-}
-
-// B = 2: each lane reads a RUN of two consecutive blocks per row (two
-// dwordx4 loads, lane stride 32 B) so the row shift (8 S lookups) is paid
-// once per 32 bytes: 40 instead of 48 lookups per 32 B. The lane then plays
-// the 2G-lane geometry's blocks 2l, 2l+1 (kc = lane_consts64(2G)).
-// ABL != 0 only in bench-only ablation builds (probes.hip); results are then
-// NOT CRCs: 1 = no S (row-shift) lookups, 2 = one D step per block instead of
-// two, 4 = no table lookups at all.
-template <int G, int U, int D, int V = 1, int B = 1, int ABL = 0>
-__global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
-    build_tables64(lds, kc);
-
-    constexpr uint64_t GPW = 64 / G;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & (G - 1);
-    const uint32_t grp = lane / G;
-    const LaneAddr64 la = lane_addr64(lane);
-
-    const uint64_t ngroups = (args.count + GPW - 1) / GPW;
-    const uint64_t wv0 = (uint64_t)blockIdx.x * kWaves + wave_id();
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-    if (wv0 >= ngroups) return;
-    const uint64_t nslots = (ngroups - 1 - wv0) / nwaves + 1;
-    const uint64_t spb = args.rows / U;
-    const uint64_t nsteps = nslots * spb;
-    constexpr uint64_t kRow = 16ull * G * B;
-
-    auto buffer_of = [&](uint64_t slot) -> uint64_t {
-        const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
-        return bi < args.count ? bi : args.count - 1;
-    };
-    auto slot_base = [&](uint64_t slot) -> const uint8_t* {
-        if (slot >= nslots) slot = nslots - 1;
-        return args.base + buffer_of(slot) * args.stride + 16ull * B * gl;
-    };
-    uint64_t lslot = 0, lstep = 0;
-    const uint8_t* lptr = slot_base(0);
-    auto advance = [&]() {
-        if (++lstep == spb) {
-            lstep = 0;
-            ++lslot;
-            lptr = slot_base(lslot);
-        } else if (lslot < nslots) {
-            lptr += kRow * U;
-        }
-    };
-    constexpr int S = D + 1;
-    uint4 ring[S][U][B];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int b = 0; b < B; ++b) ring[d][u][b] = load16(lptr + u * kRow + 16 * b);
-        advance();
-    }
-    const uint64_t padded = (nsteps + S - 1) / S * S;
-    static_assert(U % V == 0 && G * V * B <= 64 && (V == 1 || B == 1),
-                  "interleave must divide the step; V*B*G virtual lanes <= 64; runs and interleave exclusive");
-    constexpr int VGB = G * V * B;
-    constexpr int LOG2VG = VGB == 64 ? 6 : VGB == 32 ? 5 : VGB == 16 ? 4 : VGB == 8 ? 3 : 2;
-    uint64_t slot = 0, step = 0;
-    uint2 pc[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) pc[j] = make_uint2(0, 0);
-    for (uint64_t s = 0; s < padded; s += S) {
-#pragma unroll
-        for (int d = 0; d < S; ++d) {
-            const int refill = (d + D) % S;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int b = 0; b < B; ++b) ring[refill][u][b] = load16(lptr + u * kRow + 16 * b);
-            advance();
-            uint2 c[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if constexpr (ABL & 4) {
-                    c[u] = make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w);
-                } else if constexpr (ABL & 2) {
-                    c[u] = dstep64(lds, make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w),
-                                   la);
-                } else {
-                    c[u] = crc_run64<B>(lds, ring[d][u], la);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if constexpr (ABL & 1) pc[u % V] = make_uint2((pc[u % V].x ^ (pc[u % V].y << 1)) ^ c[u].x,
-                                                              (pc[u % V].y ^ (pc[u % V].x >> 1)) ^ c[u].y);
-                else pc[u % V] = sstep64(lds, pc[u % V], la, c[u]);
-            }
-            if (++step == spb) {
-                uint64_t acc = 0;
-#pragma unroll
-                for (int j = 0; j < V; ++j)
-                    acc ^= shift64<LOG2VG>(u64of(pc[j]), (uint32_t)((G * V - 1 - (j * G + gl)) * B), lds);
-#pragma unroll
-                for (int o = G / 2; o > 0; o >>= 1) {
-                    const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);
-                    const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), o, 64);
-                    acc ^= ((uint64_t)hi32 << 32) | lo32;
-                }
-                const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
-                if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = ~(acc ^ args.init_shift);
-#pragma unroll
-                for (int j = 0; j < V; ++j) pc[j] = make_uint2(0, 0);
-                step = 0;
-                ++slot;
-            }
-        }
-    }
-}
-
-// out[i] ^= seed_i * x^(8*nbytes) (the uniform kernel used seed0 = 0:
-// ~(F ^ ~s*X) = ~(F ^ ~0*X) ^ s*X).
-__global__ void crc64_seed_kernel(uint64_t* out, uint64_t count, const uint64_t* seeds, SeedConsts64 sc) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    out[i] ^= mul_basis64(seeds[i], sc.basis);
-}
-
-
-// ---------------------------------------------- CRC-64 combine / fold / extend
-// crc64ecma_combine(c1, c2, len2) = c1 ? c2 ^ c1 * x^(8*len2) : c2
-// (crc.cpp crc64ecma_combine_sw: the inverted-CRC combine is linear). A
-// message's CRC chained over its segments (crc64ecma_extend, seg after seg)
-// is therefore acc = seed; acc = acc * x^(8*len_s) ^ crc64ecma(seg_s, 0).
-struct PowTable64 {
-    uint64_t x8pow2[64];  // x^(8 * 2^i) mod P64
-};
-
-constexpr uint64_t kOne64 = 1ull << 63;
-
-__device__ __forceinline__ uint64_t xpow8_tab64(uint64_t n, const PowTable64& t) {
-    uint64_t k = kOne64;
-    for (int i = 0; n; ++i, n >>= 1)
-        if (n & 1) k = mulmod64(k, t.x8pow2[i]);
-    return k;
-}
-
-__global__ void crc64_combine_kernel(const uint64_t* c1, const uint64_t* c2, const uint32_t* l2, uint64_t n,
-                                     uint64_t* out, PowTable64 pt) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t a = c1[i], b = c2[i];
-    out[i] = a ? b ^ mulmod64(a, xpow8_tab64(l2[i], pt)) : b;
-}
-
-// crc64ecma_trim per element (do_crc_trim, crc.cpp:442-456, with
-// T = CRC64ECMA_Component): 64-bit size check; shifts by the 32-bit lengths
-// crc_apply_shifts takes; combine's crc1 == 0 shortcut.
-__global__ void crc64_trim_kernel(const photon_crc64_component* all, const photon_crc64_component* pre,
-                                  const photon_crc64_component* suf, uint64_t n, uint64_t* out, uint32_t* nerr,
-                                  PowTable64 lsh, PowTable64 rsh) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const photon_crc64_component a = all[i], p = pre[i], s = suf[i];
-    if (a.size < p.size + s.size) {
-        out[i] = 0;
-        if (nerr) atomicAdd(nerr, 1u);
-        return;
-    }
-    uint64_t crc = a.crc;
-    if (p.size && p.crc) crc ^= mulmod64(p.crc, xpow8_tab64((uint32_t)(a.size - p.size), lsh));
-    if (s.size) crc = mulmod64(crc ^ s.crc, xpow8_tab64((uint32_t)s.size, rsh));
-    out[i] = crc;
-}
-
-// One thread per message (as crc32c_msg_fold_kernel).
-__global__ void crc64_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_t* msg_start, uint64_t nmsg,
-                                      const uint64_t* seg_crc, uint64_t seed0, const uint64_t* seeds,
-                                      uint64_t* out, PowTable64 pt) {
-    const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= nmsg) return;
-    const uint64_t s0 = msg_start[m], s1 = msg_start[m + 1];
-    uint64_t acc = seeds ? seeds[m] : seed0;
-    uint64_t klen = 0, k = kOne64;
-    for (uint64_t s = s0; s < s1; s += 4) {
-        uint64_t len[4], c[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (s + j < s1) {
-                len[j] = iov[s + j].len;
-                c[j] = seg_crc[s + j];
-            }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (s + j < s1) {
-                if (len[j] != klen) {
-                    k = xpow8_tab64(len[j], pt);
-                    klen = len[j];
-                }
-                acc = mulmod64(acc, k) ^ c[j];
-            }
-    }
-    out[m] = acc;
-}
-
-// One long buffer split into k pieces of `piece` bytes (the last one
-// last_len): out = sum_i crc_i * x^(8 * bytes after piece i) ^ seed * x^(8n)
-// (the seed term only for seed != 0: combine's shortcut). One 1024-thread
-// block; thread t folds a contiguous run of pieces by Horner with
-// K = x^(8*piece), shifts it past the rest, then a block XOR reduction.
-__global__ __launch_bounds__(1024) void crc64_fold_pieces_kernel(const uint64_t* crcs, uint64_t k, uint64_t piece,
-                                                                 uint64_t last_len, uint64_t seed, uint64_t nbytes,
-                                                                 uint64_t kpiece, uint64_t* out, PowTable64 pt) {
-    __shared__ uint64_t red[1024];
-    const uint32_t t = threadIdx.x;
-    const uint64_t per = (k + 1023) / 1024;
-    const uint64_t lo = t * per, hi = lo + per < k ? lo + per : k;
-    uint64_t acc = 0;
-    if (lo < hi) {
-        // pieces lo..hi-1, all full-size except possibly piece k-1 (which is
-        // then the run's last): Horner over the full pieces, last one appended.
-        for (uint64_t i = lo; i < hi; ++i) {
-            const bool last = i == k - 1;
-            acc = last ? mulmod64(acc, xpow8_tab64(last_len, pt)) ^ crcs[i] : mulmod64(acc, kpiece) ^ crcs[i];
-        }
-        // acc = sum crc_i * x^(8 * bytes from the end of piece i to the end of
-        // the run); shift it past the bytes after the run.
-        if (hi < k) acc = mulmod64(acc, xpow8_tab64((k - 1 - hi) * piece + last_len, pt));
-    }
-    red[t] = acc;
-    __syncthreads();
-    for (uint32_t o = 512; o > 0; o >>= 1) {
-        if (t < o) red[t] ^= red[t + o];
-        __syncthreads();
-    }
-    if (t == 0) *out = red[0] ^ (seed ? mulmod64(seed, xpow8_tab64(nbytes, pt)) : 0ull);
-}
-
-
 }  // namespace pcrc
