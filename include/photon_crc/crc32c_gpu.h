@@ -264,6 +264,26 @@ int photon_crc_host_unregister(void* ptr);
 int photon_crc32c_file_strided(int fd, uint64_t offset, uint64_t stride, uint64_t nbytes, uint64_t count,
                                uint32_t seed0, uint32_t* h_out);
 
+/* Runtime shim so that Photon code drives the batches without HIP headers
+ * (host code stays Photon C++; HIP stays behind this library):
+ *   stream_create / _destroy / _sync: a non-blocking stream of the current
+ *       device (the `stream` argument of the calls above);
+ *   stream_on_complete: run fn(arg) on a runtime thread once everything
+ *       enqueued on `stream` so far has finished (fn may call
+ *       photon::semaphore::signal, thread/thread.h:511-520; it must not call
+ *       into this library or HIP);
+ *   device_alloc / _free: device memory of the current device;
+ *   memcpy_async: copy n bytes between any host/device pointers, ordered on
+ *       `stream` (pinned host memory for true asynchrony).
+ * 0 or a negative errno-style code, as everywhere. */
+int photon_crc_stream_create(void** stream);
+int photon_crc_stream_destroy(void* stream);
+int photon_crc_stream_sync(void* stream);
+int photon_crc_stream_on_complete(void* stream, void (*fn)(void* arg), void* arg);
+int photon_crc_device_alloc(void** ptr, uint64_t nbytes);
+int photon_crc_device_free(void* ptr);
+int photon_crc_memcpy_async(void* dst, const void* src, uint64_t nbytes, void* stream);
+
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
  * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),

@@ -68,6 +68,13 @@ def _declare(L):
     fn("photon_crc64_set_run_blocks", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_msg_mode", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_host_register", ctypes.c_int, vp, u64)
+    fn("photon_crc_stream_create", ctypes.c_int, ctypes.POINTER(vp))
+    fn("photon_crc_stream_destroy", ctypes.c_int, vp)
+    fn("photon_crc_stream_sync", ctypes.c_int, vp)
+    fn("photon_crc_stream_on_complete", ctypes.c_int, vp, vp, vp)
+    fn("photon_crc_device_alloc", ctypes.c_int, ctypes.POINTER(vp), u64)
+    fn("photon_crc_device_free", ctypes.c_int, vp)
+    fn("photon_crc_memcpy_async", ctypes.c_int, vp, vp, u64, vp)
     fn("photon_crc_host_unregister", ctypes.c_int, vp)
     fn("photon_crc32c_file_strided", ctypes.c_int, ctypes.c_int, u64, u64, u64, u64, u32, vp)
     fn("photon_crc32c_series_device", ctypes.c_int, vp, u32, u32, vp, vp)

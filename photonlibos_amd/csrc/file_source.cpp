@@ -1,4 +1,6 @@
-// file_source.cpp -- producers of checksum input outside device memory
+// file_source.cpp -- the runtime shim (streams, device memory, copies,
+// completion callbacks: Photon code needs no HIP headers) and producers of
+// checksum input outside device memory
 // (include/photon_crc/crc32c_gpu.h):
 //   photon_crc_host_register / _unregister: make existing host buffers (e.g.
 //       the iovec targets of IFile::preadv, fs/filesystem.h:54-70) readable by
@@ -94,6 +96,56 @@ int read_span_parallel(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_ma
 }  // namespace
 
 extern "C" {
+
+int photon_crc_stream_create(void** stream) {
+    if (!stream) return report_error(-EINVAL, "null stream pointer");
+    if (photon_crc_device_count() <= 0) return -ENODEV;
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) return report_hip_error(e, "hipStreamCreateWithFlags");
+    *stream = s;
+    return 0;
+}
+
+int photon_crc_stream_destroy(void* stream) {
+    if (!stream) return 0;
+    hipError_t e = hipStreamDestroy(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipStreamDestroy");
+}
+
+int photon_crc_stream_sync(void* stream) {
+    if (photon_crc_device_count() <= 0) return -ENODEV;
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipStreamSynchronize");
+}
+
+int photon_crc_stream_on_complete(void* stream, void (*fn)(void* arg), void* arg) {
+    if (!fn) return report_error(-EINVAL, "null callback");
+    if (photon_crc_device_count() <= 0) return -ENODEV;
+    hipError_t e = hipLaunchHostFunc(static_cast<hipStream_t>(stream), fn, arg);
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipLaunchHostFunc");
+}
+
+int photon_crc_device_alloc(void** ptr, uint64_t nbytes) {
+    if (!ptr || !nbytes) return report_error(-EINVAL, "null pointer or zero size");
+    if (photon_crc_device_count() <= 0) return -ENODEV;
+    hipError_t e = hipMalloc(ptr, nbytes);
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipMalloc");
+}
+
+int photon_crc_device_free(void* ptr) {
+    if (!ptr) return 0;
+    hipError_t e = hipFree(ptr);
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipFree");
+}
+
+int photon_crc_memcpy_async(void* dst, const void* src, uint64_t nbytes, void* stream) {
+    if (!nbytes) return 0;
+    if (!dst || !src) return report_error(-EINVAL, "null pointer");
+    if (photon_crc_device_count() <= 0) return -ENODEV;
+    hipError_t e = hipMemcpyAsync(dst, src, nbytes, hipMemcpyDefault, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : report_hip_error(e, "hipMemcpyAsync");
+}
 
 int photon_crc_host_register(void* ptr, uint64_t len) {
     if (!ptr || !len) return report_error(-EINVAL, "null or empty range");

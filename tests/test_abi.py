@@ -80,6 +80,11 @@ def test_device_calls_fail_loudly_without_gpu():
         ck.file_strided(0, 0, 4096, 4096, 1)
     with pytest.raises(ck.CrcError):
         ck.host_batch_strided_multi(0x1000, 4096, 4096, 1, 0x2000)
+    import ctypes
+    from photonlibos_amd._native import lib
+    p = ctypes.c_void_p()
+    assert lib().photon_crc_device_alloc(ctypes.byref(p), 4096) < 0
+    assert lib().photon_crc_stream_create(ctypes.byref(p)) < 0
     with pytest.raises(ck.CrcError):
         ck.batch_strided_shards([dict(device=0, d_base=0x1000, stride=4096, nbytes=4096, count=1, d_out=0x2000)])
 
