@@ -54,7 +54,7 @@ CONFIGS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=25,
                     help="untimed steps; the first ~10 back-to-back launches run slower while clocks settle")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))

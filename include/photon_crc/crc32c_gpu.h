@@ -201,6 +201,9 @@ int photon_crc64ecma_host_batch_strided(const void* h_base, uint64_t stride, uin
                                         uint64_t seed0, const uint64_t* h_seeds, uint64_t* h_out);
 int photon_crc64ecma_combine_batch(const uint64_t* d_crc1, const uint64_t* d_crc2, const uint32_t* d_len2,
                                    uint64_t count, uint64_t* d_out, void* stream);
+/* photon_crc32c_batch_msg_n for CRC-64/ECMA: d_out[m] = crc64ecma_extend
+ * chained over message m's segments from seed_m. d_seg_out (per-segment CRCs
+ * from seed 0) is optional. */
 int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
                                  uint64_t nseg, uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_seg_out,
                                  uint64_t* d_out, void* stream);

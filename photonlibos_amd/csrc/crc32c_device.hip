@@ -934,19 +934,32 @@ int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* 
                                  uint64_t nseg, uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_seg_out,
                                  uint64_t* d_out, void* stream) {
     if (!nmsg) return 0;
-    if (!d_iov || !d_msg_start || !d_seg_out || !d_out) return fail(-EINVAL, "null argument");
+    if (!d_iov || !d_msg_start || !d_out) return fail(-EINVAL, "null argument");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    // d_seg_out is optional: without it the segment CRCs live in stream-ordered scratch.
+    void* scratch = nullptr;
+    if (!d_seg_out) {
+        hipError_t e = hipMallocAsync(&scratch, (nseg ? nseg : 1) * sizeof(uint64_t), st);
+        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+        d_seg_out = static_cast<uint64_t*>(scratch);
+    }
     Batch64Args a{};
     a.iov = d_iov;
     a.count = nseg;
     a.out = d_seg_out;
     a.seed0 = 0;
     int rc = launch_batch64(a, 8192, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(crc64_msg_fold_kernel, dim3((nmsg + 255) / 256), dim3(256), 0, st, d_iov, d_msg_start, nmsg,
-                       d_seg_out, seed0, d_seeds, d_out, pow_table64());
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : hip_fail(e, "crc64_msg_fold_kernel launch");
+    if (!rc) {
+        hipLaunchKernelGGL(crc64_msg_fold_kernel, dim3((nmsg + 255) / 256), dim3(256), 0, st, d_iov, d_msg_start,
+                           nmsg, d_seg_out, seed0, d_seeds, d_out, pow_table64());
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "crc64_msg_fold_kernel launch");
+    }
+    if (scratch) {
+        hipError_t e = hipFreeAsync(scratch, st);
+        if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    }
+    return rc;
 }
 
 int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,

@@ -1,6 +1,7 @@
 """Randomised parity: many random shapes through every CRC32C / CRC-64 device
 entry point and engine variant, checked bit-exactly against the pinned
 oracle (tests/_oracle.py). Seeds are fixed, so a failure reproduces."""
+import os
 import random
 
 import numpy as np
@@ -12,6 +13,8 @@ from photonlibos_amd import datagen
 pytestmark = pytest.mark.gpu
 
 POOL = 4 << 20
+# PHOTON_FUZZ_ROUNDS=k multiplies the rounds (longer soak runs, new seeds).
+SOAK = max(1, int(os.environ.get("PHOTON_FUZZ_ROUNDS", "1")))
 
 
 @pytest.fixture(scope="module")
@@ -29,6 +32,9 @@ def _reset():
     ck.set_generic_rows(4)
     ck.set_stream_config(0, 0, 0)
     ck.set_msg_mode(0)
+    ck.set_stream64_run_blocks(1)
+    ck.set_stream64_interleave(1)
+    ck.set_stream64_config(4, 3)
 
 
 ENGINES = [  # (lanes, generic rows, streaming shape)
@@ -47,7 +53,7 @@ def _lengths(rnd, k):
     return out
 
 
-@pytest.mark.parametrize("round_", range(4))
+@pytest.mark.parametrize("round_", range(4 * SOAK))
 def test_fuzz_iov_batches(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(1000 + round_)
@@ -71,7 +77,7 @@ def test_fuzz_iov_batches(dev_pool, oracle, round_):
             assert got[k] == oracle.crc32c(host[o:o + n], s), (lanes, rows, stream, o, n, s)
 
 
-@pytest.mark.parametrize("round_", range(3))
+@pytest.mark.parametrize("round_", range(3 * SOAK))
 def test_fuzz_strided_batches(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(2000 + round_)
@@ -94,7 +100,7 @@ def test_fuzz_strided_batches(dev_pool, oracle, round_):
             assert got[i] == oracle.crc32c(host[o:o + nbytes], seed0), (lanes, rows, stream, nbytes, stride, i)
 
 
-@pytest.mark.parametrize("round_", range(3))
+@pytest.mark.parametrize("round_", range(3 * SOAK))
 def test_fuzz_messages(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(3000 + round_)
@@ -126,7 +132,7 @@ def test_fuzz_messages(dev_pool, oracle, round_):
                 assert got[m] == oracle.extend_chain(parts, seeds[m]), (mode, lanes, m)
 
 
-@pytest.mark.parametrize("round_", range(2))
+@pytest.mark.parametrize("round_", range(2 * SOAK))
 def test_fuzz_crc64(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(4000 + round_)
@@ -146,3 +152,91 @@ def test_fuzz_crc64(dev_pool, oracle, round_):
         got = out.cpu().numpy().view(np.uint64)
         for k, (o, n, s) in enumerate(zip(offs, lens, seeds)):
             assert int(got[k]) == oracle.crc64ecma(host[o:o + n], s), (lanes, o, n)
+
+
+SHAPES64 = [  # (lanes, run blocks, interleave, (U, D)); (0, 0) = streaming kernel off
+    (0, 1, 1, (4, 3)), (8, 1, 1, (4, 1)), (16, 2, 1, (4, 3)), (32, 2, 1, (2, 2)), (32, 1, 2, (4, 3)),
+    (16, 1, 4, (4, 2)), (64, 1, 1, (8, 1)), (8, 1, 1, (0, 0)), (64, 1, 1, (0, 0)),
+]
+
+
+@pytest.mark.parametrize("round_", range(3 * SOAK))
+def test_fuzz_crc64_strided(dev_pool, oracle, round_):
+    torch, host, d = dev_pool
+    rnd = random.Random(5000 + round_)
+    for lanes, b, v, (u, dd) in SHAPES64:
+        ck.set_lanes_per_buffer(lanes)
+        ck.set_stream64_run_blocks(b)
+        ck.set_stream64_interleave(v)
+        ck.set_stream64_config(u, dd)
+        aligned = rnd.random() < 0.6
+        nbytes = rnd.choice([4096, 8192, 65536, 16 * 64 * 8]) if aligned else rnd.randrange(1, 70000)
+        stride = nbytes if aligned else nbytes + rnd.randrange(0, 64)
+        count = max(1, min(rnd.randrange(1, 300), (POOL - 64) // stride))
+        base = 0 if aligned else rnd.randrange(0, 16)
+        seed0 = rnd.getrandbits(64)
+        seeds = [rnd.getrandbits(64) for _ in range(count)] if rnd.random() < 0.4 else None
+        d_seeds = torch.from_numpy(np.asarray(seeds, np.uint64).view(np.int64)).cuda() if seeds else None
+        out = torch.zeros(count, dtype=torch.int64, device="cuda")
+        ck.batch64_strided(d.data_ptr() + base, stride, nbytes, count, out, seed=seed0, seeds=d_seeds)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64)
+        for i in range(count):
+            o = base + i * stride
+            want = oracle.crc64ecma(host[o:o + nbytes], seeds[i] if seeds else seed0)
+            assert int(got[i]) == want, (lanes, b, v, u, dd, nbytes, stride, i)
+
+
+def _chain64(oracle, parts, seed):
+    c = seed
+    for p in parts:
+        c = oracle.crc64ecma(p, c)
+    return c
+
+
+@pytest.mark.parametrize("round_", range(3 * SOAK))
+def test_fuzz_crc64_messages(dev_pool, oracle, round_):
+    torch, host, d = dev_pool
+    rnd = random.Random(6000 + round_)
+    for lanes in (0, 8, 64):
+        ck.set_lanes_per_buffer(lanes)
+        nmsg = rnd.randrange(1, 300)
+        iov, start, msgs = [], [0], []
+        for _ in range(nmsg):
+            parts = []
+            for n in _lengths(rnd, rnd.choice([0, 1, 3, 8])):
+                n = min(n, 40000)
+                o = rnd.randrange(0, POOL - n)
+                iov.append((d.data_ptr() + o, n))
+                parts.append(host[o:o + n])
+            start.append(len(iov))
+            msgs.append(parts)
+        seeds = [rnd.getrandbits(64) for _ in range(nmsg)]
+        d_iov = torch.from_numpy(np.asarray(iov or [(0, 0)], np.uint64).view(np.int64)).cuda()
+        d_start = torch.from_numpy(np.asarray(start, np.uint64).view(np.int64)).cuda()
+        d_seeds = torch.from_numpy(np.asarray(seeds, np.uint64).view(np.int64)).cuda()
+        out = torch.zeros(nmsg, dtype=torch.int64, device="cuda")
+        seg = torch.zeros(max(len(iov), 1), dtype=torch.int64, device="cuda") if rnd.random() < 0.5 else None
+        ck.batch64_msg_n(d_iov, d_start, nmsg, len(iov), seg, out, seeds=d_seeds)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64)
+        for m, parts in enumerate(msgs):
+            assert int(got[m]) == _chain64(oracle, parts, seeds[m]), (lanes, m)
+
+
+@pytest.mark.parametrize("round_", range(2 * SOAK))
+def test_fuzz_extend_device(dev_pool, oracle, round_):
+    # One long buffer (the one-buffer fold path) at random offsets / lengths.
+    torch, host, d = dev_pool
+    rnd = random.Random(7000 + round_)
+    out32 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out64 = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(6):
+        n = rnd.choice([rnd.randrange(0, 5000), rnd.randrange(5000, 1 << 20), rnd.randrange(1 << 20, POOL - 64)])
+        o = rnd.randrange(0, POOL - n)
+        s32, s64 = rnd.getrandbits(32), rnd.getrandbits(64)
+        ck.extend_device(d.data_ptr() + o, n, s32, out32)
+        ck.extend64_device(d.data_ptr() + o, n, out64, seed=s64)
+        torch.cuda.synchronize()
+        assert int(out32.cpu().numpy().view(np.uint32)[0]) == oracle.crc32c(host[o:o + n], s32), (o, n)
+        assert int(out64.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(host[o:o + n], s64), (o, n)
