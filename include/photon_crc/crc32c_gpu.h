@@ -230,9 +230,9 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
  * step with the row shifts folded into the tables). */
 int photon_crc_set_generic_rows(int rows_per_step);
 
-/* The CRC-64 streaming kernel's shape: rows per step U and steps in flight D,
- * one of (4,3) (default), (4,2), (8,1), (2,4); U = 0 turns it off (generic
- * kernel for every CRC-64 batch). */
+/* The CRC-64 streaming kernel (uniform batches; off by default, the generic
+ * kernel is faster): a shape turns it on -- rows per step U and steps in
+ * flight D, one of (4,1..3), (2,2..4), (8,1); U = 0 turns it off again. */
 int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
 
 /* Interleaved row partials per lane in the CRC-64 streaming kernel (testing /

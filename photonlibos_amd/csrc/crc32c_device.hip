@@ -70,7 +70,7 @@ int g_stream_b = 1, g_stream_u = 4, g_stream_d = 3;  // streaming kernel: run bl
 // tables the generic kernel measures faster on every config
 // (profiles/tune_r01_generic_rows.jsonl), so it is off by default.
 bool g_stream_enabled = false;
-bool g_stream64_enabled = true;
+bool g_stream64_enabled = false;  // the generic kernel is faster with lagged blocks
 
 int fail(int code, const std::string& what) {
     g_err = what;

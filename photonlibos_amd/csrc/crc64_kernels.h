@@ -124,9 +124,13 @@ __device__ __forceinline__ uint2 sstep64(const uint32_t* lds, uint2 p, const Lan
     return step64<1>(lds, p, a, e);
 }
 
-// CRC register (init 0) after a 16-byte block.
-__device__ __forceinline__ uint2 crc16_64(const uint32_t* lds, uint4 w, const LaneAddr64& a) {
-    return dstep64(lds, dstep64(lds, make_uint2(w.x, w.y), a, make_uint2(w.z, w.w)), a);
+// Lagged block CRC: the CRC register (init 0) after a 16-byte block is
+// crc16(w) = (lo * x^64 ^ hi) * x^64 = v * x^64 with v = D(lo) ^ hi. The
+// column recurrence P <- P * X ^ crc16(w) (X = x^(128G)) is run on
+// Q = P * x^-64 instead: Q <- Q * X ^ v, so each block costs one D step (8
+// lookups) + one S step (8) instead of 24 lookups; P = D(Q) once per buffer.
+__device__ __forceinline__ uint2 lag16_64(const uint32_t* lds, uint4 w, const LaneAddr64& a) {
+    return dstep64(lds, make_uint2(w.x, w.y), a, make_uint2(w.z, w.w));
 }
 
 __device__ __forceinline__ uint64_t u64of(uint2 v) { return ((uint64_t)v.y << 32) | v.x; }
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                     const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
                     w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
                 }
-                pc = crc16_64(lds, w, la);
+                pc = lag16_64(lds, w, la);
             }
             uint64_t row = 1;
             if (row + U <= full) {
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                     for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
                     uint2 c[U];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, cur[u], la);
+                    for (int u = 0; u < U; ++u) c[u] = lag16_64(lds, cur[u], la);
 #pragma unroll
                     for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
 #pragma unroll
@@ -295,14 +299,15 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                 }
                 uint2 c[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) c[u] = crc16_64(lds, cur[u], la);
+                for (int u = 0; u < U; ++u) c[u] = lag16_64(lds, cur[u], la);
 #pragma unroll
                 for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
                 row += U;
             }
-            for (; row < full; ++row) pc = sstep64(lds, pc, la, crc16_64(lds, load16(lp + row * (16 * G)), la));
+            for (; row < full; ++row) pc = sstep64(lds, pc, la, lag16_64(lds, load16(lp + row * (16 * G)), la));
             if (full >= 1 && full < rows && full * G + gl < nb)
-                pc = sstep64(lds, pc, la, crc16_64(lds, load16(lp + full * (16 * G)), la));
+                pc = sstep64(lds, pc, la, lag16_64(lds, load16(lp + full * (16 * G)), la));
+            pc = dstep64(lds, pc, la);  // Q -> P
             reg = group_reduce64<G>(u64of(pc), (rlast + G - 1 - gl) & (G - 1), lds);
             if (gl == 0)
                 for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
@@ -319,25 +324,26 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
 // lane l plays virtual lane j*G + l of a V*G-lane geometry (row shift
 // x^(8*16*G*V), the kc passed is lane_consts64(G*V)); V independent S chains
 // of U/V steps instead of one of U steps.
-// CRC register (init 0) after a run of B consecutive 16-byte blocks.
+// Lagged CRC (x^-64 times the CRC register, init 0) after a run of B
+// consecutive 16-byte blocks (lag16_64 for B = 1).
 template <int B>
-__device__ __forceinline__ uint2 crc_run64(const uint32_t* lds, const uint4 (&w)[B], const LaneAddr64& a) {
+__device__ __forceinline__ uint2 lag_run64(const uint32_t* lds, const uint4 (&w)[B], const LaneAddr64& a) {
     uint2 c = dstep64(lds, make_uint2(w[0].x, w[0].y), a, make_uint2(w[0].z, w[0].w));
 #pragma unroll
     for (int b = 1; b < B; ++b) {
         c = dstep64(lds, c, a, make_uint2(w[b].x, w[b].y));
         c = dstep64(lds, c, a, make_uint2(w[b].z, w[b].w));
     }
-    return dstep64(lds, c, a);
+    return c;
 }
 
 // B = 2: each lane reads a RUN of two consecutive blocks per row (two
-// dwordx4 loads, lane stride 32 B) so the row shift (8 S lookups) is paid
-// once per 32 bytes: 40 instead of 48 lookups per 32 B. The lane then plays
-// the 2G-lane geometry's blocks 2l, 2l+1 (kc = lane_consts64(2G)).
+// dwordx4 loads, lane stride 32 B) and pays the row shift once per 32 bytes
+// (3 D + 1 S steps = 32 lookups per 32 B, as two lagged single blocks). The
+// lane then plays the 2G-lane geometry's blocks 2l, 2l+1 (kc = lane_consts64(2G)).
 // ABL != 0 only in bench-only ablation builds (probes.hip); results are then
-// NOT CRCs: 1 = no S (row-shift) lookups, 2 = one D step per block instead of
-// two, 4 = no table lookups at all.
+// NOT CRCs: 1 = no S (row-shift) lookups, 2 = one D step on lo ^ hi per
+// block (no data chain), 4 = no table lookups at all.
 template <int G, int U, int D, int V = 1, int B = 1, int ABL = 0>
 __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
@@ -414,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args arg
                     c[u] = dstep64(lds, make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w),
                                    la);
                 } else {
-                    c[u] = crc_run64<B>(lds, ring[d][u], la);
+                    c[u] = lag_run64<B>(lds, ring[d][u], la);
                 }
             }
 #pragma unroll
@@ -426,8 +432,9 @@ __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args arg
             if (++step == spb) {
                 uint64_t acc = 0;
 #pragma unroll
-                for (int j = 0; j < V; ++j)
-                    acc ^= shift64<LOG2VG>(u64of(pc[j]), (uint32_t)((G * V - 1 - (j * G + gl)) * B), lds);
+                for (int j = 0; j < V; ++j)  // Q -> P (dstep), then the lane shift
+                    acc ^= shift64<LOG2VG>(u64of(ABL ? pc[j] : dstep64(lds, pc[j], la)),
+                                           (uint32_t)((G * V - 1 - (j * G + gl)) * B), lds);
 #pragma unroll
                 for (int o = G / 2; o > 0; o >>= 1) {
                     const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);

@@ -96,7 +96,7 @@ for r in range(args.rounds):
                 refs[key] = o
             assert np.array_equal(o, refs[key]), f"variant {v}/G{l} disagrees"
 ck.set_stream_config(0, 0, 0)
-ck.set_stream64_config(4, 3)
+ck.set_stream64_config(0, 0)
 ck.set_stream64_interleave(1)
 ck.set_stream64_run_blocks(1)
 ck.set_generic_rows(4)

@@ -34,7 +34,7 @@ def _reset():
     ck.set_msg_mode(0)
     ck.set_stream64_run_blocks(1)
     ck.set_stream64_interleave(1)
-    ck.set_stream64_config(4, 3)
+    ck.set_stream64_config(0, 0)
 
 
 ENGINES = [  # (lanes, generic rows, streaming shape)
