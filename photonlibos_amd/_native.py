@@ -4,7 +4,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libphoton_checksum.so")
+# PHOTON_CRC_LIB: load another build of the library (A/B of two builds on one box).
+LIB_PATH = os.environ.get("PHOTON_CRC_LIB") or os.path.join(_HERE, "lib", "libphoton_checksum.so")
 
 _lib = None
 
