@@ -227,14 +227,19 @@ def cpu_reference_c1(seconds):
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
     if not os.path.exists(harness):
         return {}
+    # beside it, this library's drop-in host engine (same header, same buffers)
+    dropin = os.path.join(REPO, "tests", "cpp", "bin", "host_bench")
     out = {}
     for threads in (1, max(1, min(16, os.cpu_count() or 1))):
-        r = subprocess.run([harness, "bench", "1024", "4096", str(threads), str(seconds)],
-                           capture_output=True, text=True, timeout=seconds * 4 + 60)
-        if r.returncode == 0:
-            out[f"threads_{threads}"] = round(json.loads(r.stdout.strip().splitlines()[-1])["gib_per_s"], 3)
-    return {"unit": "GiB/s", "workload": "C1: 1024 x 4 KiB random buffers (cache-resident), Photon crc32c()",
-            **out} if out else {}
+        for key, cmd in ((f"threads_{threads}", [harness, "bench"]), (f"dropin_threads_{threads}", [dropin])):
+            if not os.path.exists(cmd[0]):
+                continue
+            r = subprocess.run(cmd + ["1024", "4096", str(threads), str(seconds)],
+                               capture_output=True, text=True, timeout=seconds * 4 + 60)
+            if r.returncode == 0:
+                out[key] = round(json.loads(r.stdout.strip().splitlines()[-1])["gib_per_s"], 3)
+    return {"unit": "GiB/s", "workload": "C1: 1024 x 4 KiB random buffers (cache-resident), Photon crc32c(); "
+            "dropin_*: this library's crc32c() drop-in on the same buffers", **out} if out else {}
 
 
 def load_traffic(path, config):
