@@ -61,7 +61,125 @@ __global__ __launch_bounds__(1024) void rows_kernel(const uint8_t* base, uint64_
     sink[blockIdx.x * 1024ull + threadIdx.x] = acc;
 }
 
+// The generic strided CRC32C kernel (crc32c_batch_kernel's non-message path,
+// same buffer_crc) with per-wave timestamps and a choice of task hand-out:
+//   MODE 0: static (wave w takes wave tasks w, w + nwaves, ... as the product);
+//   MODE 1: every task from one device-scope ticket counter (next ticket
+//           fetched before the current task runs);
+//   MODE 2: static for the first `static_rounds` rounds, tickets for the rest;
+//   MODE 3: as 2 with 8 per-XCC ticket regions and stealing across them;
+//   MODE 4: static with the chunk of workgroup b rotated by the round.
+// t[4*gw..4*gw+3] = s_memrealtime (100 MHz) at the wave start / end, HW_ID, XCC_ID.
+template <int G, int MODE>
+__global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::BatchArgs args, pcrc::LaneConsts kc,
+                                                                     uint64_t* t, uint32_t* ticket,
+                                                                     uint32_t static_rounds) {
+    using namespace pcrc;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    build_tables(lds, kc);
+    constexpr int GPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = wave_id();
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const LaneAddr la = lane_addr(lane);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    const uint64_t ntask = (args.count + GPW - 1) / GPW;
+    const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave;
+    const uint64_t nstatic = (MODE == 0 || MODE == 4) ? ntask : MODE == 1 ? 0 : std::min<uint64_t>(ntask, static_rounds * nwaves);
+    // The ticket's atomic is issued one task ahead and read (readfirstlane)
+    // only after that task: its return latency hides behind the task's loads.
+    auto take = [&]() -> uint32_t { return lane == 0 ? atomicAdd(ticket, 1u) : 0u; };
+    auto take_at = [&](uint32_t* c) -> uint32_t { return lane == 0 ? atomicAdd(c, 1u) : 0u; };
+    auto value = [&](uint32_t v) -> uint64_t { return nstatic + (uint64_t)__builtin_amdgcn_readfirstlane(v); };
+    auto run = [&](uint64_t wv) {
+        const uint64_t bi = wv * GPW + grp;
+        const bool active = bi < args.count;
+        const uint8_t* p = active ? args.base + bi * args.stride : nullptr;
+        const uint64_t n = active ? args.nbytes : 0;
+        const uint32_t crc = buffer_crc<G, 4>(lds, p, n, args.seed0, gl, la);
+        if (active && gl == 0) args.out[bi] = crc;
+    };
+    if (MODE == 4) {
+        // Static, but workgroup b takes chunk (b + k) % grid in round k, so
+        // every XCC (b % 8 under round-robin placement) cycles through every
+        // chunk offset instead of always the same ones.
+        for (uint64_t k = 0; k * nwaves < ntask; ++k) {
+            const uint64_t wv = k * nwaves + ((blockIdx.x + k) % gridDim.x) * kWaves + wave;
+            if (wv < ntask) run(wv);
+        }
+    } else {
+        for (uint64_t wv = gw; wv < nstatic; wv += nwaves) run(wv);
+    }
+    if (MODE == 3) {
+        // Tail tasks j = nstatic + x + 8*i in 8 regions x, one ticket counter
+        // each (128 B apart); a wave drains its own XCC's region, then the
+        // others in order. A relaxed load skips exhausted regions without an
+        // atomic; the next ticket is taken one task ahead.
+        const uint64_t tail = ntask - nstatic;
+        const uint32_t home = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7u;
+        for (uint32_t r = 0; r < 8; ++r) {
+            const uint32_t x = (home + r) & 7u;
+            const uint64_t cnt = tail > x ? (tail - x + 7) / 8 : 0;
+            uint32_t* ctr = ticket + 32 * x;
+            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cnt) continue;
+            uint64_t c = __builtin_amdgcn_readfirstlane(take_at(ctr));
+            while (c < cnt) {
+                const uint32_t nx = take_at(ctr);
+                run(nstatic + x + 8 * c);
+                c = __builtin_amdgcn_readfirstlane(nx);
+            }
+        }
+    } else if (MODE == 1 || MODE == 2) {
+        uint64_t wv = value(take());
+        while (wv < ntask) {
+            const uint32_t nx = take();
+            run(wv);
+            wv = value(nx);
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+        t[4 * gw] = t0;
+        t[4 * gw + 1] = t1;
+        t[4 * gw + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID: wave, simd, cu, se
+        t[4 * gw + 3] = __builtin_amdgcn_s_getreg(20 | (3 << 11));   // XCC_ID
+    }
+}
+
 extern "C" {
+
+// crc_wave_times_kernel over a strided batch; `t` holds 4 * grid * 16 words,
+// `ticket` 256 words (zeroed here on the stream before the launch).
+int probe_crc_wave_times(const void* base, uint64_t nbytes, uint64_t count, uint32_t* out, uint64_t* t,
+                         uint32_t* ticket, int g, int mode, int static_rounds, int cus, void* stream) {
+    using namespace pcrc;
+    LaneConsts kc;
+    kc.kshift = xpow(8ull * 16ull * (uint64_t)g);
+    for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), kc.basis[k]);
+    BatchArgs a{};
+    a.base = static_cast<const uint8_t*>(base);
+    a.stride = nbytes;
+    a.nbytes = nbytes;
+    a.count = count;
+    a.out = out;
+    const uint64_t waves = (count + 64 / g - 1) / (64 / g);
+    uint64_t grid = (waves + kWaves - 1) / kWaves;
+    if (grid > (uint64_t)cus) grid = cus;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (hipMemsetAsync(ticket, 0, 1024, s) != hipSuccess) return -5;
+    const uint32_t sr = (uint32_t)static_rounds;
+#define WT(GG, M) \
+    hipLaunchKernelGGL((crc_wave_times_kernel<GG, M>), dim3(grid), dim3(kBlock), 0, s, a, kc, t, ticket, sr)
+    if (g == 8) {
+        if (mode == 1) WT(8, 1); else if (mode == 2) WT(8, 2); else if (mode == 3) WT(8, 3); else if (mode == 4) WT(8, 4); else WT(8, 0);
+    } else {
+        if (mode == 1) WT(32, 1); else if (mode == 2) WT(32, 2); else if (mode == 3) WT(32, 3); else if (mode == 4) WT(32, 4); else WT(32, 0);
+    }
+#undef WT
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 int probe_read_gridstride(const void* p, uint64_t nbytes, uint32_t* sink, int blocks, int unroll, int nt,
                           void* stream) {
