@@ -2,24 +2,40 @@
 """Benchmark of the north-star path: CRC32C over device-resident buffers on
 MI355X through the C-ABI engine (libphoton_checksum.so).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5] [--h2d]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|...]
 
 One "step" = one pass of the hot path over one batch (BASELINE.json configs):
-  c2 (default, configs[1]): 65,536 x 64 KiB random buffers, device-resident
-  c3: 1,048,576 x 4 KiB        c4: 32,768 x 1 MiB per GPU (the 8-GPU config's shard)
-  c5: 65,536 messages x 8 non-contiguous 8 KiB segments, per-message CRC (chained extend)
-  c5_seg: the same with every segment's own CRC written too
-  --h2d: the c2 batch starting and ending in pinned host memory (chunked
-         H2D + kernel + D2H); reported in DESIGN.md, never as `value`.
-Multi-GPU: one process per GPU (torchrun); every rank checksums its own
-independent batch (weak scaling, no data-path collective; gloo carries only
-the timing barrier and the max-over-ranks). Rank 0 prints one JSON line.
+  c2 (default at N=1, configs[1]): 65,536 x 64 KiB random buffers, device-resident
+  c4 (default at N>1, configs[3]): 32,768 x 1 MiB per GPU = the 256 Ki x 1 MiB
+      batch sharded over 8 GPUs (weak scaling: the per-GPU shard is fixed)
+  c3: 1,048,576 x 4 KiB        c5: 65,536 messages x 8 non-contiguous 8 KiB
+      segments, per-segment CRC + crc32c_combine fold (BASELINE.json configs[4])
+  c5_chain: the C5 shape, one CRC per message chained through the seed
+      (Crc32Hasher::extend_hash, rpc/serialize.h:244-251), no segment CRCs
+  c2_crc64: the C2 shape with CRC-64/ECMA (next row f2)
+  --h2d / --rpc-batch / --rpc-latency / --file-records: host-memory rates
+      for DESIGN.md, never `value`.
+
+Multi-GPU: one process per GPU. The driver launches
+`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`;
+a plain `python bench.py --gpus N` (no WORLD_SIZE in the environment) starts
+that launcher itself as a child process, before anything touches the GPU,
+and exits with its status. Every rank checksums its own independent shard
+(no data-path collective; gloo carries only the timing barrier, the
+max-over-ranks and the per-rank report). Rank 0 prints one JSON line.
+Fewer visible GPUs than --gpus is an error (exit 2) unless --share-gpus
+(a rehearsal: ranks share the visible GPUs round-robin, marked in the line).
+--cpu-rehearsal runs the same launcher / timed region / report with a host
+step (this library's crc32c() drop-in) for the CPU tests.
 """
 import argparse
 import json
 import os
+import shutil
+import socket
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -28,7 +44,7 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from photonlibos_amd import checksum as ck  # noqa: E402
+ck = None  # photonlibos_amd.checksum, imported once this process is a rank (after the launcher decision)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md "Chip-level parameters"
 GIB = float(1 << 30)
@@ -40,12 +56,13 @@ CONFIGS = {
     "c3": dict(kind="strided", nbytes=4096, count=1 << 20,
                workload="C3: 1048576 x 4 KiB RPC-payload buffers, device-resident, per GPU"),
     "c4": dict(kind="strided", nbytes=1 << 20, count=32768,
-               workload="C4 shard: 32768 x 1 MiB buffers per GPU (256K x 1 MiB over 8 GPUs)"),
-    "c5": dict(kind="msg", nbytes=8192, count=65536, nseg=8, seg_out=False,
-               workload="C5: 65536 messages x 8 non-contiguous 8 KiB segments, per-message CRC "
-                        "(Crc32Hasher: crc32c_extend chained over the segments = per-segment CRC + combine)"),
-    "c5_seg": dict(kind="msg", nbytes=8192, count=65536, nseg=8, seg_out=True,
-                   workload="C5 shape, per-segment CRCs also written (segment kernel + fold kernel)"),
+               workload="C4 shard: 32768 x 1 MiB buffers per GPU (256K x 1 MiB over 8 GPUs, no collective)"),
+    "c5": dict(kind="msg", nbytes=8192, count=65536, nseg=8, seg_out=True,
+               workload="C5: 65536 messages x 8 non-contiguous 8 KiB segments, per-segment CRC + "
+                        "crc32c_combine fold per message (every segment's CRC and every message's CRC written)"),
+    "c5_chain": dict(kind="msg", nbytes=8192, count=65536, nseg=8, seg_out=False,
+                     workload="C5 shape, per-message CRC only (Crc32Hasher: crc32c_extend chained over the "
+                              "segments through the seed)"),
     "c2_crc64": dict(kind="strided64", nbytes=65536, count=65536,
                      workload="C2 shape, CRC-64/ECMA (next row): 65536 x 64 KiB, device-resident, per GPU"),
 }
@@ -55,9 +72,13 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=25,
-                    help="untimed steps; the first ~10 back-to-back launches run slower while clocks settle")
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--warmup", type=int, default=25)
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c2 at --gpus 1, c4 (the 8-GPU config's shard) at --gpus > 1")
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="rehearsal: allow more ranks than visible GPUs (round-robin); marked in the output")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="no GPU: the same launcher and report with a host crc32c() step (CPU tests)")
     ap.add_argument("--h2d", action="store_true", help="host-memory end-to-end rate (for DESIGN.md)")
     ap.add_argument("--h2d-devices", type=int, default=1,
                     help="with --h2d: shard the host batch over this many devices of ONE process (0 = all)")
@@ -66,11 +87,52 @@ def parse(argv=None):
     ap.add_argument("--rpc-latency", action="store_true", help="submit+wait latency of small CheckedMessage batches")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="do not run the rocprofv3 FETCH_SIZE child pass; read profiles/pmc_<config>.json instead")
+    ap.add_argument("--no-shape64", action="store_true", help="skip the one-wavefront-per-buffer (G=64) side line")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (profiles/*.json) giving HBM bytes per launch")
-    return ap.parse_args(argv)
+                    help="PMC summary (profiles/*.json) giving HBM bytes per launch (fallback when no live pass)")
+    args = ap.parse_args(argv)
+    if args.config is None:
+        args.config = "c4" if args.gpus > 1 else "c2"
+    return args
 
+
+# ------------------------------------------------------------------ launcher
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(args, argv, port):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """Start one rank process per GPU (torch.distributed.run as a CHILD; this
+    process never touches the GPU: torch.cuda.device_count() does not
+    initialise it on this image) and return the launcher's exit status."""
+    if not args.cpu_rehearsal:
+        visible = torch.cuda.device_count()
+        if visible < args.gpus and not args.share_gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) visible "
+                  "(--share-gpus runs a rehearsal with ranks sharing them)", file=sys.stderr)
+            return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(launcher_cmd(args, argv, free_port()), env=env)
+
+
+# -------------------------------------------------------------- timed region
 
 def shard_seed_base(rank, count):
     """Rank r checksums buffers with global ids [r*count, (r+1)*count):
@@ -80,8 +142,9 @@ def shard_seed_base(rank, count):
 
 def timed_region(step, steps, warmup, sync, dist=None, on_step=None):
     """Run `warmup` untimed steps, then exactly `steps` steps bracketed by a
-    barrier + device sync on both sides. Returns the max over ranks of the
-    wall time and of the mean per-step time reported by `on_step` (ms)."""
+    barrier + device sync on both sides. Returns (max over ranks of the wall
+    time, max over ranks of the mean per-launch ms from `on_step`, this rank's
+    wall time, this rank's per-launch ms list)."""
     for _ in range(warmup):
         step()
     sync()
@@ -99,18 +162,37 @@ def timed_region(step, steps, warmup, sync, dist=None, on_step=None):
     elapsed = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
-    per_step_ms = float(np.mean([m() for m in marks])) if marks else elapsed / steps * 1e3
+    launch_ms = [m() for m in marks] if marks else [elapsed / steps * 1e3] * steps
+    per_step_ms = float(np.mean(launch_ms))
+    local = (elapsed, launch_ms)
     if dist is not None:
         t = torch.tensor([elapsed, per_step_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, per_step_ms = float(t[0]), float(t[1])
-    return elapsed, per_step_ms
+    return elapsed, per_step_ms, local[0], local[1]
+
+
+def gather_ranks(dist, rec):
+    """Every rank's small report dict, in rank order (gloo all_gather_object)."""
+    if dist is None:
+        return [rec]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, rec)
+    return out
 
 
 def aggregate_gibps(bytes_per_step_per_rank, steps, world, elapsed):
     """Whole-job throughput: every rank's bytes over the slowest rank's time."""
     return bytes_per_step_per_rank * steps * world / elapsed / GIB
 
+
+def launch_summary(ms):
+    a = np.asarray(ms, dtype=np.float64)
+    return {"first5": [round(float(x), 4) for x in a[:5]], "mean": round(float(a.mean()), 4),
+            "median": round(float(np.median(a)), 4), "min": round(float(a.min()), 4), "max": round(float(a.max()), 4)}
+
+
+# ------------------------------------------------------------------ workload
 
 class Workload:
     """Device-resident synthetic batch for one config on the current device."""
@@ -119,10 +201,7 @@ class Workload:
         self.cfg = cfg
         self.stream = stream
         n, cnt = cfg["nbytes"], cfg["count"]
-        if cfg["kind"] in ("strided", "strided64"):
-            slots = cnt
-        else:
-            slots = cnt * cfg["nseg"]
+        slots = cnt if cfg["kind"] in ("strided", "strided64") else cnt * cfg["nseg"]
         seed_base = shard_seed_base(rank, slots)
         self.payload = torch.empty(n * slots, dtype=torch.uint8, device="cuda")
         ck.fill_splitmix(self.payload, n, n, slots, seed_base, stream=stream)
@@ -143,7 +222,6 @@ class Workload:
             self.start = torch.from_numpy(np.arange(0, slots + 1, nseg, dtype=np.uint64).view(np.int64)).cuda()
             self.seg_out = torch.zeros(slots, dtype=torch.int32, device="cuda")
             self.out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
-        torch.cuda.synchronize()
 
     def step(self):
         c = self.cfg
@@ -156,8 +234,8 @@ class Workload:
                            self.seg_out if c.get("seg_out") else None, self.out, stream=self.stream)
 
     def self_check(self):
-        """Spot-check results against the product's own host engine (crc32c_hw
-        and crc32c_combine), not the oracle."""
+        """Spot-check the LAST timed step's results against the product's own
+        host engine (crc32c_hw / crc32c_extend / crc64ecma_sw), not the oracle."""
         c = self.cfg
         n = c["nbytes"]
         if c["kind"] == "strided64":
@@ -175,38 +253,84 @@ class Workload:
                     return False
             return True
         iov = self.iov.cpu().numpy().view(np.uint64)
+        seg = self.seg_out.cpu().numpy().view(np.uint32)
         base = self.payload.data_ptr()
         for m in (0, c["count"] - 1):
             acc = 0
             for j in range(c["nseg"]):
                 off = int(iov[m * c["nseg"] + j, 0]) - base
-                acc = ck.crc32c_extend(self.payload[off:off + n].cpu().numpy().tobytes(), acc)
+                data = self.payload[off:off + n].cpu().numpy().tobytes()
+                if c.get("seg_out") and ck.crc32c_hw(data) != seg[m * c["nseg"] + j]:
+                    return False
+                acc = ck.crc32c_extend(data, acc)
             if acc != out[m]:
                 return False
         return True
 
 
+# --------------------------------------------------------------- CPU baseline
+
+def usable_cores():
+    """Cores this process may run on: the affinity mask, capped by a cgroup CPU
+    quota when one is set (a GPU box grants each GPU's job a CPU share while
+    nproc / the affinity mask show the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                period = float(f.read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    used = aff if quota is None else max(1, min(aff, int(quota)))
+    return used, {"affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return [ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")][0]
+    except Exception:
+        return ""
+
+
+def _run_harness(cmd, nbuf, n, threads, seconds):
+    r = subprocess.run(cmd + [str(nbuf), str(n), str(threads), str(seconds)], capture_output=True, text=True,
+                       timeout=seconds * 4 + 120)
+    if r.returncode != 0:
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline(cfg, seconds):
-    """Photon's own CPU checksum (reference crc.cpp, oracle/_ref/ref_harness),
-    timed on this host; the oracle's C port as fallback."""
+    """Photon's own CPU checksum (reference crc.cpp compiled unmodified into
+    oracle/_ref/ref_harness) on this host, over a bounded 256 MiB sample of the
+    same workload, on 1 thread and on every usable core (persistent pinned
+    thread pool, tests/cpp/spin_pool.h); the oracle's C port as fallback."""
     n = cfg["nbytes"]
-    nbuf = max(1, (256 << 20) // n)  # bounded 256 MiB sample of the same workload
-    threads = max(1, min(16, os.cpu_count() or 1))
+    nbuf = max(1, (256 << 20) // n)
+    cores, cinfo = usable_cores()
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    sample = f"{nbuf} x {n} B random host buffers (256 MiB, stream 0x5EED0001+i), best pass over >= {seconds:.0f} s"
+    sample = f"{nbuf} x {n} B random host buffers (256 MiB, stream 0x5EED0001+i), best pass"
     if os.path.exists(harness):
-        out = subprocess.run([harness, "bench", str(nbuf), str(n), str(threads), str(seconds)],
-                             capture_output=True, text=True, timeout=seconds * 4 + 120)
-        if out.returncode == 0:
-            r = json.loads(out.stdout.strip().splitlines()[-1])
-            cpu = ""
-            try:
-                cpu = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
-            except Exception:
-                pass
-            return {"value": round(r["gib_per_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
-                    "sample": sample + f"; Photon crc32c() auto-dispatch (crc.cpp:339-358) on {threads} threads"
-                    + (f" of {cpu}" if cpu else "")}
+        allc = _run_harness([harness, "bench"], nbuf, n, cores, seconds)
+        one = _run_harness([harness, "bench"], nbuf, n, 1, seconds / 2)
+        if allc is not None:
+            model = cpu_model()
+            return {"value": round(allc["gib_per_s"], 3), "unit": "GiB/s", "cores": cores, "kind": "reference",
+                    "sample": sample + f"; Photon crc32c() auto-dispatch (crc.cpp:339-358) on {cores} pinned "
+                    "threads" + (f" of {model}" if model else ""),
+                    "median_pass_gib_per_s": round(allc["gib_per_s_median"], 3),
+                    "single_thread": round(one["gib_per_s"], 3) if one else None, **cinfo}
     # Fallback: the oracle's C restatement (slicing-by-8), one thread.
     from tests import _oracle
     from photonlibos_amd import datagen
@@ -221,26 +345,27 @@ def cpu_baseline(cfg, seconds):
 
 
 def cpu_reference_c1(seconds):
-    """config C1 (1024 x 4 KiB, the reference's CPU-runnable
-    case) with Photon's own crc32c() on 1 thread and on 16 threads, beside the
-    main baseline. Empty when the reference build is absent."""
+    """Config C1 (1024 x 4 KiB, the reference's CPU-runnable case, cache-
+    resident) with Photon's own crc32c() and this library's drop-in, on 1
+    thread and on every usable core. Empty when the reference build is absent."""
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
     if not os.path.exists(harness):
         return {}
-    # beside it, this library's drop-in host engine (same header, same buffers)
     dropin = os.path.join(REPO, "tests", "cpp", "bin", "host_bench")
+    cores, _ = usable_cores()
     out = {}
-    for threads in (1, max(1, min(16, os.cpu_count() or 1))):
+    for threads in sorted({1, cores}):
         for key, cmd in ((f"threads_{threads}", [harness, "bench"]), (f"dropin_threads_{threads}", [dropin])):
-            if not os.path.exists(cmd[0]):
-                continue
-            r = subprocess.run(cmd + ["1024", "4096", str(threads), str(seconds)],
-                               capture_output=True, text=True, timeout=seconds * 4 + 60)
-            if r.returncode == 0:
-                out[key] = round(json.loads(r.stdout.strip().splitlines()[-1])["gib_per_s"], 3)
+            if os.path.exists(cmd[0]):
+                r = _run_harness(cmd, 1024, 4096, threads, seconds)
+                if r is not None:
+                    out[key] = round(r["gib_per_s"], 3)
     return {"unit": "GiB/s", "workload": "C1: 1024 x 4 KiB random buffers (cache-resident), Photon crc32c(); "
-            "dropin_*: this library's crc32c() drop-in on the same buffers", **out} if out else {}
+            "dropin_*: this library's crc32c() drop-in on the same buffers; persistent pinned thread pool",
+            **out} if out else {}
 
+
+# ------------------------------------------------------------- HBM traffic
 
 def load_traffic(path, config):
     if path is None:
@@ -250,8 +375,43 @@ def load_traffic(path, config):
     with open(path) as f:
         d = json.load(f)
     v = d.get("hbm_bytes_per_launch")
-    return int(v) if v else None  # HBM bytes per launch (PMC, corrected), vs the algorithmic bytes
+    return int(v) if v else None
 
+
+def live_traffic(config, timeout=150):
+    """HBM read bytes per launch of the config's main kernel, measured now: a
+    child `rocprofv3 --pmc FETCH_SIZE` pass (counters only, no tracing) over
+    `bench.py --pmc-child` (3 launches of the same workload), FETCH_SIZE KiB
+    x 1024 x 2 (gfx950 counts half the bytes of wide coalesced reads,
+    MI355X_MICROARCH.md HBM section). None if rocprofv3 is unavailable."""
+    import csv
+    import glob
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        cmd = [prof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--config", config, "--steps", "3", "--warmup", "1",
+               "--pmc-child"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=d)
+        except subprocess.TimeoutExpired:
+            return None
+        if r.returncode != 0:
+            return None
+        per = {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Counter_Name") == "FETCH_SIZE":
+                        per.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
+    if not per:
+        return None
+    name = max(per, key=lambda k: float(np.mean(per[k])))
+    return {"bytes": int(round(float(np.mean(per[name])) * 1024 * 2)), "kernel": name, "launches": len(per[name])}
+
+
+# ------------------------------------------------------------- host-memory modes
 
 def run_h2d(args, stream):
     """Host-memory end-to-end rate for the c2 batch (pinned host -> CRCs on host)."""
@@ -271,7 +431,7 @@ def run_h2d(args, stream):
         step = lambda: ck.host_batch_strided_multi(host, n, n, cnt, out, ndev=ndev)  # noqa: E731
     used = torch.cuda.device_count() if ndev <= 0 else min(ndev, torch.cuda.device_count())
     steps = max(2, min(args.steps, 10))
-    elapsed, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
+    elapsed, _, _, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
     ok = ck.crc32c_hw(host[:n].numpy().tobytes()) == int(out[0].item()) & 0xFFFFFFFF
     print(json.dumps({"metric": "GiB/s CRC32C host-resident (pinned) end to end: H2D + kernel + D2H",
                       "value": round(n * cnt * steps / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": used,
@@ -318,7 +478,7 @@ def run_rpc_batch(args, stream):
         batch.wait()
 
     steps = max(2, min(args.steps, 10))
-    elapsed, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
+    elapsed, _, _, _ = timed_region(step, steps, 2, torch.cuda.synchronize)
     nbytes = n * slots
     print(json.dumps({"metric": "GiB/s CRC32C CheckedMessage batch validation, payload in pinned host memory "
                                 "(zero-copy: descriptors, payload and verdicts in pinned memory)",
@@ -362,10 +522,9 @@ def run_rpc_latency(args, stream):
         row = {"messages": k, "payload_bytes": k * nseg * n, "gpu_submit_wait_us": round(gpu_us, 1)}
         harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
         if os.path.exists(harness):  # Photon's crc32c() over the same byte count, one core
-            r = subprocess.run([harness, "bench", str(k * nseg), str(n), "1", "1"], capture_output=True, text=True,
-                               timeout=120)
-            if r.returncode == 0:
-                row["photon_cpu_1core_us"] = round(json.loads(r.stdout.strip().splitlines()[-1])["best_s"] * 1e6, 1)
+            r = _run_harness([harness, "bench"], k * nseg, n, 1, 1)
+            if r is not None:
+                row["photon_cpu_1core_us"] = round(r["best_s"] * 1e6, 1)
         rows.append(row)
         batch.close()
     for a in regions:
@@ -378,7 +537,6 @@ def run_file_records(args):
     """§8(f) row 4: CRC32C of the 4 KiB records of a 1 GiB file (page-cache
     hot, buffered pread into pinned chunks + GPU pipeline), end to end.
     Reported in DESIGN.md, never as `value`."""
-    import tempfile
     n, size = 4096, 1 << 30
     count = size // n
     with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp"), delete=True) as f:
@@ -395,49 +553,109 @@ def run_file_records(args):
                 out = ck.file_strided(fd, 0, n, n, count)
             el = time.perf_counter() - t0
             ok = out[7] == ck.crc32c_hw(os.pread(fd, n, 7 * n))
+            # two concurrent callers (per-call chunk buffers, shared reader pool)
+            import threading
+            outs = [None, None]
+
+            def one(k):
+                outs[k] = ck.file_strided(fd, 0, n, n, count)
+            t1 = time.perf_counter()
+            th = [threading.Thread(target=one, args=(k,)) for k in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            el2 = time.perf_counter() - t1
+            ok = ok and all(np.array_equal(o, out) for o in outs)
         finally:
             os.close(fd)
     print(json.dumps({"metric": "GiB/s CRC32C of 4 KiB file records (pread into pinned chunks + GPU pipeline), "
                                 "page-cache hot", "value": round(size * steps / el / GIB, 3), "unit": "GiB/s",
-                      "n_gpus": 1, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3), "self_check": ok,
+                      "n_gpus": 1, "steps": steps, "ms_per_step": round(el / steps * 1e3, 3),
+                      "two_concurrent_callers_ms": round(el2 * 1e3, 3), "self_check": ok,
                       "config": {"workload": "1 GiB file, 262144 x 4 KiB records"}}))
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------- CPU rehearsal
+
+def run_cpu_rehearsal(args, rank, world, dist):
+    """The N-rank launcher, timed region and report with no GPU: every rank
+    checksums its own shard of 64 x 64 KiB host buffers through this library's
+    crc32c() drop-in (the C-ABI library's host engine). For the CPU tests."""
+    from photonlibos_amd import datagen
+    n, cnt = 65536, 64
+    bufs = [datagen.stream_bytes(shard_seed_base(rank, cnt) + i, n).tobytes() for i in range(cnt)]
+    out = [0] * cnt
+
+    def step():
+        for i, b in enumerate(bufs):
+            out[i] = ck.crc32c(b)
+    def on_step(s, f):
+        t0 = time.perf_counter()
+        f()
+        dt = (time.perf_counter() - t0) * 1e3
+        return lambda: dt
+
+    elapsed, _, local_el, local_ms = timed_region(step, args.steps, args.warmup, lambda: None, dist, on_step)
+    ranks = gather_ranks(dist, {"rank": rank, "wall_s": round(local_el, 6), "first_crc": int(out[0]),
+                                "launch_ms": launch_summary(local_ms)})
+    if rank == 0:
+        print(json.dumps({"metric": "GiB/s CRC32C host rehearsal of the N-rank bench path (no GPU)",
+                          "value": round(aggregate_gibps(n * cnt, args.steps, world, elapsed), 3), "unit": "GiB/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "scaling": "weak",
+                          "rehearsal": "cpu", "per_rank": ranks,
+                          "config": {"workload": f"{cnt} x {n} B host buffers per rank, crc32c() drop-in",
+                                     "parallelism": f"shard-per-rank x{world}"}}), flush=True)
+
+
+# ----------------------------------------------------------------------- main
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (args.pmc_child or args.h2d or args.rpc_batch or args.rpc_latency
+                                   or args.file_records):
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    global ck
+    from photonlibos_amd import checksum as _ck
+    ck = _ck
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    # one process per GPU; ranks beyond the visible devices (a rehearsal on a
-    # smaller box) share them round-robin
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    if args.cpu_rehearsal:
+        run_cpu_rehearsal(args, rank, world, dist)
+        if dist:
+            dist.destroy_process_group()
+        return 0
+    visible = torch.cuda.device_count()
+    if visible < 1 or (world > visible and not args.share_gpus):
+        print(f"bench.py: rank {rank}: {visible} GPU(s) visible for {world} ranks", file=sys.stderr)
+        return 2
+    device = local % visible
+    torch.cuda.set_device(device)
     ck.set_lanes_per_buffer(args.lanes)
     stream = torch.cuda.current_stream()
-    if args.h2d:
+    if args.h2d or args.rpc_batch or args.rpc_latency or args.file_records:
         if rank == 0:
-            run_h2d(args, stream)
-        return
-    if args.rpc_batch:
-        if rank == 0:
-            run_rpc_batch(args, stream)
-        return
-    if args.rpc_latency:
-        if rank == 0:
-            run_rpc_latency(args, stream)
-        return
-    if args.file_records:
-        if rank == 0:
-            run_file_records(args)
-        return
+            if args.h2d:
+                run_h2d(args, stream)
+            elif args.rpc_batch:
+                run_rpc_batch(args, stream)
+            elif args.rpc_latency:
+                run_rpc_latency(args, stream)
+            else:
+                run_file_records(args)
+        return 0
     cfg = CONFIGS[args.config]
-    wl = Workload(cfg, rank, stream)
-    wl.step()
-    torch.cuda.synchronize()
-    ok = wl.self_check()
+    wl = Workload(cfg, rank, stream)  # the fill kernel runs right before the warmup launches
 
     def on_step(s, step):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -446,12 +664,43 @@ def main():
         b.record(stream)
         return lambda: a.elapsed_time(b)
 
-    elapsed, kernel_ms = timed_region(wl.step, args.steps, args.warmup, torch.cuda.synchronize, dist, on_step)
+    if args.pmc_child:  # the workload's launches under rocprofv3 --pmc (live_traffic)
+        for _ in range(args.warmup + args.steps):
+            wl.step()
+        torch.cuda.synchronize()
+        return 0
+    elapsed, kernel_ms, local_el, local_ms = timed_region(wl.step, args.steps, args.warmup, torch.cuda.synchronize,
+                                                          dist, on_step)
+    ok = wl.self_check()  # the last timed step's results, checked after the timed region
     value = aggregate_gibps(wl.bytes_per_step, args.steps, world, elapsed)
     per_launch_gbps = wl.bytes_per_step / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic_json, args.config)
+    ls = launch_summary(local_ms)
+    ranks = gather_ranks(dist, {"rank": rank, "device": device, "wall_s": round(local_el, 6),
+                                "launch_ms": ls, "self_check": ok})
+    all_ok = all(r["self_check"] for r in ranks)
+
+    shape64 = None
+    if world == 1 and cfg["kind"] == "strided" and not args.no_shape64 and not args.lanes:
+        # The north star's literal shape (one wavefront per buffer, G = 64)
+        # beside the measured-best lane group, outside the timed region.
+        ck.set_lanes_per_buffer(64)
+        _, ms64, _, l64 = timed_region(wl.step, 20, 3, torch.cuda.synchronize, None, on_step)
+        ck.set_lanes_per_buffer(0)
+        shape64 = {"lanes_per_buffer": 64, "kernel_ms_mean": round(ms64, 4),
+                   "kernel_ms_median": round(float(np.median(l64)), 4),
+                   "frac": round(wl.bytes_per_step / (ms64 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+
+    traffic, traffic_src = None, None
+    if rank == 0 and world == 1 and not args.no_live_pmc:
+        lt = live_traffic(args.config)
+        if lt is not None:
+            traffic, traffic_src = lt["bytes"], f"live rocprofv3 --pmc FETCH_SIZE x1024x2, {lt['launches']} launches"
+    if traffic is None:
+        traffic = load_traffic(args.traffic_json, args.config)
+        traffic_src = f"profiles/pmc_{args.config}.json (committed PMC pass)" if traffic else None
 
     if rank == 0:
+        steady = wl.bytes_per_step / (float(np.median([r["launch_ms"]["median"] for r in ranks])) * 1e-3) / 1e9
         res = {
             "metric": METRIC.replace("CRC32C", "CRC-64/ECMA") if cfg["kind"] == "strided64" else METRIC,
             "value": round(value, 3),
@@ -470,16 +719,30 @@ def main():
                        "lanes_per_buffer": args.lanes or "auto"},
             "roofline": {"bound": "hbm", "achieved": round(per_launch_gbps, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(per_launch_gbps / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "algorithmic_bytes": wl.bytes_per_step},
-            "self_check": ok,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes": wl.bytes_per_step,
+                         "frac_kernel": round(per_launch_gbps / HBM_PEAK_GBPS, 4),
+                         "frac_wall": round(wl.bytes_per_step * args.steps * world / elapsed / 1e9
+                                            / (HBM_PEAK_GBPS * world), 4),
+                         "frac_steady_median_launch": round(steady / HBM_PEAK_GBPS, 4),
+                         "clock_note": "frac/frac_kernel: mean HIP-event launch time (slowest rank); frac_wall: "
+                                       "value's wall clock; frac_steady: median launch"},
+            "per_rank": ranks if world > 1 else None,
+            "launch_ms": ls if world == 1 else None,
+            "self_check": all_ok,
         }
+        if args.share_gpus and world > visible:
+            res["rehearsal"] = f"{world} ranks sharing {visible} visible GPU(s): not a scaling measurement"
+        if shape64:
+            res["north_star_shape_g64"] = shape64
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-            res["cpu_reference_c1"] = cpu_reference_c1(min(5.0, args.cpu_seconds))
+            res["cpu_reference_c1"] = cpu_reference_c1(min(2.0, args.cpu_seconds))
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0 if all_ok else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

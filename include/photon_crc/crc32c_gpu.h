@@ -159,10 +159,17 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
  * is device memory (hipMemoryTypeDevice) and, if so, run the calls above
  * synchronously on that pointer's device (legacy default stream), else call
  * the host engine. Off (the default, also at load time) restores the host
- * engines. Returns 0, or -EIO if a routed call failed since the last switch
- * (a routed call that fails returns 0 / writes nothing and records the error
- * text; there is no CPU recomputation). */
+ * engines. The reference signatures have no error channel and the reference
+ * always computes (crc.cpp:114-117), so a routed call whose device work
+ * fails NEVER returns a made-up value: it is reported on stderr, counted,
+ * errno is set to EIO, and the bytes are copied to the host and checksummed
+ * by the host engine (same result as the reference); if even that copy fails
+ * the process aborts with a message. Returns 0, or -EIO if a routed call
+ * failed since the last switch (photon_crc_dispatch_fallbacks() counts them). */
 int photon_crc_set_device_dispatch(int on);
+/* Number of routed calls so far whose device work failed and that were
+ * recomputed on the host (0 in a healthy process; tests assert it). */
+uint64_t photon_crc_dispatch_fallbacks(void);
 
 /* CRC-64/ECMA batches (reference crc64ecma.h:20-38: reflected polynomial
  * 0xC96C5795D7870F42, init and result inverted):
@@ -214,43 +221,8 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
 int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                      uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream);
 
-/* Engine selection for photon_crc32c_batch_* (testing / tuning):
- * lanes per buffer G in {4,8,16,32,64}; 0 = automatic (default). */
-int photon_crc_set_lanes_per_buffer(int g);
-
-/* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
- * lane run B, rows per step U and steps in flight D, one of (1,4,3), (2,2,3),
- * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4).
- * The streaming kernel is OFF by default (the generic kernel is faster with
- * the current tables); run_blocks = 0 turns it off again. */
-int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
-
-/* Batch kernel variant (testing / tuning): 2, 4 (default) or 8 = the generic
- * kernel with that many rows per step; 0 = the fused kernel (four rows per
- * step with the row shifts folded into the tables). */
-int photon_crc_set_generic_rows(int rows_per_step);
-
-/* The CRC-64 streaming kernel (uniform batches; off by default, the generic
- * kernel is faster): a shape turns it on -- rows per step U and steps in
- * flight D, one of (4,1..3), (2,2..4), (8,1); U = 0 turns it off again. */
-int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
-
-/* Interleaved row partials per lane in the CRC-64 streaming kernel (testing /
- * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
-int photon_crc64_set_interleave(int partials);
-
-/* Message batches (photon_crc32c_batch_msg[_n], the CheckedMessage batch),
- * testing / tuning: 0 = automatic (default: one kernel with a lane group per
- * message, chained through the seed, when no per-segment CRCs are requested
- * and there are >= 4096 wavefronts' worth of short messages; else parallel
- * segment CRCs + a fold kernel), 1 = always the one-kernel form, 2 = always
- * the two-kernel form. */
-int photon_crc_set_msg_mode(int mode);
-
-/* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
- * each lane reads two consecutive 16-byte blocks per row, one row shift per
- * 32 bytes (lanes per buffer <= 32; overrides the interleave). */
-int photon_crc64_set_run_blocks(int blocks);
+/* Tuning knobs, the failure-injection hook and the bench data utilities are
+ * declared in <photon_crc/tuning.h> (not for production callers). */
 
 /* Producers outside device memory.
  * photon_crc_host_register: make an existing host range (e.g. the iovec
@@ -286,20 +258,6 @@ int photon_crc_stream_on_complete(void* stream, void (*fn)(void* arg), void* arg
 int photon_crc_device_alloc(void** ptr, uint64_t nbytes);
 int photon_crc_device_free(void* ptr);
 int photon_crc_memcpy_async(void* dst, const void* src, uint64_t nbytes, void* stream);
-
-/* Test/bench utility (not on the checksum path): fill count buffers of
- * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
- * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),
- * little-endian; identical to photonlibos_amd.datagen. */
-int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
-                                  uint64_t seed_base, void* stream);
-
-/* Bench utility (not on the checksum path): read nbytes (16-byte aligned
- * base) once with the CRC kernels' load instructions and fold them into
- * d_sink (>= 256 words; grid = min(8*CUs, sink_words/256) blocks of 256):
- * the achievable HBM-read rate the roofline is compared against. */
-int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
-                                void* stream);
 
 #ifdef __cplusplus
 }

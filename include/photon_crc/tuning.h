@@ -1,0 +1,86 @@
+/*
+ * tuning.h -- NOT for production callers of libphoton_checksum.so.
+ *
+ * Engine-shape knobs used by the tuning scripts and the parity tests (every
+ * variant is parity-tested; the defaults are the measured-fastest shapes),
+ * a failure-injection hook for the failure-contract test, and the bench's
+ * synthetic-data utilities. Every knob is a process-wide atomic word that a
+ * launch reads once, so changing one while other threads submit batches is
+ * race-free (each launch runs entirely with the old or entirely with the new
+ * shape); it is still a process-wide setting, which is why it is not part of
+ * the production header <photon_crc/crc32c_gpu.h>.
+ */
+#ifndef PHOTON_CRC_TUNING_H
+#define PHOTON_CRC_TUNING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Engine selection for photon_crc32c_batch_* (testing / tuning):
+ * lanes per buffer G in {4,8,16,32,64}; 0 = automatic (default). */
+int photon_crc_set_lanes_per_buffer(int g);
+
+/* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
+ * lane run B, rows per step U and steps in flight D, one of (1,4,3), (2,2,3),
+ * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4).
+ * The streaming kernel is OFF by default (the generic kernel is faster with
+ * the current tables); run_blocks = 0 turns it off again. */
+int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
+
+/* Batch kernel variant (testing / tuning): 2, 4 (default) or 8 = the generic
+ * kernel with that many rows per step; 0 = the fused kernel (four rows per
+ * step with the row shifts folded into the tables). */
+int photon_crc_set_generic_rows(int rows_per_step);
+
+/* The CRC-64 streaming kernel (uniform batches; off by default, the generic
+ * kernel is faster): a shape turns it on -- rows per step U and steps in
+ * flight D, one of (4,1..3), (2,2..4), (8,1); U = 0 turns it off again. */
+int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
+
+/* Interleaved row partials per lane in the CRC-64 streaming kernel (testing /
+ * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
+int photon_crc64_set_interleave(int partials);
+
+/* Message batches (photon_crc32c_batch_msg[_n], the CheckedMessage batch),
+ * testing / tuning: 0 = automatic (default: one kernel with a lane group per
+ * message, chained through the seed, when no per-segment CRCs are requested
+ * and there are >= 4096 wavefronts' worth of short messages; else parallel
+ * segment CRCs + a fold kernel), 1 = always the one-kernel form, 2 = always
+ * the two-kernel form. */
+int photon_crc_set_msg_mode(int mode);
+
+/* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
+ * each lane reads two consecutive 16-byte blocks per row, one row shift per
+ * 32 bytes (lanes per buffer <= 32; overrides the interleave). */
+int photon_crc64_set_run_blocks(int blocks);
+
+/* Lanes per buffer the engine picks for buffers of typical length n (the
+ * lane-group table of DESIGN.md §4, or the override when one is set). */
+int photon_crc_lanes_for(uint64_t nbytes);
+
+/* Failure injection (tests only): the next `n` device entry points called on
+ * this thread return -EIO before enqueuing anything ("injected failure"). */
+void photon_crc_test_fail_next(int n);
+
+/* Test/bench utility (not on the checksum path): fill count buffers of
+ * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
+ * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),
+ * little-endian; identical to photonlibos_amd.datagen. */
+int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
+                                  uint64_t seed_base, void* stream);
+
+/* Bench utility (not on the checksum path): read nbytes (16-byte aligned
+ * base) once with the CRC kernels' load instructions and fold them into
+ * d_sink (>= 256 words; grid = min(8*CUs, sink_words/256) blocks of 256):
+ * the achievable HBM-read rate the roofline is compared against. */
+int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
+                                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PHOTON_CRC_TUNING_H */

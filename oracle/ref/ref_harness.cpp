@@ -18,6 +18,8 @@
 #include <thread>
 #include <vector>
 
+#include "../../tests/cpp/spin_pool.h"
+
 // Declarations as in the reference's public headers (crc32c.h:20-92,
 // crc64ecma.h:20-87) and the test's extra entry points (test_checksum.cpp:86-87).
 uint32_t crc32c_sw(const uint8_t*, size_t, uint32_t);
@@ -255,35 +257,22 @@ static int vectors() {
 
 // `bench <nbuf> <len> <threads> <min_seconds>`: Photon's crc32c() (auto
 // dispatch, crc.cpp:339-358 on SSE4.2 hosts) over nbuf random buffers of len
-// bytes (stream 0x5EED0001 + i), split across threads; best pass of several.
+// bytes (stream 0x5EED0001 + i), split across a persistent pool of pinned
+// threads (tests/cpp/spin_pool.h: no thread start-up inside a pass); each
+// thread first-touches its own slice. Best and median pass over min_seconds.
 static int bench(size_t nbuf, size_t len, int threads, double min_s) {
+    benchpool::SpinPool pool(threads);
     std::vector<uint8_t> buf(nbuf * len);
-    for (size_t i = 0; i < nbuf; ++i) fill(buf.data() + i * len, len, 0x5EED0001ull + i);
     std::vector<uint32_t> out(nbuf);
-    auto pass = [&]() {
-        auto t0 = std::chrono::steady_clock::now();
-        std::vector<std::thread> th;
-        for (int t = 0; t < threads; ++t)
-            th.emplace_back([&, t]() {
-                size_t b = nbuf * t / threads, e = nbuf * (t + 1) / threads;
-                for (size_t i = b; i < e; ++i) out[i] = crc32c_auto(buf.data() + i * len, len, 0);
-            });
-        for (auto& x : th) x.join();
-        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    };
-    double best = 1e30, total = 0;
-    int passes = 0;
-    while (total < min_s || passes < 3) {
-        double t = pass();
-        best = t < best ? t : best;
-        total += t;
-        ++passes;
-    }
+    benchpool::time_passes(pool, nbuf, 0.0, [&](size_t i) { fill(buf.data() + i * len, len, 0x5EED0001ull + i); });
+    const benchpool::PassStats st = benchpool::time_passes(
+        pool, nbuf, min_s, [&](size_t i) { out[i] = crc32c_auto(buf.data() + i * len, len, 0); });
     uint32_t x = 0;
     for (auto c : out) x ^= c;
-    printf("{\"gib_per_s\": %.4f, \"best_s\": %.6f, \"passes\": %d, \"threads\": %d, \"nbuf\": %zu, "
-           "\"len\": %zu, \"xor_of_crcs\": %u}\n",
-           (double)nbuf * len / best / (1u << 30), best, passes, threads, nbuf, len, x);
+    printf("{\"gib_per_s\": %.4f, \"gib_per_s_median\": %.4f, \"best_s\": %.6f, \"passes\": %d, "
+           "\"threads\": %d, \"nbuf\": %zu, \"len\": %zu, \"xor_of_crcs\": %u}\n",
+           (double)nbuf * len / st.best_s / (1u << 30), (double)nbuf * len / st.median_s / (1u << 30), st.best_s,
+           st.passes, threads, nbuf, len, x);
     return 0;
 }
 

@@ -78,6 +78,10 @@ def _declare(L):
     fn("photon_crc_memcpy_async", ctypes.c_int, vp, vp, u64, vp)
     fn("photon_crc_host_unregister", ctypes.c_int, vp)
     fn("photon_crc32c_file_strided", ctypes.c_int, ctypes.c_int, u64, u64, u64, u64, u32, vp)
+    fn("photon_crc_dispatch_fallbacks", u64)
+    # tuning / test hooks (include/photon_crc/tuning.h)
+    fn("photon_crc_lanes_for", ctypes.c_int, u64)
+    fn("photon_crc_test_fail_next", None, ctypes.c_int)
     fn("photon_crc32c_series_device", ctypes.c_int, vp, u32, u32, vp, vp)
     fn("photon_crc32c_combine_series_device", ctypes.c_int, vp, u32, u32, vp, vp)
     fn("photon_crc32c_trim_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp, vp)

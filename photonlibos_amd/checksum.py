@@ -402,8 +402,26 @@ def extend_device(data, nbytes, seed, out, stream=None):
 
 def set_device_dispatch(on):
     """Route crc32c_auto / crc32c_series_auto / crc32c_combine_series_auto to the
-    device for device pointers (photon_crc_set_device_dispatch)."""
+    device for device pointers (photon_crc_set_device_dispatch). Raises
+    CrcError(-EIO) if a routed call failed on the device since the last switch
+    (it was recomputed on the host: dispatch_fallbacks())."""
     _check(lib().photon_crc_set_device_dispatch(1 if on else 0))
+
+
+def dispatch_fallbacks():
+    """Routed calls whose device work failed and were recomputed on the host."""
+    return int(lib().photon_crc_dispatch_fallbacks())
+
+
+def lanes_for(nbytes):
+    """Lanes per buffer the engine picks for buffers of nbytes (tuning.h)."""
+    return int(lib().photon_crc_lanes_for(nbytes))
+
+
+def inject_failures(n):
+    """tuning.h failure injection: the next n device entry points called on
+    this thread return -EIO before enqueuing anything."""
+    lib().photon_crc_test_fail_next(n)
 
 
 _CRC_PTR_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32)

@@ -24,6 +24,7 @@ namespace {
 
 using pcrc::report_error;
 using pcrc::report_hip_error;
+using pcrc::registered_range_check;
 
 // ------------------------------------------------------------------ pool
 constexpr int kMinClass = 12;               // 4 KiB blocks
@@ -87,6 +88,23 @@ const void* device_address(const void* p, uint64_t n, bool* host) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
+        return nullptr;
+    }
+    // The whole range [p, p+n) must lie inside the one allocation or
+    // registration that p belongs to, else the kernels would read past it:
+    // device memory is checked against its allocation, host memory against a
+    // photon_crc_host_register registration (memory registered by other code
+    // keeps the start-pointer check: HIP does not report those ranges).
+    if (a.type == hipMemoryTypeDevice) {
+        void* lo = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&lo, &size, const_cast<void*>(p)) == hipSuccess && size) {
+            const uintptr_t q = reinterpret_cast<uintptr_t>(p), b0 = reinterpret_cast<uintptr_t>(lo);
+            if (q < b0 || n > size || q - b0 > size - n) return nullptr;
+        } else {
+            (void)hipGetLastError();
+        }
+    } else if (registered_range_check(p, n) == 0) {
         return nullptr;
     }
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) {
@@ -337,7 +355,16 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
 
 int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*done)(void* arg), void* arg) {
     if (!b) return report_error(-EINVAL, "null batch");
-    if (b->submitted && !b->completed) return report_error(-EBUSY, "batch still running");
+    if (b->submitted && !b->completed) {
+        // A caller driven by the `done` callback never called wait(): if the
+        // previous submit has finished, settle it and go on; -EBUSY only while
+        // it is really still running.
+        hipError_t q = hipEventQuery(b->done_ev);
+        if (q == hipErrorNotReady) return report_error(-EBUSY, "batch still running");
+        if (q != hipSuccess) return report_hip_error(q, "hipEventQuery");
+        int64_t frc = finish(b);
+        if (frc < 0) return (int)frc;
+    }
     DeviceScope scope(b->dev);
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e = hipSuccess;

@@ -48,6 +48,7 @@
 #include <photon/common/checksum/crc64ecma.h>
 
 #include "../../include/photon_crc/crc32c_gpu.h"
+#include "../../include/photon_crc/tuning.h"
 #include "crc32c_kernels.h"
 #include "crc64_kernels.h"
 #include "gf2.h"
@@ -59,18 +60,43 @@ namespace pcrc {
 namespace {
 
 thread_local std::string g_err;
-int g_lanes_override = 0;
+
+// Tuning knobs (include/photon_crc/tuning.h). Photon calls the checksum from
+// many vCPU threads at once and the reference promises reentrant calls
+// (crc.cpp:126-137: pointers written once, pure functions), so every knob is
+// an atomic word that a launch reads ONCE; a multi-field shape is packed into
+// one word so a launch never sees half of a concurrent setter's update.
+std::atomic<int> g_lanes_override{0};
 // Batch kernel: rows per step of the generic kernel (2, 4, 8), or 0 = the
 // fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
 // the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
-int g_generic_u = 4;
-int g_msg_mode = 0;  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
-int g_stream_b = 1, g_stream_u = 4, g_stream_d = 3;  // streaming kernel: run blocks, rows/step, steps in flight
-// The streaming kernel is a tuning option: with the conflict-free rotated
-// tables the generic kernel measures faster on every config
-// (profiles/tune_r01_generic_rows.jsonl), so it is off by default.
-bool g_stream_enabled = false;
-bool g_stream64_enabled = false;  // the generic kernel is faster with lagged blocks
+std::atomic<int> g_generic_u{4};
+std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
+// Streaming kernel shape, 0 = off (the default: with the conflict-free rotated
+// tables the generic kernel measures faster on every config,
+// profiles/tune_r01_generic_rows.jsonl), else run blocks | rows/step << 8 |
+// steps in flight << 16.
+std::atomic<uint32_t> g_stream_cfg{0};
+// CRC-64 streaming kernel: bit 31 = on (off by default: the generic kernel is
+// faster with lagged blocks), rows/step (bits 0-7), steps in
+// flight (8-15), interleave (16-23), run blocks (24-30).
+std::atomic<uint32_t> g_stream64_cfg{4u | 3u << 8 | 1u << 16 | 1u << 24};
+std::mutex g_knob_mu;  // serialises read-modify-write setters of packed words
+
+struct Stream64Cfg {
+    bool on;
+    int u, d, v, b;
+};
+Stream64Cfg stream64_cfg() {
+    const uint32_t w = g_stream64_cfg.load(std::memory_order_relaxed);
+    return {(w >> 31) != 0, (int)(w & 0xff), (int)((w >> 8) & 0xff), (int)((w >> 16) & 0xff),
+            (int)((w >> 24) & 0x7f)};
+}
+void set_stream64_cfg(const Stream64Cfg& c) {
+    g_stream64_cfg.store((c.on ? 1u << 31 : 0u) | (uint32_t)c.u | (uint32_t)c.d << 8 | (uint32_t)c.v << 16 |
+                             (uint32_t)c.b << 24,
+                         std::memory_order_relaxed);
+}
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -89,9 +115,15 @@ struct DeviceInfo {
 
 std::mutex g_mu;
 std::vector<DeviceInfo> g_dev;
+thread_local int g_fail_next = 0;  // photon_crc_test_fail_next (tuning.h)
 
 // Resolve the current device; only gfx950 is supported (no other code path).
+// Every device entry point passes through here before it enqueues anything.
 int current_device(int* cus) {
+    if (g_fail_next > 0) {
+        --g_fail_next;
+        return fail(-EIO, "injected failure (photon_crc_test_fail_next)");
+    }
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -110,6 +142,56 @@ int current_device(int* cus) {
     if (!di.ok) return fail(-ENODEV, "photon_crc: no gfx950 device (got other arch)");
     *cus = di.cus;
     return dev;
+}
+
+// Stream-ordered scratch for multi-kernel calls (segment CRCs between the
+// segment and fold kernels, piece descriptors of one long buffer). It comes
+// from a library-owned pool per device whose memory is reused ONLY in the
+// order of the stream that freed it: opportunistic and event-following
+// cross-stream reuse are off. With HIP's default pool, 16 threads submitting
+// on their own streams read another call's segment CRCs now and then
+// (tests/cpp/concurrency_test.cpp: 2-8 wrong message CRCs in 30 K); with
+// cross-stream reuse off they never do.
+struct ScratchPool {
+    bool ready = false;
+    hipMemPool_t pool = nullptr;
+};
+std::mutex g_pool_mu;
+ScratchPool g_pools[64];
+
+int scratch_alloc(void** p, uint64_t bytes, hipStream_t st) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    if (dev < 0 || dev >= 64) return fail(-ENODEV, "device index beyond the scratch-pool table");
+    hipMemPool_t pool;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        ScratchPool& sp = g_pools[dev];
+        if (!sp.ready) {
+            hipMemPoolProps props{};
+            props.allocType = hipMemAllocationTypePinned;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            if ((e = hipMemPoolCreate(&sp.pool, &props)) != hipSuccess) return hip_fail(e, "hipMemPoolCreate");
+            int off = 0;
+            uint64_t keep = 64ull << 20;  // keep up to 64 MiB cached between calls
+            if ((e = hipMemPoolSetAttribute(sp.pool, hipMemPoolReuseAllowOpportunistic, &off)) != hipSuccess ||
+                (e = hipMemPoolSetAttribute(sp.pool, hipMemPoolReuseAllowInternalDependencies, &off)) != hipSuccess ||
+                (e = hipMemPoolSetAttribute(sp.pool, hipMemPoolReuseFollowEventDependencies, &off)) != hipSuccess ||
+                (e = hipMemPoolSetAttribute(sp.pool, hipMemPoolAttrReleaseThreshold, &keep)) != hipSuccess)
+                return hip_fail(e, "hipMemPoolSetAttribute");
+            sp.ready = true;
+        }
+        pool = sp.pool;
+    }
+    e = hipMallocFromPoolAsync(p, bytes ? bytes : 1, pool, st);
+    return e == hipSuccess ? 0 : hip_fail(e, "hipMallocFromPoolAsync");
+}
+
+int scratch_free(void* p, hipStream_t st) {
+    hipError_t e = hipFreeAsync(p, st);
+    return e == hipSuccess ? 0 : hip_fail(e, "hipFreeAsync");
 }
 
 // Constants for G lanes per buffer and runs of B blocks per lane per row:
@@ -200,7 +282,7 @@ const PowTable& rshift_table() {
 // Lanes per buffer: one wavefront per buffer for large buffers; pack small
 // buffers so every lane still walks >= 16 rows (DESIGN.md "Lane groups").
 int choose_lanes(uint64_t typical_len) {
-    if (g_lanes_override) return g_lanes_override;
+    if (const int g = g_lanes_override.load(std::memory_order_relaxed)) return g;
     // Measured with scripts/tune_gpu.py (profiles/tune_r01.md): 1 MiB buffers
     // G=64, 64 KiB G=32, 4-8 KiB G=8.
     if (typical_len >= (512u << 10)) return 64;
@@ -236,7 +318,8 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
     if (grid > (uint64_t)cus) grid = cus;
-    if (g_generic_u == 0) {
+    const int rows_per_step = g_generic_u.load(std::memory_order_relaxed);
+    if (rows_per_step == 0) {
         const FusedConsts& fc = fused_consts(g);
 #define LF(GG) hipLaunchKernelGGL((crc32c_fused_kernel<GG>), dim3(grid), dim3(kBlock), 0, stream, a, fc)
         switch (g) {
@@ -262,9 +345,9 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
         case 8: LB(8, UU); break;   \
         default: LB(4, UU); break;  \
     }
-    if (g_generic_u == 2) {
+    if (rows_per_step == 2) {
         LBG(2)
-    } else if (g_generic_u == 8) {
+    } else if (rows_per_step == 8) {
         LBG(8)
     } else {
         LBG(4)
@@ -316,14 +399,10 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     return 0;
 }
 
-// CRC-64 streaming kernel shape (rows per step, steps in flight, interleaved
-// partials per lane).
-int g_stream64_u = 4, g_stream64_d = 3, g_stream64_v = 1, g_stream64_b = 1;
-
 template <int G, int U, int D>
-void launch_uniform64_v(const Uniform64Args& a, dim3 grid, hipStream_t st) {
+void launch_uniform64_v(const Uniform64Args& a, dim3 grid, hipStream_t st, const Stream64Cfg& c) {
     if constexpr (G <= 32) {
-        if (g_stream64_b == 2) {
+        if (c.b == 2) {
             hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, 1, 2>), grid, dim3(kBlock), 0, st, a,
                                lane_consts64(2 * G));
             return;
@@ -331,37 +410,38 @@ void launch_uniform64_v(const Uniform64Args& a, dim3 grid, hipStream_t st) {
     }
     constexpr int V2 = (G <= 32 && U % 2 == 0) ? 2 : 1;
     constexpr int V4 = (G <= 16 && U % 4 == 0) ? 4 : V2;
-    if (g_stream64_v >= 4)
+    if (c.v >= 4)
         hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, V4>), grid, dim3(kBlock), 0, st, a, lane_consts64(G * V4));
-    else if (g_stream64_v >= 2)
+    else if (c.v >= 2)
         hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, V2>), grid, dim3(kBlock), 0, st, a, lane_consts64(G * V2));
     else
         hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, 1>), grid, dim3(kBlock), 0, st, a, lane_consts64(G));
 }
 
 template <int G>
-bool launch_uniform64_g(const Uniform64Args& a, dim3 grid, hipStream_t st) {
-    const int u = g_stream64_u, d = g_stream64_d;
-    if (u == 4 && d == 2) launch_uniform64_v<G, 4, 2>(a, grid, st);
-    else if (u == 4 && d == 3) launch_uniform64_v<G, 4, 3>(a, grid, st);
-    else if (u == 2 && d == 4) launch_uniform64_v<G, 2, 4>(a, grid, st);
-    else if (u == 8 && d == 1) launch_uniform64_v<G, 8, 1>(a, grid, st);
-    else if (u == 2 && d == 2) launch_uniform64_v<G, 2, 2>(a, grid, st);
-    else if (u == 2 && d == 3) launch_uniform64_v<G, 2, 3>(a, grid, st);
-    else if (u == 4 && d == 1) launch_uniform64_v<G, 4, 1>(a, grid, st);
+bool launch_uniform64_g(const Uniform64Args& a, dim3 grid, hipStream_t st, const Stream64Cfg& c) {
+    const int u = c.u, d = c.d;
+    if (u == 4 && d == 2) launch_uniform64_v<G, 4, 2>(a, grid, st, c);
+    else if (u == 4 && d == 3) launch_uniform64_v<G, 4, 3>(a, grid, st, c);
+    else if (u == 2 && d == 4) launch_uniform64_v<G, 2, 4>(a, grid, st, c);
+    else if (u == 8 && d == 1) launch_uniform64_v<G, 8, 1>(a, grid, st, c);
+    else if (u == 2 && d == 2) launch_uniform64_v<G, 2, 2>(a, grid, st, c);
+    else if (u == 2 && d == 3) launch_uniform64_v<G, 2, 3>(a, grid, st, c);
+    else if (u == 4 && d == 1) launch_uniform64_v<G, 4, 1>(a, grid, st, c);
     else return false;
     return true;
 }
 
 int try_launch_uniform64(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint64_t seed0,
                          const uint64_t* seeds, uint64_t* out, hipStream_t stream) {
-    if (!g_stream64_enabled || count == 0) return 1;
+    const Stream64Cfg c = stream64_cfg();
+    if (!c.on || count == 0) return 1;
     const int g = choose_lanes(nbytes);
-    const int b = (g_stream64_b == 2 && g <= 32) ? 2 : 1;
+    const int b = (c.b == 2 && g <= 32) ? 2 : 1;
     const uint64_t row = 16ull * g * b;
     if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
     const uint64_t rows = nbytes / row;
-    if (rows % (uint64_t)g_stream64_u) return 1;
+    if (rows % (uint64_t)c.u) return 1;
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
@@ -373,11 +453,11 @@ int try_launch_uniform64(const uint8_t* base, uint64_t stride, uint64_t nbytes, 
     Uniform64Args a{base, stride, rows, count, out, mulmod64(seeds ? ~0ull : ~seed0, xn)};
     bool ok = false;
     switch (g) {
-        case 64: ok = launch_uniform64_g<64>(a, dim3(grid), stream); break;
-        case 32: ok = launch_uniform64_g<32>(a, dim3(grid), stream); break;
-        case 16: ok = launch_uniform64_g<16>(a, dim3(grid), stream); break;
-        case 8: ok = launch_uniform64_g<8>(a, dim3(grid), stream); break;
-        default: ok = launch_uniform64_g<4>(a, dim3(grid), stream); break;
+        case 64: ok = launch_uniform64_g<64>(a, dim3(grid), stream, c); break;
+        case 32: ok = launch_uniform64_g<32>(a, dim3(grid), stream, c); break;
+        case 16: ok = launch_uniform64_g<16>(a, dim3(grid), stream, c); break;
+        case 8: ok = launch_uniform64_g<8>(a, dim3(grid), stream, c); break;
+        default: ok = launch_uniform64_g<4>(a, dim3(grid), stream, c); break;
     }
     if (!ok) return fail(-EINVAL, "unsupported CRC-64 streaming configuration");
     hipError_t e = hipGetLastError();
@@ -412,8 +492,7 @@ void launch_uniform_t(const UniformArgs& a, dim3 grid, hipStream_t stream) {
 
 // The instantiated (B, U, D) shapes: ring registers (D+1)*U*B*4 <= 80 VGPRs.
 template <int G>
-bool launch_uniform_g(const UniformArgs& a, dim3 grid, hipStream_t stream) {
-    const int b = g_stream_b, u = g_stream_u, d = g_stream_d;
+bool launch_uniform_g(const UniformArgs& a, dim3 grid, hipStream_t stream, int b, int u, int d) {
     if (b == 2 && u == 2 && d == 3) launch_uniform_t<G, 2, 2, 3>(a, grid, stream);
     else if (b == 1 && u == 4 && d == 3) launch_uniform_t<G, 1, 4, 3>(a, grid, stream);
     else if (b == 4 && u == 1 && d == 3) launch_uniform_t<G, 4, 1, 3>(a, grid, stream);
@@ -437,12 +516,14 @@ bool stream_shape_ok(int b, int u, int d) {
 
 int try_launch_uniform(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint32_t seed0,
                        const uint32_t* seeds, uint32_t* out, hipStream_t stream) {
-    if (!g_stream_enabled || count == 0) return 1;
+    const uint32_t cfg = g_stream_cfg.load(std::memory_order_relaxed);
+    if (!cfg || count == 0) return 1;
+    const int sb = (int)(cfg & 0xff), su = (int)((cfg >> 8) & 0xff), sd = (int)((cfg >> 16) & 0xff);
     const int g = choose_lanes(nbytes);
-    const uint64_t row = 16ull * g * (uint64_t)g_stream_b;
+    const uint64_t row = 16ull * g * (uint64_t)sb;
     if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
     const uint64_t rows = nbytes / row;
-    if (rows % (uint64_t)g_stream_u) return 1;
+    if (rows % (uint64_t)su) return 1;
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
@@ -453,11 +534,11 @@ int try_launch_uniform(const uint8_t* base, uint64_t stride, uint64_t nbytes, ui
     UniformArgs a{base, stride, rows, count, out};
     bool ok = false;
     switch (g) {
-        case 64: ok = launch_uniform_g<64>(a, dim3(grid), stream); break;
-        case 32: ok = launch_uniform_g<32>(a, dim3(grid), stream); break;
-        case 16: ok = launch_uniform_g<16>(a, dim3(grid), stream); break;
-        case 8: ok = launch_uniform_g<8>(a, dim3(grid), stream); break;
-        default: ok = launch_uniform_g<4>(a, dim3(grid), stream); break;
+        case 64: ok = launch_uniform_g<64>(a, dim3(grid), stream, sb, su, sd); break;
+        case 32: ok = launch_uniform_g<32>(a, dim3(grid), stream, sb, su, sd); break;
+        case 16: ok = launch_uniform_g<16>(a, dim3(grid), stream, sb, su, sd); break;
+        case 8: ok = launch_uniform_g<8>(a, dim3(grid), stream, sb, su, sd); break;
+        default: ok = launch_uniform_g<4>(a, dim3(grid), stream, sb, su, sd); break;
     }
     if (!ok) return fail(-EINVAL, "unsupported streaming configuration");
     hipError_t e = hipGetLastError();
@@ -540,60 +621,72 @@ const char* photon_crc_last_error(void) { return g_err.c_str(); }
 int photon_crc_set_lanes_per_buffer(int g) {
     if (g != 0 && g != 4 && g != 8 && g != 16 && g != 32 && g != 64)
         return fail(-EINVAL, "lanes per buffer must be 0, 4, 8, 16, 32 or 64");
-    g_lanes_override = g;
+    g_lanes_override.store(g, std::memory_order_relaxed);
     return 0;
 }
+
+int photon_crc_lanes_for(uint64_t nbytes) { return choose_lanes(nbytes); }
+
+void photon_crc_test_fail_next(int n) { g_fail_next = n > 0 ? n : 0; }
 
 int photon_crc_set_generic_rows(int rows_per_step) {
     if (rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
         return fail(-EINVAL, "rows per step must be 0 (fused kernel), 2, 4 or 8");
-    g_generic_u = rows_per_step;
+    g_generic_u.store(rows_per_step, std::memory_order_relaxed);
     return 0;
 }
 
 int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight) {
     if (run_blocks == 0) {
-        g_stream_enabled = false;
+        g_stream_cfg.store(0, std::memory_order_relaxed);
         return 0;
     }
     if (!stream_shape_ok(run_blocks, rows_per_step, steps_in_flight))
         return fail(-EINVAL, "unsupported (run_blocks, rows_per_step, steps_in_flight)");
-    g_stream_enabled = true;
-    g_stream_b = run_blocks;
-    g_stream_u = rows_per_step;
-    g_stream_d = steps_in_flight;
+    g_stream_cfg.store((uint32_t)run_blocks | (uint32_t)rows_per_step << 8 | (uint32_t)steps_in_flight << 16,
+                       std::memory_order_relaxed);
     return 0;
 }
 
 int photon_crc_set_msg_mode(int mode) {
     if (mode < 0 || mode > 2) return fail(-EINVAL, "message mode must be 0 (auto), 1 (fused) or 2 (two kernels)");
-    g_msg_mode = mode;
+    g_msg_mode.store(mode, std::memory_order_relaxed);
     return 0;
 }
 
 int photon_crc64_set_run_blocks(int blocks) {
     if (blocks != 1 && blocks != 2) return fail(-EINVAL, "run blocks must be 1 or 2");
-    g_stream64_b = blocks;
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    Stream64Cfg c = stream64_cfg();
+    c.b = blocks;
+    set_stream64_cfg(c);
     return 0;
 }
 
 int photon_crc64_set_interleave(int partials) {
     if (partials != 1 && partials != 2 && partials != 4) return fail(-EINVAL, "interleave must be 1, 2 or 4");
-    g_stream64_v = partials;
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    Stream64Cfg c = stream64_cfg();
+    c.v = partials;
+    set_stream64_cfg(c);
     return 0;
 }
 
 int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight) {
     const int u = rows_per_step, d = steps_in_flight;
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    Stream64Cfg c = stream64_cfg();
     if (u == 0) {
-        g_stream64_enabled = false;
+        c.on = false;
+        set_stream64_cfg(c);
         return 0;
     }
     if (!((u == 4 && (d >= 1 && d <= 3)) || (u == 2 && (d >= 2 && d <= 4)) || (u == 8 && d == 1)))
         return fail(-EINVAL, "unsupported CRC-64 (rows_per_step, steps_in_flight)");
-    g_stream64_enabled = true;
-    g_stream64_u = u;
-    g_stream64_d = d;
+    c.on = true;
+    c.u = u;
+    c.d = d;
+    set_stream64_cfg(c);
     return 0;
 }
 
@@ -636,7 +729,11 @@ int host_batch_impl(const void* h_base, uint64_t stride, uint64_t nbytes, uint64
                     T* h_out,
                     int (*device_batch)(const void*, uint64_t, uint64_t, uint64_t, T, const T*, T*, void*)) {
     if (!count) return 0;
-    if (!h_base || !h_out || stride < nbytes) return fail(-EINVAL, "bad arguments");
+    if (!h_out || (!h_base && nbytes) || stride < nbytes) return fail(-EINVAL, "bad arguments");
+    if (!nbytes) {  // crc32c_extend / crc64ecma_extend over 0 bytes return the seed (crc.cpp:340)
+        for (uint64_t i = 0; i < count; ++i) h_out[i] = h_seeds ? h_seeds[i] : seed0;
+        return 0;
+    }
     const uint64_t pitch = (nbytes + 255) & ~uint64_t(255);
     if (pitch > kStageBytes) return fail(-EINVAL, "buffer larger than a staging chunk (256 MiB)");
     int cus = 0;
@@ -647,6 +744,16 @@ int host_batch_impl(const void* h_base, uint64_t stride, uint64_t nbytes, uint64
     std::lock_guard<std::mutex> lk(p->mu);
     int rc = pipe_init(*p);
     if (rc) return rc;
+    // Any return after the first enqueue drains both streams first: copies
+    // from the caller's h_base and kernels writing p->d_out must not outlive
+    // the call (the caller may free h_base; the next call reuses the slots).
+    struct Drain {
+        HostPipe* p;
+        ~Drain() {
+            (void)hipStreamSynchronize(p->copy);
+            (void)hipStreamSynchronize(p->comp);
+        }
+    } drain{p};
     hipError_t e;
     const uint64_t bytes = count * sizeof(T);
     if (p->out_cap < bytes) {
@@ -707,7 +814,7 @@ int photon_crc64ecma_host_batch_strided(const void* h_base, uint64_t stride, uin
 int photon_crc32c_host_batch_strided_multi(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                            uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out, int ndev) {
     if (!count) return 0;
-    if (!h_base || !h_out || stride < nbytes) return fail(-EINVAL, "bad arguments");
+    if (!h_out || (!h_base && nbytes) || stride < nbytes) return fail(-EINVAL, "bad arguments");
     int total = 0;
     hipError_t e = hipGetDeviceCount(&total);
     if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
@@ -814,8 +921,8 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
     // (With per-segment CRCs requested the fused form folds with a multiply per
     // segment on one lane and measured slower than the fold kernel, so it is
     // automatic only for the seed-chained form.)
-    const bool fused = g_msg_mode == 1 ||
-                       (g_msg_mode == 0 && !d_seg_out && nmsg >= 4096 * gpw && nseg <= 64 * nmsg);
+    const int mode = g_msg_mode.load(std::memory_order_relaxed);
+    const bool fused = mode == 1 || (mode == 0 && !d_seg_out && nmsg >= 4096 * gpw && nseg <= 64 * nmsg);
     if (fused) {
         int cus = 0;
         int dev = current_device(&cus);
@@ -845,8 +952,7 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
     if (!d_seg_out && nseg && seg_scratch) {
         a.out = seg_scratch;
     } else if (!d_seg_out && nseg) {
-        e = hipMallocAsync(&scratch, nseg * 4, st);
-        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+        if (int rc = scratch_alloc(&scratch, nseg * 4, st)) return rc;
         a.out = static_cast<uint32_t*>(scratch);
     }
     int rc = launch_batch(a, 8192, st, lanes);
@@ -858,8 +964,8 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
         if (e != hipSuccess) rc = hip_fail(e, "crc32c_msg_fold_kernel launch");
     }
     if (scratch) {
-        e = hipFreeAsync(scratch, st);
-        if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+        const int frc = scratch_free(scratch, st);
+        if (!rc) rc = frc;
     }
     return rc;
 }
@@ -939,8 +1045,7 @@ int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* 
     // d_seg_out is optional: without it the segment CRCs live in stream-ordered scratch.
     void* scratch = nullptr;
     if (!d_seg_out) {
-        hipError_t e = hipMallocAsync(&scratch, (nseg ? nseg : 1) * sizeof(uint64_t), st);
-        if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+        if (int rc = scratch_alloc(&scratch, (nseg ? nseg : 1) * sizeof(uint64_t), st)) return rc;
         d_seg_out = static_cast<uint64_t*>(scratch);
     }
     Batch64Args a{};
@@ -956,8 +1061,8 @@ int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* 
         if (e != hipSuccess) rc = hip_fail(e, "crc64_msg_fold_kernel launch");
     }
     if (scratch) {
-        hipError_t e = hipFreeAsync(scratch, st);
-        if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+        const int frc = scratch_free(scratch, st);
+        if (!rc) rc = frc;
     }
     return rc;
 }
@@ -977,8 +1082,8 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     int dev = current_device(&cus);
     if (dev < 0) return dev;
     void* scratch = nullptr;
-    hipError_t e = hipMallocAsync(&scratch, k * sizeof(photon_crc_iovec) + k * 8, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    if (int rc = scratch_alloc(&scratch, k * sizeof(photon_crc_iovec) + k * 8, st)) return rc;
+    hipError_t e;
     auto* iov = static_cast<photon_crc_iovec*>(scratch);
     auto* crcs = reinterpret_cast<uint64_t*>(iov + k);
     hipLaunchKernelGGL(crc32c_split_kernel, dim3((k + 255) / 256), dim3(256), 0, st,
@@ -999,8 +1104,8 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
         e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "crc64_fold_pieces_kernel launch");
     }
-    e = hipFreeAsync(scratch, st);
-    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    const int frc = scratch_free(scratch, st);
+    if (!rc) rc = frc;
     return rc;
 }
 
@@ -1088,8 +1193,8 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     if (dev < 0) return dev;
     // Stream-ordered scratch: k descriptors + k piece CRCs.
     void* scratch = nullptr;
-    hipError_t e = hipMallocAsync(&scratch, k * sizeof(photon_crc_iovec) + k * 4, st);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    if (int rc = scratch_alloc(&scratch, k * sizeof(photon_crc_iovec) + k * 4, st)) return rc;
+    hipError_t e;
     auto* iov = static_cast<photon_crc_iovec*>(scratch);
     auto* crcs = reinterpret_cast<uint32_t*>(iov + k);
     hipLaunchKernelGGL(crc32c_split_kernel, dim3((k + 255) / 256), dim3(256), 0, st,
@@ -1110,8 +1215,8 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
         e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "crc32c_extend_finish_kernel launch");
     }
-    e = hipFreeAsync(scratch, st);
-    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    const int frc = scratch_free(scratch, st);
+    if (!rc) rc = frc;
     return rc;
 }
 
@@ -1186,12 +1291,44 @@ struct DeviceScope {
     }
 };
 
-// A routed call that fails has no error channel in the reference signature:
-// it is reported loudly (stderr, errno = EIO, sticky flag), never recomputed.
+// A routed call that fails has no error channel in the reference signature,
+// and the reference always computes (crc.cpp:114-117): never return a made-up
+// value. The failure is reported loudly (stderr, counter, sticky flag, errno
+// = EIO) and the bytes are copied to the host and checksummed by the host
+// engine -- the same result the reference returns. If even that copy fails
+// (the device is gone), there is no right answer to give: abort.
+std::atomic<uint64_t> g_fallbacks{0};
+
 void routed_failure(const char* what, int rc) {
     g_dispatch_err.store(1);
-    fprintf(stderr, "photon_crc device dispatch: %s failed (%d): %s\n", what, rc, g_err.c_str());
+    g_fallbacks.fetch_add(1);
+    fprintf(stderr, "photon_crc device dispatch: %s failed on the device (%d): %s; recomputing on the host\n", what,
+            rc, g_err.c_str());
     errno = EIO;
+}
+
+[[noreturn]] void routed_abort(const char* what, hipError_t e) {
+    fprintf(stderr, "photon_crc device dispatch: %s: device copy for the host recomputation failed: %s; aborting "
+            "rather than returning a wrong checksum\n", what, hipGetErrorString(e));
+    abort();
+}
+
+// Feed [p, p+n) of device memory through host memory in chunks.
+template <typename F>
+void for_host_chunks(const uint8_t* p, size_t n, const char* what, F f) {
+    constexpr size_t kChunk = 16u << 20;
+    std::vector<uint8_t> buf(n < kChunk ? n : kChunk);
+    for (size_t off = 0; off < n; off += buf.size()) {
+        const size_t k = n - off < buf.size() ? n - off : buf.size();
+        hipError_t e = hipMemcpy(buf.data(), p + off, k, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) routed_abort(what, e);
+        f(buf.data(), k);
+    }
+}
+
+uint32_t host_crc_of_device(const uint8_t* p, size_t n, uint32_t crc) {
+    for_host_chunks(p, n, "crc32c_extend", [&](const uint8_t* h, size_t k) { crc = g_host_crc(h, k, crc); });
+    return crc;
 }
 
 // Run f(d_tmp) with `bytes` of stream-ordered device scratch on the default
@@ -1199,15 +1336,15 @@ void routed_failure(const char* what, int rc) {
 template <typename F>
 int with_scratch(uint64_t bytes, void* h_out, uint64_t out_bytes, F f) {
     void* tmp = nullptr;
-    hipError_t e = hipMallocAsync(&tmp, bytes, nullptr);
-    if (e != hipSuccess) return hip_fail(e, "hipMallocAsync");
+    if (int arc = scratch_alloc(&tmp, bytes, nullptr)) return arc;
     int rc = f(tmp);
+    hipError_t e;
     if (!rc) {
         e = hipMemcpyAsync(h_out, tmp, out_bytes, hipMemcpyDeviceToHost, nullptr);
         if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync");
     }
-    e = hipFreeAsync(tmp, nullptr);
-    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipFreeAsync");
+    const int frc = scratch_free(tmp, nullptr);
+    if (!rc) rc = frc;
     e = hipStreamSynchronize(nullptr);
     if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
     return rc;
@@ -1221,25 +1358,51 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     int rc = with_scratch(4, &r, 4, [&](void* d) {
         return photon_crc32c_extend_device(p, n, crc, static_cast<uint32_t*>(d), nullptr);
     });
-    if (rc) routed_failure("crc32c_extend", rc);
-    return rc ? 0 : r;
+    if (!rc) return r;
+    routed_failure("crc32c_extend", rc);
+    return host_crc_of_device(p, n, crc);
 }
 
 void dispatch_series(const uint8_t* buf, uint32_t part, uint32_t n, uint32_t* parts) {
     const int dev = (part && n) ? device_of(buf) : -1;
     if (dev < 0) return g_host_series(buf, part, n, parts);
     DeviceScope scope(dev);
+    // The device form keeps the SSE4.2 engine's rule (parts < 8 B give 0,
+    // crc.cpp:481-500); when the saved host engine is crc32c_series_sw those
+    // parts get their real CRCs (crc.cpp:474-478), so run the plain batch.
+    const bool sw = g_host_series == crc32c_series_sw;
+    auto run = [&](uint32_t* out) {
+        return sw ? photon_crc32c_batch_strided(buf, part, part, n, 0, nullptr, out, nullptr)
+                  : photon_crc32c_series_device(buf, part, n, out, nullptr);
+    };
+    const bool parts_on_dev = device_of(parts) == dev;
     int rc;
-    if (device_of(parts) == dev) {
-        rc = photon_crc32c_series_device(buf, part, n, parts, nullptr);
+    if (parts_on_dev) {
+        rc = run(parts);
         hipError_t e = rc ? hipSuccess : hipStreamSynchronize(nullptr);
         if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
     } else {
-        rc = with_scratch(4ull * n, parts, 4ull * n, [&](void* d) {
-            return photon_crc32c_series_device(buf, part, n, static_cast<uint32_t*>(d), nullptr);
-        });
+        rc = with_scratch(4ull * n, parts, 4ull * n, [&](void* d) { return run(static_cast<uint32_t*>(d)); });
     }
-    if (rc) routed_failure("crc32c_series", rc);
+    if (!rc) return;
+    routed_failure("crc32c_series", rc);
+    std::vector<uint32_t> h(n);
+    uint64_t i = 0;
+    std::vector<uint8_t> part_buf;
+    for_host_chunks(buf, (size_t)part * n, "crc32c_series", [&](const uint8_t* hp, size_t k) {
+        // whole parts only: gather across chunk edges into part_buf
+        part_buf.insert(part_buf.end(), hp, hp + k);
+        size_t whole = part_buf.size() / part;
+        g_host_series(part_buf.data(), part, (uint32_t)whole, h.data() + i);
+        i += whole;
+        part_buf.erase(part_buf.begin(), part_buf.begin() + whole * part);
+    });
+    if (parts_on_dev) {
+        hipError_t e = hipMemcpy(parts, h.data(), 4ull * n, hipMemcpyHostToDevice);
+        if (e != hipSuccess) routed_abort("crc32c_series", e);
+    } else {
+        memcpy(parts, h.data(), 4ull * n);
+    }
 }
 
 uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
@@ -1250,8 +1413,12 @@ uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
     int rc = with_scratch(4, &r, 4, [&](void* d) {
         return photon_crc32c_combine_series_device(crc, part, n, static_cast<uint32_t*>(d), nullptr);
     });
-    if (rc) routed_failure("crc32c_combine_series", rc);
-    return rc ? 0 : r;
+    if (!rc) return r;
+    routed_failure("crc32c_combine_series", rc);
+    std::vector<uint32_t> h(n);
+    hipError_t e = hipMemcpy(h.data(), crc, 4ull * n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) routed_abort("crc32c_combine_series", e);
+    return g_host_cseries(h.data(), part, n);
 }
 
 uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
@@ -1262,8 +1429,10 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     int rc = with_scratch(8, &r, 8, [&](void* d) {
         return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), nullptr);
     });
-    if (rc) routed_failure("crc64ecma_extend", rc);
-    return rc ? 0 : r;
+    if (!rc) return r;
+    routed_failure("crc64ecma_extend", rc);
+    for_host_chunks(p, n, "crc64ecma_extend", [&](const uint8_t* h, size_t k) { crc = g_host_crc64(h, k, crc); });
+    return crc;
 }
 
 }  // namespace
@@ -1291,3 +1460,5 @@ extern "C" int photon_crc_set_device_dispatch(int on) {
     }
     return g_dispatch_err.exchange(0) ? -EIO : 0;
 }
+
+extern "C" uint64_t photon_crc_dispatch_fallbacks(void) { return pcrc::g_fallbacks.load(); }

@@ -17,6 +17,7 @@
 #include <unistd.h>
 
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -95,6 +96,21 @@ int read_span_parallel(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_ma
 
 }  // namespace
 
+// Ranges registered through photon_crc_host_register, so the message batch
+// can check that a segment [p, p+n) stays inside its registration.
+std::mutex g_reg_mu;
+std::map<uintptr_t, uint64_t> g_reg;
+
+int pcrc::registered_range_check(const void* p, uint64_t n) {
+    const uintptr_t q = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.upper_bound(q);
+    if (it == g_reg.begin()) return -1;
+    --it;
+    if (q - it->first >= it->second) return -1;  // not inside a known registration
+    return n <= it->second - (q - it->first) ? 1 : 0;
+}
+
 extern "C" {
 
 int photon_crc_stream_create(void** stream) {
@@ -150,12 +166,18 @@ int photon_crc_memcpy_async(void* dst, const void* src, uint64_t nbytes, void* s
 int photon_crc_host_register(void* ptr, uint64_t len) {
     if (!ptr || !len) return report_error(-EINVAL, "null or empty range");
     hipError_t e = hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable);
-    return e == hipSuccess ? 0 : report_hip_error(e, "hipHostRegister");
+    if (e != hipSuccess) return report_hip_error(e, "hipHostRegister");
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[reinterpret_cast<uintptr_t>(ptr)] = len;
+    return 0;
 }
 
 int photon_crc_host_unregister(void* ptr) {
     hipError_t e = hipHostUnregister(ptr);
-    return e == hipSuccess ? 0 : report_hip_error(e, "hipHostUnregister");
+    if (e != hipSuccess) return report_hip_error(e, "hipHostUnregister");
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg.erase(reinterpret_cast<uintptr_t>(ptr));
+    return 0;
 }
 
 int photon_crc32c_file_strided(int fd, uint64_t offset, uint64_t stride, uint64_t nbytes, uint64_t count,

@@ -17,4 +17,8 @@ int report_hip_error(hipError_t e, const char* what);
 int batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg, uint64_t nseg,
                     uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_seg_out, uint32_t* d_out, void* stream,
                     int lanes, uint32_t* seg_scratch = nullptr);
+// [p, p+n) against the ranges registered with photon_crc_host_register:
+// 1 inside one registration, 0 p is registered but the range runs past it,
+// -1 p is in no registration made through this library.
+int registered_range_check(const void* p, uint64_t n);
 }  // namespace pcrc

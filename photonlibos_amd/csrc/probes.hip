@@ -69,7 +69,9 @@ __global__ __launch_bounds__(1024) void rows_kernel(const uint8_t* base, uint64_
 //   MODE 2: static for the first `static_rounds` rounds, tickets for the rest;
 //   MODE 3: as 2 with 8 per-XCC ticket regions and stealing across them;
 //   MODE 4: static with the chunk of workgroup b rotated by the round.
-// t[4*gw..4*gw+3] = s_memrealtime (100 MHz) at the wave start / end, HW_ID, XCC_ID.
+// t[6*gw..6*gw+5] = s_memrealtime (100 MHz) at the wave start / end, HW_ID, XCC_ID,
+// s_memtime (shader clock) at the wave start / end: the in-kernel clock of a
+// wave is d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
 template <int G, int MODE>
 __global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::BatchArgs args, pcrc::LaneConsts kc,
                                                                      uint64_t* t, uint32_t* ticket,
@@ -77,6 +79,7 @@ __global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::Batc
     using namespace pcrc;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
     build_tables(lds, kc);
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
@@ -139,18 +142,21 @@ __global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::Batc
             wv = value(nx);
         }
     }
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
-        t[4 * gw] = t0;
-        t[4 * gw + 1] = t1;
-        t[4 * gw + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID: wave, simd, cu, se
-        t[4 * gw + 3] = __builtin_amdgcn_s_getreg(20 | (3 << 11));   // XCC_ID
+        t[6 * gw] = t0;
+        t[6 * gw + 1] = t1;
+        t[6 * gw + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID: wave, simd, cu, se
+        t[6 * gw + 3] = __builtin_amdgcn_s_getreg(20 | (3 << 11));   // XCC_ID
+        t[6 * gw + 4] = c0;
+        t[6 * gw + 5] = c1;
     }
 }
 
 extern "C" {
 
-// crc_wave_times_kernel over a strided batch; `t` holds 4 * grid * 16 words,
+// crc_wave_times_kernel over a strided batch; `t` holds 6 * grid * 16 words,
 // `ticket` 256 words (zeroed here on the stream before the launch).
 int probe_crc_wave_times(const void* base, uint64_t nbytes, uint64_t count, uint32_t* out, uint64_t* t,
                          uint32_t* ticket, int g, int mode, int static_rounds, int cus, void* stream) {

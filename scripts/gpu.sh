@@ -1,0 +1,65 @@
+#!/bin/bash
+# One parameterised driver for GPU-box work (replaces round 1's one-off
+# gpu_*.sh wrappers). Every GPU step has its own time limit, steps stop at the
+# first failure (no retries), outputs land under gpurun_out/.
+#
+#   scripts/gpu.sh tests                 pytest -m gpu + smoke()
+#   scripts/gpu.sh bench [ARGS...]       python bench.py ARGS  -> gpurun_out/bench_<tag>.json
+#   scripts/gpu.sh prof CONFIG [ARGS]    rocprofv3 --kernel-trace --stats of bench.py --config CONFIG
+#   scripts/gpu.sh pmc CONFIG            rocprofv3 --pmc FETCH_SIZE pass (counters only)
+#   scripts/gpu.sh sq CONFIG             SQ/GRBM counter passes (scripts/pmc_kernel.sh)
+#   scripts/gpu.sh probe SCRIPT [ARGS]   python scripts/SCRIPT ARGS (bench-only probes)
+# Several commands chain with "::", e.g.
+#   scripts/gpu.sh tests :: bench --steps 20 --warmup 5 :: prof c2
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+n=0
+
+run_one() {
+  local cmd=$1; shift
+  n=$((n+1))
+  case $cmd in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+        || { echo "pytest failed"; tail -30 $O/pytest_gpu.log; return 1; }
+      tail -3 $O/pytest_gpu.log
+      timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; cat $O/smoke.log; return 1; } ;;
+    bench)
+      local tag; tag=$(echo "$*" | tr -c 'a-zA-Z0-9_' '_' | sed 's/__*/_/g;s/^_//;s/_$//'); tag=${tag:-default}
+      timeout -k 10 600 python -u bench.py "$@" > $O/bench_$tag.json 2> $O/bench_$tag.err \
+        || { echo "bench $* failed"; tail -20 $O/bench_$tag.err; return 1; }
+      cut -c1-400 $O/bench_$tag.json ;;
+    prof)
+      local c=$1; shift
+      (cd /tmp && true)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o $c -- \
+        python3 bench.py --config $c --no-cpu-baseline --no-live-pmc "$@" > $O/prof_$c.log 2>&1 \
+        || { echo "prof $c failed"; tail -20 $O/prof_$c.log; return 1; } ;;
+    pmc)
+      local c=$1
+      timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_$c -o $c -- \
+        python3 bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline --no-live-pmc --no-shape64 > $O/pmc_$c.log 2>&1 \
+        || { echo "pmc $c failed"; tail -20 $O/pmc_$c.log; return 1; } ;;
+    sq)
+      bash scripts/pmc_kernel.sh $1 $O/sq_$1 > /dev/null || { echo "sq $1 failed"; return 1; } ;;
+    probe)
+      local s=$1; shift
+      timeout -k 10 600 python -u scripts/$s "$@" > $O/probe_${s%.py}_$n.jsonl 2> $O/probe_${s%.py}_$n.err \
+        || { echo "probe $s failed"; tail -20 $O/probe_${s%.py}_$n.err; return 1; }
+      cut -c1-300 $O/probe_${s%.py}_$n.jsonl ;;
+    *) echo "unknown command $cmd"; return 1 ;;
+  esac
+}
+
+args=()
+for a in "$@" "::"; do
+  if [ "$a" = "::" ]; then
+    [ ${#args[@]} -gt 0 ] && { run_one "${args[@]}" || exit 1; }
+    args=()
+  else
+    args+=("$a")
+  fi
+done
+echo "gpu.sh: all ok"

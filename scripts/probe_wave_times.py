@@ -29,7 +29,7 @@ st = torch.cuda.current_stream()
 s = st.cuda_stream
 cus = torch.cuda.get_device_properties(0).multi_processor_count
 nw = cus * 16
-t = torch.zeros(4 * nw, dtype=torch.int64, device="cuda")
+t = torch.zeros(6 * nw, dtype=torch.int64, device="cuda")
 ticket = torch.zeros(256, dtype=torch.int32, device="cuda")
 rounds = int(os.environ.get("ROUNDS", "6"))
 
@@ -41,7 +41,7 @@ def launch(buf, n, cnt, out, g, mode, sr):
 
 
 def spread():
-    v = t.cpu().numpy().reshape(-1, 4).astype(np.int64)
+    v = t.cpu().numpy().reshape(-1, 6).astype(np.int64)
     v = v[v[:, 1] > 0]
     span = v[:, 1].max() - v[:, 0].min()
     idle = (v[:, 1].max() - v[:, 1]).sum() / (len(v) * span)
@@ -54,7 +54,7 @@ def structure():
     """Where the slow waves sit (last launch): mean busy time (end - start, us)
     per XCC, per shader engine, per SIMD and per wave slot; and the spread of
     per-CU means."""
-    v = t.cpu().numpy().reshape(-1, 4).astype(np.int64)
+    v = t.cpu().numpy().reshape(-1, 6).astype(np.int64)
     v = v[v[:, 1] > 0]
     busy = (v[:, 1] - v[:, 0]) / 100.0
     hw, xcc = v[:, 2], v[:, 3] & 0xF

@@ -5,6 +5,7 @@
 // crc32c(), and 20 timed launches. Exit 0 on bit-exact results.
 #include <photon/common/checksum/crc32c.h>
 #include <photon_crc/crc32c_gpu.h>
+#include <photon_crc/tuning.h>  // photon_crc_util_fill_splitmix (test data)
 
 #include <stdio.h>
 

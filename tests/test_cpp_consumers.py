@@ -77,3 +77,15 @@ def test_host_engines_under_asan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "asan64: 0 mismatches" in r.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_concurrent_submitters():
+    """16 threads on their own streams submit mixed batches while a 17th
+    flips every tuning knob; every result equals the oracle's (reentrancy,
+    crc.cpp:126-137)."""
+    exe = os.path.join(BIN, "concurrency_test")
+    assert os.path.exists(exe)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches, 0 errors" in r.stdout

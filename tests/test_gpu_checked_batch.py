@@ -143,3 +143,36 @@ def test_capacity_and_empty(torch_dev):
     assert b.result(1) == (True, 0)
     b.close()
     alloc.dealloc(a)
+
+
+def test_resubmit_after_completion_without_wait(torch_dev, oracle):
+    """A caller driven by completion (the `done` callback, or a stream sync)
+    may resubmit a finished batch without calling wait(): no -EBUSY."""
+    torch = torch_dev
+    d = torch.randint(0, 256, (8192,), dtype=torch.uint8, device="cuda")
+    want = oracle.crc32c(d.cpu().numpy())
+    b = MessageBatch(1, 1)
+    b.add([(d.data_ptr(), 8192)], None, want)
+    for _ in range(3):
+        b.submit()
+        torch.cuda.synchronize()  # finished, never waited on
+    assert b.wait() == 0 and b.result(0) == (True, want)
+    b.close()
+
+
+def test_segment_past_its_allocation_is_refused(torch_dev):
+    """[p, p+n) must lie inside p's allocation: a segment running past the end
+    of a hipMalloc'd block is -EFAULT, not a read of unmapped memory."""
+    import ctypes
+    from photonlibos_amd._native import lib
+    p = ctypes.c_void_p()
+    assert lib().photon_crc_device_alloc(ctypes.byref(p), 4096) == 0
+    try:
+        b = MessageBatch(2, 2)
+        b.add([(p.value, 4096)])            # the whole block: fine
+        with pytest.raises(CrcError) as e:
+            b.add([(p.value + 16, 4096)])   # 16 bytes past the end
+        assert e.value.code == -14
+        b.close()
+    finally:
+        lib().photon_crc_device_free(p.value)

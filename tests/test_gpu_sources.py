@@ -106,3 +106,20 @@ def test_registered_host_memory_in_batch(torch_dev, oracle):
     finally:
         b.close()
         ck.host_unregister(base)
+
+
+def test_registered_segment_past_registration_refused(torch_dev):
+    """A segment starting inside a photon_crc_host_register range but running
+    past its end is refused (-EFAULT) instead of read past the mapping."""
+    buf = np.zeros((1 << 20) + 4096, np.uint8)
+    base = (buf.ctypes.data + 4095) & ~4095
+    ck.host_register(base, 1 << 20)
+    try:
+        b = MessageBatch(4, 4)
+        b.add([(base + 100, (1 << 20) - 100)])  # exactly to the end: fine
+        with pytest.raises(CrcError) as e:
+            b.add([(base + 100, (1 << 20) - 99)])
+        assert e.value.code == -14
+        b.close()
+    finally:
+        ck.host_unregister(base)

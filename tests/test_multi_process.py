@@ -1,9 +1,14 @@
-"""The N>1 bench path on CPU: world_size-2 gloo processes run bench.py's
-timed region (barrier + sync both sides, max over ranks) with a CPU step,
-and the shard assignment gives every rank a disjoint buffer range with no
-data-path collective. CPU only."""
+"""The N>1 bench path on CPU: bench.py's own launcher (`--gpus 2` with no
+WORLD_SIZE starts torch.distributed.run as a child) runs two gloo ranks that
+each checksum their own shard through the library's host engine, time it in
+the same timed region (barrier + sync both sides, max over ranks) and report
+per rank; the shard assignment gives every rank a disjoint buffer range with
+no data-path collective. CPU only."""
+import json
 import os
 import socket
+import subprocess
+import sys
 import time
 
 import pytest
@@ -26,7 +31,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     delay = 0.002 * (rank + 1)          # rank 1 is the slow one
     step = lambda: time.sleep(delay)    # noqa: E731
-    elapsed, per_step = bench.timed_region(step, steps=10, warmup=2, sync=lambda: None, dist=dist)
+    elapsed, per_step, _, _ = bench.timed_region(step, steps=10, warmup=2, sync=lambda: None, dist=dist)
     q.put((rank, elapsed, per_step))
     dist.destroy_process_group()
 
@@ -63,3 +68,50 @@ def test_shards_are_disjoint(config):
 def test_bench_defaults():
     a = bench.parse([])
     assert a.gpus == 1 and a.config == "c2" and a.steps > 0 and a.warmup > 0
+    # N > 1 defaults to the 8-GPU config's shard (C4: 32 Ki x 1 MiB per GPU)
+    a = bench.parse(["--gpus", "8"])
+    assert a.config == "c4" and bench.CONFIGS["c4"]["count"] * 8 == 256 * 1024
+
+
+def _run_bench(*argv, timeout=240):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    return subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), *argv], capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=bench.REPO)
+
+
+def test_launcher_two_ranks_cpu(oracle):
+    """`bench.py --gpus 2` (no WORLD_SIZE) launches 2 ranks itself; the line
+    says n_gpus 2, and each rank checksummed ITS shard (global ids r*64..)."""
+    from photonlibos_amd import datagen
+    r = _run_bench("--gpus", "2", "--cpu-rehearsal", "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout  # rank 0 prints ONE line
+    res = json.loads(line[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["warmup"] == 1 and res["scaling"] == "weak"
+    assert [p["rank"] for p in res["per_rank"]] == [0, 1]
+    for p in res["per_rank"]:
+        want = oracle.crc32c(datagen.stream_bytes(bench.shard_seed_base(p["rank"], 64), 65536))
+        assert p["first_crc"] == want
+        assert len(p["launch_ms"]["first5"]) == 3
+    # whole-job value = both ranks' bytes over the slowest rank's wall time
+    slow = max(p["wall_s"] for p in res["per_rank"])
+    assert res["value"] == pytest.approx(2 * 3 * 64 * 65536 / slow / (1 << 30), rel=0.05)
+
+
+def test_launcher_refuses_missing_gpus():
+    """--gpus 2 with fewer visible GPUs (none here) exits non-zero instead of
+    silently measuring one GPU."""
+    r = _run_bench("--gpus", "2", "--steps", "1", "--warmup", "0", timeout=120)
+    assert r.returncode == 2 and "visible" in r.stderr
+
+
+def test_world_size_must_match_gpus():
+    env_args = ("--gpus", "4", "--cpu-rehearsal", "--steps", "1", "--warmup", "0")
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), *env_args], capture_output=True,
+                       text=True, timeout=120, env=env, cwd=bench.REPO)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
