@@ -233,7 +233,9 @@ int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64
  * pread()s 4 KiB-aligned chunks (so an O_DIRECT fd works: the device reads
  * what the disk DMA'd, the CPU touches no payload byte) into two pinned chunk
  * buffers while the GPU pipeline checksums the previous chunk. Synchronous;
- * -EIO if the file ends before the last record, -errno on a read error. */
+ * -EIO if the file ends before the last record, -errno on a read error.
+ * Concurrent callers each check out their own pinned chunk pair (pairs are
+ * cached for reuse) and share one persistent pool of reader threads. */
 int photon_crc_host_register(void* ptr, uint64_t len);
 int photon_crc_host_unregister(void* ptr);
 int photon_crc32c_file_strided(int fd, uint64_t offset, uint64_t stride, uint64_t nbytes, uint64_t count,

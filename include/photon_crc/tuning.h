@@ -65,6 +65,20 @@ int photon_crc_lanes_for(uint64_t nbytes);
  * this thread return -EIO before enqueuing anything ("injected failure"). */
 void photon_crc_test_fail_next(int n);
 
+/* The constants this library GENERATES (gf2.h), for pinning against the
+ * reference's compiled tables (crc_tables.cpp:104-107, 147-164): which =
+ *   0 host x^(8*2^i)            (= crc32c_lshift_table_sw, 32)
+ *   1 host x^-(8*2^i)           (= crc32c_rshift_table_sw, 32)
+ *   2 host x^(8*2^i - 33)       ([4..31] = crc32c_lshift_table_hw[0..27])
+ *   3 host x^-(8*2^i + 33)      (= crc32c_rshift_table_hw, 32)
+ *   4 device x^(8*2^i)          (combine / fold kernels, 32)
+ *   5 device x^-(8*2^i)         (trim kernel, 32)
+ *   6 device row shifts x^(8*16*G), G = 4..64 (5)
+ *   7 device lane-combine x^(128*2^k) (image of x^0, 6)
+ *   8 host slicing table T[b] (crc.cpp:82-97, 256)
+ * Returns the number of words written to out[n], or a negative error. */
+int photon_crc_test_tables(int which, uint32_t* out, int n);
+
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
  * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),

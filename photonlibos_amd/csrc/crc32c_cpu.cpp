@@ -174,6 +174,20 @@ uint32_t trim_impl(CRC32C_Component all, CRC32C_Component prefix, CRC32C_Compone
 
 }  // namespace
 
+// The host engine's generated constants, for the pinning test (tuning.h
+// photon_crc_test_tables): 0 lsh_sw, 1 rsh_sw, 2 lsh_hw, 3 rsh_hw (32 each),
+// 8 the slicing table slice[0] (256).
+namespace pcrc {
+int host_engine_table(int which, uint32_t* out, int n) {
+    const uint32_t* src = which == 0 ? g_tab.lsh_sw : which == 1 ? g_tab.rsh_sw : which == 2 ? g_tab.lsh_hw
+                        : which == 3 ? g_tab.rsh_hw : which == 8 ? g_tab.slice[0] : nullptr;
+    const int len = which == 8 ? 256 : 32;
+    if (!src || n < len) return -22;
+    for (int i = 0; i < len; ++i) out[i] = src[i];
+    return len;
+}
+}  // namespace pcrc
+
 // ------------------------------------------------------------- exported API
 
 uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t crc) {

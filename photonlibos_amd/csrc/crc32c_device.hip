@@ -55,6 +55,7 @@
 #include "internal.h"
 
 namespace pcrc {
+int host_engine_table(int which, uint32_t* out, int n);  // crc32c_cpu.cpp
 
 // ------------------------------------------------------------------ host side
 namespace {
@@ -144,54 +145,88 @@ int current_device(int* cus) {
     return dev;
 }
 
-// Stream-ordered scratch for multi-kernel calls (segment CRCs between the
-// segment and fold kernels, piece descriptors of one long buffer). It comes
-// from a library-owned pool per device whose memory is reused ONLY in the
-// order of the stream that freed it: opportunistic and event-following
-// cross-stream reuse are off. With HIP's default pool, 16 threads submitting
-// on their own streams read another call's segment CRCs now and then
-// (tests/cpp/concurrency_test.cpp: 2-8 wrong message CRCs in 30 K); with
-// cross-stream reuse off they never do.
-struct ScratchPool {
-    bool ready = false;
-    hipMemPool_t pool = nullptr;
+// Scratch for multi-kernel calls (segment CRCs between the segment and fold
+// kernels, piece descriptors of one long buffer). NOT from HIP's stream-ordered
+// allocator: with 16 threads submitting on their own streams, hipMallocAsync /
+// hipFreeAsync on the default pool handed one call's segment-CRC scratch to
+// another stream now and then (2-8 wrong message CRCs in 30 K,
+// tests/cpp/concurrency_test.cpp), and a private pool with cross-stream reuse
+// off hung the process about one run in four. Instead the library keeps its
+// own device buffers: a call leases a buffer that no other call holds, makes
+// its stream wait for the event recorded after the buffer's previous use
+// (usually complete already: leases prefer such buffers), enqueues its work,
+// records the event again and returns the lease. Reuse across streams is
+// ordered by that event; nothing is freed while work may still use it.
+struct ScratchBuf {
+    int dev;
+    void* p;
+    uint64_t cap;
+    hipEvent_t last;  // recorded after the latest use
+    bool busy;
 };
-std::mutex g_pool_mu;
-ScratchPool g_pools[64];
+std::mutex g_scr_mu;
+std::vector<ScratchBuf*> g_scr;
 
 int scratch_alloc(void** p, uint64_t bytes, hipStream_t st) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-    if (dev < 0 || dev >= 64) return fail(-ENODEV, "device index beyond the scratch-pool table");
-    hipMemPool_t pool;
+    ScratchBuf* lease = nullptr;
+    bool wait = false;
     {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        ScratchPool& sp = g_pools[dev];
-        if (!sp.ready) {
-            hipMemPoolProps props{};
-            props.allocType = hipMemAllocationTypePinned;
-            props.location.type = hipMemLocationTypeDevice;
-            props.location.id = dev;
-            if ((e = hipMemPoolCreate(&sp.pool, &props)) != hipSuccess) return hip_fail(e, "hipMemPoolCreate");
-            int off = 0;
-            uint64_t keep = 64ull << 20;  // keep up to 64 MiB cached between calls
-            if ((e = hipMemPoolSetAttribute(sp.pool, hipMemPoolReuseAllowOpportunistic, &off)) != hipSuccess ||
-                (e = hipMemPoolSetAttribute(sp.pool, hipMemPoolReuseAllowInternalDependencies, &off)) != hipSuccess ||
-                (e = hipMemPoolSetAttribute(sp.pool, hipMemPoolReuseFollowEventDependencies, &off)) != hipSuccess ||
-                (e = hipMemPoolSetAttribute(sp.pool, hipMemPoolAttrReleaseThreshold, &keep)) != hipSuccess)
-                return hip_fail(e, "hipMemPoolSetAttribute");
-            sp.ready = true;
+        std::lock_guard<std::mutex> lk(g_scr_mu);
+        for (ScratchBuf* b : g_scr) {
+            if (b->busy || b->dev != dev || b->cap < bytes) continue;
+            const bool done = hipEventQuery(b->last) == hipSuccess;
+            if (!lease || (done && wait)) {
+                lease = b;
+                wait = !done;
+            }
+            if (done) break;
         }
-        pool = sp.pool;
+        if (lease) lease->busy = true;
     }
-    e = hipMallocFromPoolAsync(p, bytes ? bytes : 1, pool, st);
-    return e == hipSuccess ? 0 : hip_fail(e, "hipMallocFromPoolAsync");
+    if (!lease) {
+        auto* b = new ScratchBuf{dev, nullptr, 0, nullptr, true};
+        uint64_t cap = 1u << 20;
+        while (cap < bytes) cap <<= 1;
+        if ((e = hipMalloc(&b->p, cap)) != hipSuccess) {
+            delete b;
+            return hip_fail(e, "hipMalloc(scratch)");
+        }
+        if ((e = hipEventCreateWithFlags(&b->last, hipEventDisableTiming)) != hipSuccess) {
+            (void)hipFree(b->p);
+            delete b;
+            return hip_fail(e, "hipEventCreate(scratch)");
+        }
+        b->cap = cap;
+        std::lock_guard<std::mutex> lk(g_scr_mu);
+        g_scr.push_back(b);
+        lease = b;
+    } else if (wait && (e = hipStreamWaitEvent(st, lease->last, 0)) != hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_scr_mu);
+        lease->busy = false;
+        return hip_fail(e, "hipStreamWaitEvent(scratch)");
+    }
+    *p = lease->p;
+    return 0;
 }
 
+// Return a lease: its buffer may be reused once the work enqueued on `st`
+// so far has run.
 int scratch_free(void* p, hipStream_t st) {
-    hipError_t e = hipFreeAsync(p, st);
-    return e == hipSuccess ? 0 : hip_fail(e, "hipFreeAsync");
+    ScratchBuf* lease = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_scr_mu);
+        for (ScratchBuf* b : g_scr)
+            if (b->p == p && b->busy) lease = b;
+    }
+    if (!lease) return fail(-EINVAL, "scratch_free of a buffer not leased");
+    const hipError_t e = hipEventRecord(lease->last, st);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord(scratch)");  // stays leased: never reused unordered
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    lease->busy = false;
+    return 0;
 }
 
 // Constants for G lanes per buffer and runs of B blocks per lane per row:
@@ -629,6 +664,30 @@ int photon_crc_lanes_for(uint64_t nbytes) { return choose_lanes(nbytes); }
 
 void photon_crc_test_fail_next(int n) { g_fail_next = n > 0 ? n : 0; }
 
+int photon_crc_test_tables(int which, uint32_t* out, int n) {
+    if (!out) return fail(-EINVAL, "null output");
+    if (which <= 3 || which == 8) {
+        const int rc = host_engine_table(which, out, n);
+        return rc < 0 ? fail(-EINVAL, "bad table id or short output") : rc;
+    }
+    if (n < 32) return fail(-EINVAL, "short output");
+    if (which == 4 || which == 5) {  // device combine / trim powers x^(+-8*2^i)
+        const PowTable& t = which == 4 ? pow_table() : rshift_table();
+        for (int i = 0; i < 32; ++i) out[i] = t.x8pow2[i];
+        return 32;
+    }
+    if (which == 6) {  // batch kernels' row shifts x^(8*16*G), G = 4, 8, 16, 32, 64
+        for (int k = 0; k < 5; ++k) out[k] = lane_consts(4 << k).kshift;
+        return 5;
+    }
+    if (which == 7) {  // lane-combine bases: image of x^0 under x^(128*2^k), k < 6
+        const LaneConsts& c = lane_consts(64);
+        for (int k = 0; k < 6; ++k) out[k] = c.basis[k][31];
+        return 6;
+    }
+    return fail(-EINVAL, "bad table id");
+}
+
 int photon_crc_set_generic_rows(int rows_per_step) {
     if (rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
         return fail(-EINVAL, "rows per step must be 0 (fused kernel), 2, 4 or 8");
@@ -918,11 +977,10 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
     // kernel (few, long messages).
     const int g = lanes ? lanes : choose_lanes(8192);
     const uint64_t gpw = 64 / (uint64_t)g;
-    // (With per-segment CRCs requested the fused form folds with a multiply per
-    // segment on one lane and measured slower than the fold kernel, so it is
-    // automatic only for the seed-chained form.)
+    // (With per-segment CRCs requested the fused form folds with the group-
+    // spread multiply of crc32c_batch_kernel<G, U, true>.)
     const int mode = g_msg_mode.load(std::memory_order_relaxed);
-    const bool fused = mode == 1 || (mode == 0 && !d_seg_out && nmsg >= 4096 * gpw && nseg <= 64 * nmsg);
+    const bool fused = mode == 1 || (mode == 0 && nmsg >= 4096 * gpw && nseg <= 64 * nmsg);
     if (fused) {
         int cus = 0;
         int dev = current_device(&cus);

@@ -8,6 +8,10 @@
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "gf2.h"
 
+#ifndef PCRC_LOOP_UNROLL2
+#define PCRC_LOOP_UNROLL2 0
+#endif
+
 namespace pcrc {
 
 // ------------------------------------------------------------------ LDS map
@@ -287,6 +291,36 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
         }
         // Full rows 1..full-1: U rows per step, the next U in flight.
         uint64_t row = 1;
+#if PCRC_LOOP_UNROLL2
+        // (Variant: two register sets used in turn, the body unrolled by two,
+        // so no register copy sits on the loop edge: 9 % fewer instructions,
+        // measured 2.5 points SLOWER on C2, +0.6 on C3; off by default.)
+        if (row + U <= full) {
+            uint4 cur[U], nxt[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
+            for (;;) {
+                if (row + 2 * U > full) {
+                    pc = lag_column_step<U>(lds, pc, cur, la);
+                    row += U;
+                    break;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+                pc = lag_column_step<U>(lds, pc, cur, la);
+                row += U;
+                if (row + 2 * U > full) {
+                    pc = lag_column_step<U>(lds, pc, nxt, la);
+                    row += U;
+                    break;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + U + u) * (16 * G));
+                pc = lag_column_step<U>(lds, pc, nxt, la);
+                row += U;
+            }
+        }
+#else
         if (row + U <= full) {
             uint4 cur[U];
 #pragma unroll
@@ -302,6 +336,7 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
             pc = lag_column_step<U>(lds, pc, cur, la);
             row += U;
         }
+#endif
         for (; row < full; ++row) pc = sstep(lds, pc, la, lag16(lds, load16(lp + row * (16 * G)), la));
         // Partial last row.
         if (full >= 1 && full < rows && full * G + gl < nb)
@@ -330,10 +365,17 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
 
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     if constexpr (MSG) {
-        // One group per message: its segments one after the other, each CRC
-        // (seed 0) stored, and folded on the first lane: acc = acc*x^(8 len) ^ crc
-        // (crc32c_combine, crc.cpp:393-405), the shift constant reused while
-        // the segment length repeats. No second kernel.
+        // One group per message: its segments one after the other, either
+        // chained through the seed, or each CRC (seed 0) stored and folded:
+        // acc = acc*x^(8 len) ^ crc (crc32c_combine, crc.cpp:393-405). No
+        // second kernel.
+        // Fold basis cache of the per-segment form (see below), kept across
+        // the wave's messages: W register bits per lane.
+        constexpr int kFoldW = G >= 32 ? 1 : G >= 8 ? 32 / G : 1;
+        uint64_t klen = ~0ull;
+        uint32_t kb[kFoldW];
+#pragma unroll
+        for (int w = 0; w < kFoldW; ++w) kb[w] = 0;
         for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.nmsg; wv += nwaves) {
             const uint64_t m = wv * GPW + grp;
             const bool active = m < args.nmsg;
@@ -353,19 +395,59 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                                            seed, gl, la);
                 }
             } else {
-                uint64_t klen = 0;
-                uint32_t k = kOne;
+                // Per-segment CRCs (seed 0) and the fold acc = acc * K ^ c,
+                // K = x^(8 len) (crc32c_combine, crc.cpp:393-405). The multiply
+                // is spread over the group: lane gl holds the images under K of
+                // the register bits gl*W .. gl*W+W-1 (kb, rebuilt only when the
+                // length changes -- once per wave for equal segments), so
+                // acc * K is W select-XORs per lane plus an XOR reduction over
+                // the G lanes, instead of a 32-step bit-serial multiply on one
+                // lane while the others wait.
+                // Segment CRCs are not stored one by one from the first lane
+                // (a 4-byte store per segment sits in the wave's vmcnt queue in
+                // front of the next segment's loads): lane j of the group keeps
+                // the CRC of segment s0 + j (mod G), and the group stores G
+                // consecutive CRCs with one coalesced store.
+                const uint32_t leader = threadIdx.x & 63u & ~(uint32_t)(G - 1);
+                uint32_t pend = 0;
                 for (uint64_t sg = s0; sg < s1; ++sg) {
                     const uint8_t* p = static_cast<const uint8_t*>(args.iov[sg].base);
                     const uint64_t n = args.iov[sg].len;
                     const uint32_t c = buffer_crc<G, U>(lds, p, n, 0u, gl, la);
-                    if (gl == 0) {
-                        args.out[sg] = c;
+                    const uint32_t j = (uint32_t)((sg - s0) & (G - 1));
+                    const uint32_t cb = (uint32_t)__shfl((int)c, (int)leader, 64);
+                    if (gl == j) pend = cb;
+                    if (j == G - 1 || sg + 1 == s1) {
+                        const uint64_t first = sg - j;
+                        if (gl <= j) args.out[first + gl] = pend;
+                    }
+                    if constexpr (G >= 8) {
                         if (n != klen) {
-                            k = xpow8_tab(n, pt);
+                            const uint32_t kn = xpow8_tab(n, pt);
+#pragma unroll
+                            for (int w = 0; w < kFoldW; ++w) {
+                                const uint32_t bit = gl * kFoldW + w;
+                                kb[w] = bit < 32 ? mulmod(1u << bit, kn) : 0u;
+                            }
                             klen = n;
                         }
-                        acc = mulmod(acc, k) ^ c;
+                        const uint32_t a = (uint32_t)__shfl((int)acc, (int)leader, 64);
+                        uint32_t part = 0;
+#pragma unroll
+                        for (int w = 0; w < kFoldW; ++w) part ^= ((a >> (gl * kFoldW + w)) & 1u) ? kb[w] : 0u;
+#pragma unroll
+                        for (int o = G / 2; o > 0; o >>= 1) part ^= (uint32_t)__shfl_xor((int)part, o, 64);
+                        acc = part ^ c;  // valid on the group's first lane, where c is
+                    } else {
+                        // 4-lane groups (segments < 2 KiB): 8 basis words per
+                        // lane would spill; the first lane multiplies.
+                        if (gl == 0) {
+                            if (n != klen) {
+                                kb[0] = xpow8_tab(n, pt);
+                                klen = n;
+                            }
+                            acc = mulmod(acc, kb[0]) ^ c;
+                        }
                     }
                 }
             }

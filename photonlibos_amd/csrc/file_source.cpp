@@ -17,6 +17,9 @@
 #include <unistd.h>
 
 #include <condition_variable>
+#include <deque>
+#include <functional>
+#include <vector>
 #include <map>
 #include <mutex>
 #include <string>
@@ -33,18 +36,121 @@ using pcrc::report_hip_error;
 
 constexpr uint64_t kAlign = 4096;
 constexpr uint64_t kChunk = 64ull << 20;  // payload span per chunk
-constexpr int kReadThreads = 8;           // parallel preads per chunk (page-cache copies are per-core bound)
+constexpr int kReadPieces = 8;            // parallel preads per chunk (page-cache copies are per-core bound)
+constexpr int kReaderThreads = 16;        // persistent reader pool, shared by concurrent callers
+constexpr int kKeepPairs = 4;             // chunk-buffer pairs kept pinned between calls
 
-struct ChunkBufs {
-    std::mutex mu;
+// A pair of pinned chunk buffers, owned by ONE call at a time: concurrent
+// callers check out their own pair (pinned allocation is slow, so pairs are
+// kept for reuse), so they no longer serialise on one global pair.
+struct ChunkPair {
     void* buf[2] = {nullptr, nullptr};
     uint64_t cap = 0;
 };
 
-ChunkBufs& chunk_bufs() {
-    static ChunkBufs* c = new ChunkBufs;
+struct PairCache {
+    std::mutex mu;
+    std::vector<ChunkPair> free;
+};
+
+PairCache& pair_cache() {
+    static PairCache* c = new PairCache;
     return *c;
 }
+
+void free_pair(ChunkPair& p) {
+    for (void*& b : p.buf)
+        if (b) {
+            (void)hipHostFree(b);
+            b = nullptr;
+        }
+    p.cap = 0;
+}
+
+int checkout_pair(uint64_t cap, ChunkPair* out) {
+    {
+        PairCache& c = pair_cache();
+        std::lock_guard<std::mutex> lk(c.mu);
+        for (size_t i = 0; i < c.free.size(); ++i)
+            if (c.free[i].cap >= cap) {
+                *out = c.free[i];
+                c.free.erase(c.free.begin() + i);
+                return 0;
+            }
+    }
+    ChunkPair p;
+    for (void*& b : p.buf) {
+        hipError_t e = hipHostMalloc(&b, cap, hipHostMallocPortable);
+        if (e != hipSuccess) {
+            free_pair(p);
+            return report_hip_error(e, "hipHostMalloc(chunk)");
+        }
+    }
+    p.cap = cap;
+    *out = p;
+    return 0;
+}
+
+void return_pair(ChunkPair p) {
+    PairCache& c = pair_cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.free.push_back(p);
+    if ((int)c.free.size() > kKeepPairs) {  // drop the smallest
+        size_t k = 0;
+        for (size_t i = 1; i < c.free.size(); ++i)
+            if (c.free[i].cap < c.free[k].cap) k = i;
+        free_pair(c.free[k]);
+        c.free.erase(c.free.begin() + k);
+    }
+}
+
+// Persistent reader threads (created on first use) running pread pieces for
+// every caller: no thread start-up per chunk.
+class ReaderPool {
+public:
+    static ReaderPool& get() {
+        static ReaderPool* p = new ReaderPool;  // never destroyed: workers outlive static destruction
+        return *p;
+    }
+    // Run every task on the pool and wait for all of them.
+    void run_all(std::vector<std::function<void()>>& tasks) {
+        std::mutex done_mu;
+        std::condition_variable done_cv;
+        size_t left = tasks.size();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (auto& t : tasks)
+                q_.push_back([&t, &done_mu, &done_cv, &left] {
+                    t();
+                    std::lock_guard<std::mutex> g(done_mu);
+                    if (--left == 0) done_cv.notify_all();
+                });
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> g(done_mu);
+        done_cv.wait(g, [&] { return left == 0; });
+    }
+
+private:
+    ReaderPool() {
+        for (int i = 0; i < kReaderThreads; ++i)
+            std::thread([this] {
+                for (;;) {
+                    std::function<void()> job;
+                    {
+                        std::unique_lock<std::mutex> lk(mu_);
+                        cv_.wait(lk, [&] { return !q_.empty(); });
+                        job = std::move(q_.front());
+                        q_.pop_front();
+                    }
+                    job();
+                }
+            }).detach();
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+};
 
 // Read [off, off+want_max) of fd into dst, accepting a short read at end of
 // file once at least want_min bytes are in (the 4 KiB-rounded tail of the
@@ -68,30 +174,29 @@ int read_span(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_max, uint64
     return 0;
 }
 
-// read_span over kReadThreads 4 KiB-aligned pieces in parallel; only the last
-// piece may end short (at EOF).
+// read_span over kReadPieces 4 KiB-aligned pieces in parallel on the reader
+// pool; only the last piece may end short (at EOF).
 int read_span_parallel(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_max, uint64_t off, std::string* err) {
-    const uint64_t piece = ((want_max / kReadThreads) + kAlign - 1) & ~(kAlign - 1);
-    if (want_max < 4 * kAlign * kReadThreads || piece == 0) return read_span(fd, dst, want_min, want_max, off, err);
-    int rcs[kReadThreads] = {};
-    std::string errs[kReadThreads];
-    std::thread th[kReadThreads];
+    const uint64_t piece = ((want_max / kReadPieces) + kAlign - 1) & ~(kAlign - 1);
+    if (want_max < 4 * kAlign * kReadPieces || piece == 0) return read_span(fd, dst, want_min, want_max, off, err);
+    int rcs[kReadPieces + 1] = {};
+    std::string errs[kReadPieces + 1];
+    std::vector<std::function<void()>> tasks;
     int used = 0;
     for (uint64_t lo = 0; lo < want_max; lo += piece, ++used) {
         const uint64_t hi = lo + piece < want_max ? lo + piece : want_max;
         const bool last = hi == want_max;
         const uint64_t need = last ? (want_min > lo ? want_min - lo : 0) : hi - lo;
-        th[used] = std::thread([=, &rcs, &errs] { rcs[used] = read_span(fd, dst + lo, need, hi - lo, off + lo, &errs[used]); });
+        const int k = used;
+        tasks.push_back([=, &rcs, &errs] { rcs[k] = read_span(fd, dst + lo, need, hi - lo, off + lo, &errs[k]); });
     }
-    int rc = 0;
-    for (int i = 0; i < used; ++i) {
-        th[i].join();
-        if (rcs[i] && !rc) {
-            rc = rcs[i];
+    ReaderPool::get().run_all(tasks);
+    for (int i = 0; i < used; ++i)
+        if (rcs[i]) {
             *err = errs[i];
+            return rcs[i];
         }
-    }
-    return rc;
+    return 0;
 }
 
 }  // namespace
@@ -190,21 +295,12 @@ int photon_crc32c_file_strided(int fd, uint64_t offset, uint64_t stride, uint64_
     if (per == 0) per = 1;
     if (per > count) per = count;
     const uint64_t span_max = (per - 1) * stride + nbytes + 2 * kAlign;
-    ChunkBufs& cb = chunk_bufs();
-    std::lock_guard<std::mutex> lk(cb.mu);
-    if (cb.cap < span_max) {
-        for (void*& b : cb.buf)
-            if (b) {
-                (void)hipHostFree(b);
-                b = nullptr;
-            }
-        cb.cap = 0;
-        for (void*& b : cb.buf) {
-            hipError_t e = hipHostMalloc(&b, span_max, hipHostMallocPortable);
-            if (e != hipSuccess) return report_hip_error(e, "hipHostMalloc(chunk)");
-        }
-        cb.cap = span_max;
-    }
+    ChunkPair cb;
+    if (int prc = checkout_pair(span_max, &cb)) return prc;
+    struct Return {
+        ChunkPair& p;
+        ~Return() { return_pair(p); }
+    } give_back{cb};
 
     const uint64_t nchunks = (count + per - 1) / per;
     std::mutex mu;

@@ -9,6 +9,8 @@
 #   scripts/gpu.sh pmc CONFIG            rocprofv3 --pmc FETCH_SIZE pass (counters only)
 #   scripts/gpu.sh sq CONFIG             SQ/GRBM counter passes (scripts/pmc_kernel.sh)
 #   scripts/gpu.sh probe SCRIPT [ARGS]   python scripts/SCRIPT ARGS (bench-only probes)
+#   scripts/gpu.sh ab LIB ROUNDS CONFIG.. A/B of another build of the library (PHOTON_CRC_LIB=LIB)
+#                                        against the in-tree one, alternating, fresh process each
 # Several commands chain with "::", e.g.
 #   scripts/gpu.sh tests :: bench --steps 20 --warmup 5 :: prof c2
 set -o pipefail
@@ -49,6 +51,18 @@ run_one() {
       timeout -k 10 600 python -u scripts/$s "$@" > $O/probe_${s%.py}_$n.jsonl 2> $O/probe_${s%.py}_$n.err \
         || { echo "probe $s failed"; tail -20 $O/probe_${s%.py}_$n.err; return 1; }
       cut -c1-300 $O/probe_${s%.py}_$n.jsonl ;;
+    ab)
+      local lib=$1 rounds=$2; shift 2
+      for r in $(seq 1 $rounds); do
+        for c in "$@"; do
+          for side in new old; do
+            local envv=""; [ $side = old ] && envv="PHOTON_CRC_LIB=$lib"
+            env $envv timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-live-pmc --no-shape64 \
+              > $O/ab_tmp.json 2>> $O/ab.err || { echo "ab $c $side failed"; tail -5 $O/ab.err; return 1; }
+            python -c "import json,sys; d=json.loads(open('$O/ab_tmp.json').read().splitlines()[-1]); r=d['roofline']; print(json.dumps({'round': $r, 'config': '$c', 'side': '$side', 'value': d['value'], 'frac_kernel': r['frac_kernel'], 'frac_steady': r['frac_steady_median_launch'], 'ok': d['self_check']}))" | tee -a $O/ab.jsonl
+          done
+        done
+      done ;;
     *) echo "unknown command $cmd"; return 1 ;;
   esac
 }

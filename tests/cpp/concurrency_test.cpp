@@ -10,6 +10,7 @@
 // CRC-64 streaming shape). Every result is checked against the ORACLE
 // (oracle/lib/libcrc_oracle.so, the plain-C restatement pinned to the
 // reference). Built with plain g++ (no HIP headers). Exit 0 = all bit-exact.
+#include <photon_crc/checked_batch.h>
 #include <photon_crc/crc32c_gpu.h>
 #include <photon_crc/tuning.h>
 
@@ -78,6 +79,21 @@ struct Res {
 };
 Res g_res[kThreads];
 
+// A pinned host array from the library's IOAlloc pool (checked_batch.h).
+template <typename T>
+struct Pinned {
+    T* p = nullptr;
+    explicit Pinned(size_t n) {
+        void* q = nullptr;
+        const int bytes = (int)(n * sizeof(T));
+        if (photon_crc_pinned_allocate(nullptr, photon_crc_range{bytes, bytes}, &q) >= 0) p = static_cast<T*>(q);
+    }
+    ~Pinned() {
+        if (p) photon_crc_pinned_deallocate(nullptr, p);
+    }
+    T& operator[](size_t i) { return p[i]; }
+};
+
 #undef RET
 #define RET -1
 int setup(int t) {
@@ -111,9 +127,19 @@ void submitter(int t) {
     void *stream = r.stream, *d_buf = r.d_buf, *d_iov = r.d_iov, *d_seeds = r.d_seeds, *d_out = r.d_out,
          *d_start = r.d_start, *d_seg = r.d_seg, *d_a = r.d_a, *d_b = r.d_b, *d_len = r.d_len;
     Where& w = g_where[t];
+    // Host sides of every copy are pinned (IOAlloc pool of the library), as an
+    // asynchronous Photon caller's buffers would be.
+    Pinned<uint8_t> host(kBuf);
+    Pinned<photon_crc_iovec> iov(kMaxItems);
+    Pinned<uint32_t> seeds(kMaxItems), out(kMaxItems), segs(kMaxItems), a(kMaxItems), b(kMaxItems), len(kMaxItems);
+    Pinned<uint64_t> out64(kMaxItems), start(kMaxItems + 1);
+    if (!host.p || !iov.p || !seeds.p || !out.p || !segs.p || !a.p || !b.p || !len.p || !out64.p || !start.p) {
+        fprintf(stderr, "thread %d: pinned allocation failed: %s\n", t, photon_crc_last_error());
+        g_err.fetch_add(1);
+        return;
+    }
     TRY(photon_crc_util_fill_splitmix(d_buf, kBuf, kBuf, 1, 0x7000 + t, stream));
-    std::vector<uint8_t> host(kBuf);
-    TRY(photon_crc_memcpy_async(host.data(), d_buf, kBuf, stream));
+    TRY(photon_crc_memcpy_async(host.p, d_buf, kBuf, stream));
     TRY(photon_crc_stream_sync(stream));
     const uint8_t* dbase = static_cast<const uint8_t*>(d_buf);
     const uint64_t lens[] = {0, 1, 15, 100, 4096, 4097, 8192, 65536, 200000};
@@ -130,67 +156,63 @@ void submitter(int t) {
             const uint64_t count = std::min<uint64_t>(kMaxItems, stride ? (kBuf - n) / stride : kMaxItems);
             const uint32_t seed = (uint32_t)rng();
             p0 = n, p1 = stride, p2 = count;
-            std::vector<uint32_t> out(count);
             TRY(photon_crc32c_batch_strided(dbase, stride, n, count, seed, nullptr, static_cast<uint32_t*>(d_out),
                                             stream));
-            TRY(photon_crc_memcpy_async(out.data(), d_out, count * 4, stream));
+            TRY(photon_crc_memcpy_async(out.p, d_out, count * 4, stream));
             w.phase = 2;
             TRY(photon_crc_stream_sync(stream));
             w.phase = 3;
-            for (uint64_t i = 0; i < count; ++i) check(out[i] == or_crc32c_sw(host.data() + i * stride, n, seed));
+            for (uint64_t i = 0; i < count; ++i) check(out[i] == or_crc32c_sw(host.p + i * stride, n, seed));
         } else if (kind == 1) {  // ragged iovec batch with per-buffer seeds
             const int count = 1 + (int)(rng() % kMaxItems);
-            std::vector<photon_crc_iovec> iov(count);
-            std::vector<uint32_t> seeds(count), out(count);
             for (int i = 0; i < count; ++i) {
                 const uint64_t n = rng() % 70000, off = rng() % (kBuf - n);
                 iov[i] = {dbase + off, n};
                 seeds[i] = (uint32_t)rng();
             }
-            TRY(photon_crc_memcpy_async(d_iov, iov.data(), count * 16, stream));
-            TRY(photon_crc_memcpy_async(d_seeds, seeds.data(), count * 4, stream));
+            TRY(photon_crc_memcpy_async(d_iov, iov.p, count * 16, stream));
+            TRY(photon_crc_memcpy_async(d_seeds, seeds.p, count * 4, stream));
             TRY(photon_crc32c_batch_iov(static_cast<const photon_crc_iovec*>(d_iov), count, 0,
                                         static_cast<const uint32_t*>(d_seeds), static_cast<uint32_t*>(d_out), stream));
-            TRY(photon_crc_memcpy_async(out.data(), d_out, count * 4, stream));
+            TRY(photon_crc_memcpy_async(out.p, d_out, count * 4, stream));
             w.phase = 2;
             TRY(photon_crc_stream_sync(stream));
             w.phase = 3;
             for (int i = 0; i < count; ++i) {
-                const uint8_t* h = host.data() + (static_cast<const uint8_t*>(iov[i].base) - dbase);
+                const uint8_t* h = host.p + (static_cast<const uint8_t*>(iov[i].base) - dbase);
                 p0 = iov[i].len, p1 = (uintptr_t)iov[i].base & 15, p2 = count;
                 check(out[i] == or_crc32c_sw(h, iov[i].len, seeds[i]));
             }
         } else if (kind == 2) {  // messages of segments, chained; optionally with segment CRCs
             const int nmsg = 1 + (int)(rng() % 8);
-            std::vector<photon_crc_iovec> iov;
-            std::vector<uint64_t> start{0};
+            uint64_t nseg = 0;
+            start[0] = 0;
             for (int m = 0; m < nmsg; ++m) {
-                const int nseg = (int)(rng() % 8);
-                for (int j = 0; j < nseg; ++j) {
+                const int k = (int)(rng() % 8);
+                for (int j = 0; j < k; ++j) {
                     const uint64_t n = rng() % 20000, off = rng() % (kBuf - n);
-                    iov.push_back({dbase + off, n});
+                    iov[nseg++] = {dbase + off, n};
                 }
-                start.push_back(iov.size());
+                start[m + 1] = nseg;
             }
             const bool seg = rng() & 1;
             const uint32_t seed = (uint32_t)rng();
-            std::vector<uint32_t> out(nmsg), segs(iov.size() + 1);
-            if (!iov.empty()) TRY(photon_crc_memcpy_async(d_iov, iov.data(), iov.size() * 16, stream));
-            TRY(photon_crc_memcpy_async(d_start, start.data(), start.size() * 8, stream));
+            if (nseg) TRY(photon_crc_memcpy_async(d_iov, iov.p, nseg * 16, stream));
+            TRY(photon_crc_memcpy_async(d_start, start.p, (nmsg + 1) * 8, stream));
             TRY(photon_crc32c_batch_msg_n(static_cast<const photon_crc_iovec*>(d_iov),
-                                          static_cast<const uint64_t*>(d_start), nmsg, iov.size(), seed, nullptr,
+                                          static_cast<const uint64_t*>(d_start), nmsg, nseg, seed, nullptr,
                                           seg ? static_cast<uint32_t*>(d_seg) : nullptr,
                                           static_cast<uint32_t*>(d_out), stream));
-            TRY(photon_crc_memcpy_async(out.data(), d_out, nmsg * 4, stream));
-            if (seg && !iov.empty()) TRY(photon_crc_memcpy_async(segs.data(), d_seg, iov.size() * 4, stream));
+            TRY(photon_crc_memcpy_async(out.p, d_out, nmsg * 4, stream));
+            if (seg && nseg) TRY(photon_crc_memcpy_async(segs.p, d_seg, nseg * 4, stream));
             w.phase = 2;
             TRY(photon_crc_stream_sync(stream));
             w.phase = 3;
-            p0 = nmsg, p1 = iov.size(), p2 = seg;
+            p0 = nmsg, p1 = nseg, p2 = seg;
             for (int m = 0; m < nmsg; ++m) {
                 uint32_t acc = seed;
                 for (uint64_t j = start[m]; j < start[m + 1]; ++j) {
-                    const uint8_t* h = host.data() + (static_cast<const uint8_t*>(iov[j].base) - dbase);
+                    const uint8_t* h = host.p + (static_cast<const uint8_t*>(iov[j].base) - dbase);
                     if (seg) check(segs[j] == or_crc32c_sw(h, iov[j].len, 0));
                     acc = or_crc32c_sw(h, iov[j].len, acc);
                 }
@@ -200,29 +222,27 @@ void submitter(int t) {
             const uint64_t n = lens[1 + rng() % 8], count = std::min<uint64_t>(kMaxItems, (kBuf - n) / n);
             const uint64_t seed = rng();
             p0 = n, p1 = count;
-            std::vector<uint64_t> out(count);
             TRY(photon_crc64ecma_batch_strided(dbase, n, n, count, seed, nullptr, static_cast<uint64_t*>(d_out),
                                                stream));
-            TRY(photon_crc_memcpy_async(out.data(), d_out, count * 8, stream));
+            TRY(photon_crc_memcpy_async(out64.p, d_out, count * 8, stream));
             w.phase = 2;
             TRY(photon_crc_stream_sync(stream));
             w.phase = 3;
-            for (uint64_t i = 0; i < count; ++i) check(out[i] == or_crc64ecma_sw(host.data() + i * n, n, seed));
+            for (uint64_t i = 0; i < count; ++i) check(out64[i] == or_crc64ecma_sw(host.p + i * n, n, seed));
         } else {  // combine batch (with the reference's shortcuts: crc1 == 0, len2 == 0)
             const int count = kMaxItems;
-            std::vector<uint32_t> a(count), b(count), len(count), out(count);
             for (int i = 0; i < count; ++i) {
                 a[i] = i % 7 == 0 ? 0 : (uint32_t)rng();
                 b[i] = (uint32_t)rng();
                 len[i] = i % 5 == 0 ? 0 : (uint32_t)rng();
             }
-            TRY(photon_crc_memcpy_async(d_a, a.data(), count * 4, stream));
-            TRY(photon_crc_memcpy_async(d_b, b.data(), count * 4, stream));
-            TRY(photon_crc_memcpy_async(d_len, len.data(), count * 4, stream));
+            TRY(photon_crc_memcpy_async(d_a, a.p, count * 4, stream));
+            TRY(photon_crc_memcpy_async(d_b, b.p, count * 4, stream));
+            TRY(photon_crc_memcpy_async(d_len, len.p, count * 4, stream));
             TRY(photon_crc32c_combine_batch(static_cast<const uint32_t*>(d_a), static_cast<const uint32_t*>(d_b),
                                             static_cast<const uint32_t*>(d_len), count, static_cast<uint32_t*>(d_out),
                                             stream));
-            TRY(photon_crc_memcpy_async(out.data(), d_out, count * 4, stream));
+            TRY(photon_crc_memcpy_async(out.p, d_out, count * 4, stream));
             w.phase = 2;
             TRY(photon_crc_stream_sync(stream));
             w.phase = 3;

@@ -176,3 +176,49 @@ def test_segment_past_its_allocation_is_refused(torch_dev):
         b.close()
     finally:
         lib().photon_crc_device_free(p.value)
+
+
+def _cm_fixture():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "checked_message.json")) as f:
+        return json.load(f)["messages"]
+
+
+@pytest.mark.parametrize("flags", [0, 2])
+def test_batch_matches_reference_checked_message(torch_dev, flags):
+    """The device batch against the REFERENCE's own CheckedMessage template
+    (serialize.h:239-279 run by oracle/ref/checked_message_fixtures.cpp):
+    every checksum add_checksum stored, every validate_checksum verdict."""
+    from photonlibos_amd import datagen
+    msgs = _cm_fixture()
+    alloc = PinnedAlloc()
+    blocks, specs = [], []
+    for m in msgs:
+        segs = []
+        for seed, n, off in m["segs"]:
+            a = alloc.alloc(n + off + 1)
+            blocks.append(a)
+            alloc.view(a + off, n)[:] = datagen.stream_bytes(seed, n) if n else []
+            segs.append((a + off, n))
+        b = alloc.alloc(m["body"][1])
+        blocks.append(b)
+        v = alloc.view(b, m["body"][1])
+        v[:] = datagen.stream_bytes(*m["body"])
+        v[-4:] = 0
+        specs.append((segs, (b, m["body"][1])))
+    for claim in ("right", "bad"):
+        batch = MessageBatch(len(msgs), 2048, flags)
+        for k, (m, (segs, body)) in enumerate(zip(msgs, specs)):
+            c = m["checksum"] if claim == "right" else m["checksum"] ^ (1 << (k % 32))
+            batch.add(segs, body, c)
+        batch.submit()
+        nbad = batch.wait()
+        for k, m in enumerate(msgs):
+            valid, crc = batch.result(k)
+            assert crc == m["checksum"], k
+            assert valid == (m["validate"] if claim == "right" else m["validate_bad_claim"]), (k, claim)
+        assert nbad == (0 if claim == "right" else len(msgs))
+        batch.close()
+    for a in blocks:
+        alloc.dealloc(a)

@@ -123,3 +123,34 @@ def test_registered_segment_past_registration_refused(torch_dev):
         b.close()
     finally:
         ck.host_unregister(base)
+
+
+def test_concurrent_file_callers(torch_dev, oracle, data_file):
+    """Concurrent photon_crc32c_file_strided callers (different records of the
+    same file, different fds) each get their own pinned chunk buffers and
+    share the persistent reader pool: both results bit-exact."""
+    import threading
+    path, blob = data_file
+    shapes = [(0, 4096, 4096, 8192), (4096 * 3 + 1, 65536, 65000, 700)]
+    res = [None, None]
+    errs = []
+
+    def run(k):
+        off, stride, n, cnt = shapes[k]
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            res[k] = ck.file_strided(fd, off, stride, n, cnt, seed=k)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+        finally:
+            os.close(fd)
+    for _ in range(3):
+        th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        for k, (off, stride, n, cnt) in enumerate(shapes):
+            for i in list(range(0, cnt, max(1, cnt // 40))) + [cnt - 1]:
+                assert res[k][i] == oracle.crc32c(blob[off + i * stride: off + i * stride + n], k), (k, i)

@@ -130,3 +130,24 @@ def test_gf2_identities(oracle):
     assert oracle.pow32(8) == 0x00800000 and oracle.pow32(16) == 0x00008000 and oracle.pow32(32) == 0x82F63B78
     for n in (1, 7, 33, 1000, 123456789):
         assert oracle.clmul_modp32(oracle.pow32(n), oracle.ipow32(n)) == 0x80000000
+
+
+def _cm_fixture():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "checked_message.json")) as f:
+        return json.load(f)["messages"]
+
+
+def test_extend_chain_equals_reference_checked_message(oracle):
+    """The oracle's Crc32Hasher restatement (extend_chain) against the
+    reference's own CheckedMessage template (tests/golden/checked_message.json,
+    serialize.h:239-279 compiled over Photon's crc.cpp and over the drop-in)."""
+    msgs = _cm_fixture()
+    assert len(msgs) == 160 and all(m["validate"] and not m["validate_bad_claim"] for m in msgs)
+    assert any(len(m["segs"]) == 0 for m in msgs) and any(s[1] == 0 for m in msgs for s in m["segs"])
+    for m in msgs:
+        data = [datagen.stream_bytes(seed, n).tobytes() for seed, n, _ in m["segs"]]
+        body = bytearray(datagen.stream_bytes(m["body"][0], m["body"][1]).tobytes())
+        body[-4:] = b"\0\0\0\0"
+        assert oracle.extend_chain(data + [bytes(body)], 0) == m["checksum"]
