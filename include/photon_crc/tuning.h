@@ -25,7 +25,8 @@ int photon_crc_set_lanes_per_buffer(int g);
 
 /* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
  * lane run B, rows per step U and steps in flight D, one of (1,4,3), (2,2,3),
- * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4).
+ * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4), (1,4,1),
+ * (1,4,2), (1,2,2), (1,2,3); B = 1 uses lagged blocks (16 lookups per 16 B).
  * The streaming kernel is OFF by default (the generic kernel is faster with
  * the current tables); run_blocks = 0 turns it off again. */
 int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);

@@ -538,13 +538,17 @@ bool launch_uniform_g(const UniformArgs& a, dim3 grid, hipStream_t stream, int b
     else if (b == 1 && u == 6 && d == 2) launch_uniform_t<G, 1, 6, 2>(a, grid, stream);
     else if (b == 1 && u == 8 && d == 2) launch_uniform_t<G, 1, 8, 2>(a, grid, stream);
     else if (b == 1 && u == 4 && d == 4) launch_uniform_t<G, 1, 4, 4>(a, grid, stream);
+    else if (b == 1 && u == 4 && d == 1) launch_uniform_t<G, 1, 4, 1>(a, grid, stream);
+    else if (b == 1 && u == 4 && d == 2) launch_uniform_t<G, 1, 4, 2>(a, grid, stream);
+    else if (b == 1 && u == 2 && d == 2) launch_uniform_t<G, 1, 2, 2>(a, grid, stream);
+    else if (b == 1 && u == 2 && d == 3) launch_uniform_t<G, 1, 2, 3>(a, grid, stream);
     else return false;
     return true;
 }
 
 bool stream_shape_ok(int b, int u, int d) {
     return (b == 2 && u == 2 && (d == 3 || d == 4)) ||
-           (b == 1 && ((u == 4 && (d == 3 || d == 4)) || (u == 2 && d == 4) || (u == 8 && (d == 1 || d == 2)) ||
+           (b == 1 && ((u == 4 && d >= 1 && d <= 4) || (u == 2 && d >= 2 && d <= 4) || (u == 8 && (d == 1 || d == 2)) ||
                        (u == 6 && d == 2))) ||
            (b == 4 && u == 1 && (d == 3 || d == 4));
 }

@@ -11,6 +11,9 @@
 #ifndef PCRC_LOOP_UNROLL2
 #define PCRC_LOOP_UNROLL2 0
 #endif
+#ifndef PCRC_LANE_SEL
+#define PCRC_LANE_SEL 1  // per-lane v_perm selectors instead of rotating the word (+0.3 % on C2)
+#endif
 
 namespace pcrc {
 
@@ -72,6 +75,7 @@ struct LaneAddr {
     uint32_t rot;      // 8*q
     uint32_t off[4];
     uint32_t r4;       // r*4 (byte-serial tail)
+    uint32_t sel[4];   // v_perm selector of lookup i: {off.byte0, x.byte((i+q)%4), 0, 0}
 };
 
 __device__ __forceinline__ uint32_t rot32(uint32_t x, const LaneAddr& a) {
@@ -82,10 +86,20 @@ __device__ __forceinline__ uint32_t rot32(uint32_t x, const LaneAddr& a) {
 // v_perm_b32 (result bytes {off.byte0, xr.byte i, 0, 0}; selector 0..3 = the
 // second operand's bytes, 4..7 = the first's, 12 = 0x00); TOFF selects the
 // D (0) or S (kSOff) half of the row through the instruction's offset field.
+#if PCRC_LANE_SEL
+// Per-lane selectors: the v_perm of lookup i takes byte (i+q)%4 of the
+// UNROTATED word (the selector is a per-lane register), so no v_alignbit per
+// table step; one VALU per lookup either way.
+template <int I, uint32_t TOFF>
+__device__ __forceinline__ uint32_t look(const uint32_t* lds, uint32_t x, const LaneAddr& a) {
+    return lds_word(lds, __builtin_amdgcn_perm(x, a.off[I], a.sel[I]) + TOFF);
+}
+#else
 template <int I, uint32_t TOFF>
 __device__ __forceinline__ uint32_t look(const uint32_t* lds, uint32_t xr, const LaneAddr& a) {
     return lds_word(lds, __builtin_amdgcn_perm(xr, a.off[I], 0x0C0C0000u | ((4u + I) << 8)) + TOFF);
 }
+#endif
 
 // a ^ b ^ c in ONE instruction (gfx950 v_bitop3_b32, truth table 0x96).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -95,14 +109,14 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // x * x^32 mod P (the CRC register after absorbing the 32-bit word x), XORed
 // with e (the next data word, or 0).
 __device__ __forceinline__ uint32_t dstep(const uint32_t* lds, uint32_t x, const LaneAddr& a, uint32_t e = 0) {
-    const uint32_t xr = rot32(x, a);
+    const uint32_t xr = PCRC_LANE_SEL ? x : rot32(x, a);
     return xor3(xor3(look<0, 0>(lds, xr, a), look<1, 0>(lds, xr, a), look<2, 0>(lds, xr, a)),
                 look<3, 0>(lds, xr, a), e);
 }
 
 // P * x^(8*16*G) mod P through the S tables, XORed with e.
 __device__ __forceinline__ uint32_t sstep(const uint32_t* lds, uint32_t p, const LaneAddr& a, uint32_t e = 0) {
-    const uint32_t pr = rot32(p, a);
+    const uint32_t pr = PCRC_LANE_SEL ? p : rot32(p, a);
     return xor3(xor3(look<0, kSOff>(lds, pr, a), look<1, kSOff>(lds, pr, a), look<2, kSOff>(lds, pr, a)),
                 look<3, kSOff>(lds, pr, a), e);
 }
@@ -211,6 +225,8 @@ __device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
     la.rot = 8u * q;
 #pragma unroll
     for (int i = 0; i < 4; ++i) la.off[i] = (((i + q) & 3u) << 5) | (r << 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) la.sel[i] = 0x0C0C0000u | ((4u + ((i + q) & 3u)) << 8);
     la.r4 = r << 2;
     return la;
 }
@@ -900,6 +916,8 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
                 } else if constexpr (ABL & 2) {
                     const uint4 w = ring[d][u][0];
                     c[u] = dstep(lds, w.x ^ w.y ^ w.z ^ w.w, la);
+                } else if constexpr (B == 1) {
+                    c[u] = lag16(lds, ring[d][u][0], la);  // lagged blocks: 16 lookups per 16 B
                 } else {
                     c[u] = run_crc<B>(lds, ring[d][u], la);
                 }
@@ -911,6 +929,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_uniform_kernel(UniformArgs args
             }
             if (++step == spb) {
                 // End of this buffer: this lane's last run is G-1-run runs from the end.
+                if constexpr (B == 1 && ABL == 0) pc = dstep(lds, pc, la);  // Q -> P (lagged)
                 const uint32_t crc = group_reduce<G>(pc, (uint32_t)(G - 1 - run), lds);
                 const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
                 if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = crc;

@@ -25,4 +25,7 @@ for d in sys.argv[1:]:
         print(f"{d}: {k}: cycles/XCD {cyc:.4g}  LDS busy {v['SQ_LDS_IDX_ACTIVE'] / 256 / cyc:.2f}  "
               f"bank-conflict {v['SQ_LDS_BANK_CONFLICT'] / 256 / cyc:.3f}  "
               f"VALU issue {v['SQ_INSTS_VALU'] / 1024 * 2 / cyc:.2f}  "
-              f"VALU/LDS instr {v['SQ_INSTS_VALU'] / v['SQ_INSTS_LDS']:.2f}")
+              f"VALU/LDS instr {v['SQ_INSTS_VALU'] / v['SQ_INSTS_LDS']:.2f}  "
+              f"per KiB of a 4 GiB launch: VALU {v['SQ_INSTS_VALU'] / 4194304:.1f} LDS {v['SQ_INSTS_LDS'] / 4194304:.1f} "
+              f"wave-cycles {v['SQ_WAVE_CYCLES'] / 4194304:.0f} wait-any {v['SQ_WAIT_ANY'] / 4194304:.0f} "
+              f"clock {cyc / (v.get('_dur_ns', 0) or 1):.2f}")

@@ -44,7 +44,8 @@ MSG_MODES = [0, 1, 2]
 VARIANTS = [4, 0]
 
 
-STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (0, 0, 0)]
+STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (1, 4, 1), (1, 4, 2), (1, 2, 2),
+                 (1, 2, 3), (1, 8, 1), (1, 8, 2), (1, 6, 2), (1, 4, 4), (0, 0, 0)]
 
 
 def to_dev(torch, arr):
