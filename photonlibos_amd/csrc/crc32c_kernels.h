@@ -8,9 +8,6 @@
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "gf2.h"
 
-#ifndef PCRC_LOOP_UNROLL2
-#define PCRC_LOOP_UNROLL2 0
-#endif
 #ifndef PCRC_LANE_SEL
 #define PCRC_LANE_SEL 1  // per-lane v_perm selectors instead of rotating the word (+0.3 % on C2)
 #endif
@@ -269,102 +266,131 @@ __device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
 
 // -------------------------------------------------------------- generic path
 // Any pointer, any length, any seed; one group of G lanes per buffer.
-// U rows per step per lane, the next U rows' loads in flight.
-// CRC-32C of one buffer (seed applied) by a group of G lanes; the result is
-// valid on the group's first lane (gl == 0).
+// U rows per step per lane, the next U rows' loads in flight. A buffer runs in
+// three parts: geometry + preload (row 0 and the first U rows issued
+// together), body (every row: the lane's lagged column partial), finish
+// (Q -> P, lane combine, ragged tail).
+struct BufGeo {
+    const uint8_t* lp;  // this lane's block in row 0
+    const uint8_t* eb;  // end of the last whole 16-byte block
+    const uint8_t* e;   // end of the buffer
+    uint64_t nb;        // 16-byte blocks from the aligned start
+    uint64_t full;      // rows where every lane has a block
+    uint64_t rows;
+    uint32_t rlast;     // blocks in the last row, 1..G
+    int s0;             // offset of the data start in block 0
+    bool tiny;          // < 64 bytes: byte-serial on the group's first lane
+};
+
+template <int G>
+__device__ __forceinline__ BufGeo buf_geo(const uint8_t* p, uint64_t n, uint32_t gl) {
+    BufGeo g;
+    g.tiny = n < 64;
+    const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+    g.e = p + n;
+    g.eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(g.e) & ~uintptr_t(15));
+    g.s0 = (int)(p - a0);
+    g.nb = g.tiny ? 0 : (uint64_t)(g.eb - a0) >> 4;  // >= 3 blocks when n >= 64
+    g.full = g.nb / G;
+    g.rows = (g.nb + G - 1) / G;
+    g.rlast = (uint32_t)(g.nb - (g.rows ? g.rows - 1 : 0) * G);
+    g.lp = a0 + 16 * gl;
+    return g;
+}
+
+template <int U>
+struct BufPre {
+    uint4 w0;      // row 0 (the head)
+    uint4 cur[U];  // rows 1..U
+};
+
+// Issue row 0 and the first step's U rows (vmcnt counts in order: waiting
+// for row 0 does not wait for the others).
 template <int G, int U>
-__device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_t* p, uint64_t n, uint32_t seed,
-                                               uint32_t gl, const LaneAddr& la) {
+__device__ __forceinline__ void buf_preload(const BufGeo& g, uint32_t gl, BufPre<U>& pre) {
+    if (g.tiny) return;
+    if (gl < g.nb) pre.w0 = load16(g.lp);
+    if (1 + U <= g.full) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre.cur[u] = load16(g.lp + (1 + u) * (16 * G));
+    }
+}
+
+// The lane's lagged column partial Q over every row (the preloaded ones first).
+template <int G, int U>
+__device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& g, const BufPre<U>& pre,
+                                             uint32_t seed, uint32_t gl, const LaneAddr& la) {
+    if (g.tiny) return 0;
+    uint32_t pc = 0;
+    if (gl < g.nb) {
+        // Row 0 holds the head: masked leading bytes + seed.
+        uint4 w = pre.w0;
+        if (gl < 2) {
+            const int off = (int)gl * 16;
+            w.x = head_word(w.x, off, g.s0, seed);
+            w.y = head_word(w.y, off + 4, g.s0, seed);
+            w.z = head_word(w.z, off + 8, g.s0, seed);
+            w.w = head_word(w.w, off + 12, g.s0, seed);
+        }
+        pc = lag16(lds, w, la);
+    }
+    // Full rows 1..full-1: U rows per step, the next U in flight. (Measured
+    // and dropped: the loop unrolled by two with two register sets, no copy
+    // on the loop edge: 9 % fewer instructions, C2 -2.5 points, C3 +0.6.)
+    uint64_t row = 1;
+    const uint8_t* lp = g.lp;
+    if (row + U <= g.full) {
+        uint4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = pre.cur[u];
+        for (; row + 2 * U <= g.full; row += U) {
+            uint4 nxt[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+            pc = lag_column_step<U>(lds, pc, cur, la);
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+        pc = lag_column_step<U>(lds, pc, cur, la);
+        row += U;
+    }
+    for (; row < g.full; ++row) pc = sstep(lds, pc, la, lag16(lds, load16(lp + row * (16 * G)), la));
+    // Partial last row.
+    if (g.full >= 1 && g.full < g.rows && g.full * G + gl < g.nb)
+        pc = sstep(lds, pc, la, lag16(lds, load16(lp + g.full * (16 * G)), la));
+    return pc;
+}
+
+// Q -> P, shift to the end of the blocks and XOR-reduce over the group, then
+// the ragged tail (< 16 bytes); tiny buffers byte-serially. Valid on gl == 0.
+template <int G>
+__device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo& g, uint32_t pc,
+                                               const uint8_t* p, uint64_t n, uint32_t seed, uint32_t gl,
+                                               const LaneAddr& la) {
     uint32_t crc;
-    if (n < 64) {
-        // Tiny buffer: byte-serial on the group's first lane.
+    if (g.tiny) {
         crc = seed;
         if (gl == 0)
             for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
-    } else {
-        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
-        const uint8_t* e = p + n;
-        const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
-        const int s0 = (int)(p - a0);
-        const uint64_t nb = (uint64_t)(eb - a0) >> 4;  // >= 3 blocks since n >= 64
-        const uint64_t full = nb / G;                   // rows where every lane has a block
-        const uint64_t rows = (nb + G - 1) / G;
-        const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);  // blocks in the last row, 1..G
-        const uint8_t* lp = a0 + 16 * gl;               // this lane's block in row 0
-
-        // Row 0 (holds the head: masked leading bytes + seed).
-        uint32_t pc = 0;
-        if (gl < nb) {
-            uint4 w = load16(lp);
-            if (gl < 2) {
-                const int off = (int)gl * 16;
-                w.x = head_word(w.x, off, s0, seed);
-                w.y = head_word(w.y, off + 4, s0, seed);
-                w.z = head_word(w.z, off + 8, s0, seed);
-                w.w = head_word(w.w, off + 12, s0, seed);
-            }
-            pc = lag16(lds, w, la);
-        }
-        // Full rows 1..full-1: U rows per step, the next U in flight.
-        uint64_t row = 1;
-#if PCRC_LOOP_UNROLL2
-        // (Variant: two register sets used in turn, the body unrolled by two,
-        // so no register copy sits on the loop edge: 9 % fewer instructions,
-        // measured 2.5 points SLOWER on C2, +0.6 on C3; off by default.)
-        if (row + U <= full) {
-            uint4 cur[U], nxt[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
-            for (;;) {
-                if (row + 2 * U > full) {
-                    pc = lag_column_step<U>(lds, pc, cur, la);
-                    row += U;
-                    break;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                pc = lag_column_step<U>(lds, pc, cur, la);
-                row += U;
-                if (row + 2 * U > full) {
-                    pc = lag_column_step<U>(lds, pc, nxt, la);
-                    row += U;
-                    break;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + U + u) * (16 * G));
-                pc = lag_column_step<U>(lds, pc, nxt, la);
-                row += U;
-            }
-        }
-#else
-        if (row + U <= full) {
-            uint4 cur[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
-            for (; row + 2 * U <= full; row += U) {
-                uint4 nxt[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                pc = lag_column_step<U>(lds, pc, cur, la);
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-            }
-            pc = lag_column_step<U>(lds, pc, cur, la);
-            row += U;
-        }
-#endif
-        for (; row < full; ++row) pc = sstep(lds, pc, la, lag16(lds, load16(lp + row * (16 * G)), la));
-        // Partial last row.
-        if (full >= 1 && full < rows && full * G + gl < nb)
-            pc = sstep(lds, pc, la, lag16(lds, load16(lp + full * (16 * G)), la));
-
-        pc = dstep(lds, pc, la);  // Q -> P
-        crc = group_reduce<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds);
-        // Ragged tail (< 16 bytes) after the last aligned block.
-        if (gl == 0)
-            for (const uint8_t* q = eb; q < e; ++q) crc = bytestep(lds, crc, load8(q), la);
+        return crc;
     }
+    pc = dstep(lds, pc, la);  // Q -> P
+    crc = group_reduce<G>(pc, (g.rlast + G - 1 - gl) & (G - 1), lds);
+    if (gl == 0)
+        for (const uint8_t* q = g.eb; q < g.e; ++q) crc = bytestep(lds, crc, load8(q), la);
     return crc;
+}
+
+// CRC-32C of one buffer (seed applied) by a group of G lanes, unpipelined;
+// the result is valid on the group's first lane (gl == 0).
+template <int G, int U>
+__device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_t* p, uint64_t n, uint32_t seed,
+                                               uint32_t gl, const LaneAddr& la) {
+    const BufGeo g = buf_geo<G>(p, n, gl);
+    BufPre<U> pre;
+    buf_preload<G, U>(g, gl, pre);
+    const uint32_t pc = buf_body<G, U>(lds, g, pre, seed, gl, la);
+    return buf_finish<G>(lds, g, pc, p, n, seed, gl, la);
 }
 
 template <int G, int U = 4, bool MSG = false>
@@ -471,6 +497,9 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         }
         return;
     }
+    // (Measured and dropped: software-pipelining the wave's buffers -- the
+    // next buffer's descriptor and first rows issued before the current
+    // buffer's finish -- 127 instead of 106 VGPRs, C2 -1 point, C3 -0.6.)
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.count; wv += nwaves) {
         const uint64_t bi = wv * GPW + grp;
         const bool active = bi < args.count;
@@ -487,7 +516,6 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             }
             if (args.seeds) seed = args.seeds[bi];
         }
-
         const uint32_t crc = buffer_crc<G, U>(lds, p, n, seed, gl, la);
         if (active && gl == 0) args.out[bi] = crc;
     }

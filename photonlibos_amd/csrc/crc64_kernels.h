@@ -289,34 +289,6 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
 #pragma unroll
                 for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
             };
-#if PCRC_LOOP_UNROLL2
-            if (row + U <= full) {
-                // Two register sets used in turn: no register copy on the loop edge.
-                uint4 cur[U], nxt[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
-                for (;;) {
-                    if (row + 2 * U > full) {
-                        column_step(cur);
-                        row += U;
-                        break;
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                    column_step(cur);
-                    row += U;
-                    if (row + 2 * U > full) {
-                        column_step(nxt);
-                        row += U;
-                        break;
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + U + u) * (16 * G));
-                    column_step(nxt);
-                    row += U;
-                }
-            }
-#else
             if (row + U <= full) {
                 uint4 cur[U];
 #pragma unroll
@@ -332,7 +304,6 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                 column_step(cur);
                 row += U;
             }
-#endif
             for (; row < full; ++row) pc = sstep64(lds, pc, la, lag16_64(lds, load16(lp + row * (16 * G)), la));
             if (full >= 1 && full < rows && full * G + gl < nb)
                 pc = sstep64(lds, pc, la, lag16_64(lds, load16(lp + full * (16 * G)), la));

@@ -61,6 +61,42 @@ __global__ __launch_bounds__(1024) void rows_kernel(const uint8_t* base, uint64_
     sink[blockIdx.x * 1024ull + threadIdx.x] = acc;
 }
 
+// The CRC kernels' lane-group read pattern with the CRC replaced by an XOR:
+// G lanes per buffer, 64/G buffers per wave, rows of 16*G bytes, U rows per
+// step with the next U in flight (as buffer_crc), persistent 1024-thread
+// workgroups, nt loads. What does a buffer size / lane-group geometry read at?
+template <int G, int U>
+__global__ __launch_bounds__(1024) void group_rows_kernel(const uint8_t* base, uint64_t stride, uint64_t rows,
+                                                         uint64_t count, uint32_t* sink) {
+    constexpr int GPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1), grp = lane / G;
+    const uint64_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 16;
+    uint32_t acc = 0;
+    for (uint64_t wv = blockIdx.x * 16ull + wave; wv * GPW < count; wv += nwaves) {
+        const uint64_t b = wv * GPW + grp;
+        if (b >= count) continue;
+        const uint8_t* p = base + b * stride + 16 * gl;
+        uint64_t r = 0;
+        u32x4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = ld<true>(p + (uint64_t)u * 16 * G);
+        for (; r + 2 * U <= rows; r += U) {
+            u32x4 nxt[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = ld<true>(p + (r + U + u) * 16 * G);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc ^= cur[u].x ^ cur[u].y ^ cur[u].z ^ cur[u].w;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= cur[u].x ^ cur[u].y ^ cur[u].z ^ cur[u].w;
+    }
+    sink[blockIdx.x * 1024ull + threadIdx.x] = acc;
+}
+
 // The generic strided CRC32C kernel (crc32c_batch_kernel's non-message path,
 // same buffer_crc) with per-wave timestamps and a choice of task hand-out:
 //   MODE 0: static (wave w takes wave tasks w, w + nwaves, ... as the product);
@@ -253,6 +289,21 @@ int probe_crc64_ablate(const void* base, uint64_t nbytes, uint64_t count, uint64
         default: AB64(0); break;
     }
 #undef AB64
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// group_rows_kernel<G, U> over count buffers of rows*16*G bytes (rows % U == 0).
+int probe_group_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink, int blocks,
+                     int g, int u, void* stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+#define GR(GG, UU) hipLaunchKernelGGL((group_rows_kernel<GG, UU>), dim3(blocks), dim3(1024), 0, s, b, stride, rows, count, sink)
+    if (u == 8) {
+        switch (g) { case 4: GR(4, 8); break; case 8: GR(8, 8); break; case 16: GR(16, 8); break; case 32: GR(32, 8); break; default: GR(64, 8); }
+    } else {
+        switch (g) { case 4: GR(4, 4); break; case 8: GR(8, 4); break; case 16: GR(16, 4); break; case 32: GR(32, 4); break; default: GR(64, 4); }
+    }
+#undef GR
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

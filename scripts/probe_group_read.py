@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""What the CRC kernels' lane-group read pattern can read (bench-only probe,
+libphoton_probes.so group_rows_kernel: G lanes per buffer, 64/G buffers per
+wave, U rows per step + U in flight, nt loads, XOR instead of CRC) for the
+C3 shape (1 Mi x 4 KiB) and the C2 shape (64 Ki x 64 KiB), next to the CRC
+kernel itself on the same buffers. Interleaved rounds, median ms."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from photonlibos_amd import checksum as ck  # noqa: E402
+
+P = ctypes.CDLL(os.path.join(REPO, "photonlibos_amd", "lib", "libphoton_probes.so"))
+vp, u64, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+P.probe_group_rows.argtypes = [vp, u64, u64, u64, vp, ci, ci, ci, vp]
+P.probe_group_rows.restype = ci
+st = torch.cuda.current_stream()
+cus = torch.cuda.get_device_properties(0).multi_processor_count
+sink = torch.zeros(cus * 1024, dtype=torch.int32, device="cuda")
+
+
+def timed(fn, reps=20):
+    fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(reps):
+        fn()
+    b.record(st)
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+for name, n, cnt, gs in (("c3", 4096, 1 << 20, (4, 8, 16, 32, 64)), ("c2", 65536, 65536, (8, 32, 64))):
+    buf = torch.empty(n * cnt, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(buf, n, n, cnt, 0x5EED0001)
+    out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+    variants = {}
+    for g in gs:
+        for u in (4, 8):
+            rows = n // (16 * g)
+            if rows % u:
+                continue
+            variants[f"read G{g} U{u}"] = (lambda g=g, u=u, rows=rows: P.probe_group_rows(
+                buf.data_ptr(), n, rows, cnt, sink.data_ptr(), cus, g, u, st.cuda_stream))
+    variants["crc (product)"] = lambda: ck.batch_strided(buf, n, n, cnt, out, stream=st)
+    res = {k: [] for k in variants}
+    for r in range(6):
+        for k, f in (list(variants.items()) if r % 2 == 0 else list(variants.items())[::-1]):
+            res[k].append(timed(f))
+    for k, ms in res.items():
+        med = float(np.median(ms))
+        print(json.dumps({"shape": name, "variant": k, "ms": round(med, 4), "GBps": round(n * cnt / med / 1e6, 1),
+                          "frac_of_8TBps": round(n * cnt / med / 1e6 / 8000, 4)}), flush=True)
+    del buf
+    torch.cuda.empty_cache()
