@@ -235,6 +235,7 @@ LaneConsts make_lane_consts(int g, int b) {
     LaneConsts c;
     c.kshift = xpow(8ull * 16ull * (uint64_t)b * (uint64_t)g);
     for (int k = 0; k < 6; ++k) mul_basis(xpow((128ull * (uint64_t)b) << k), c.basis[k]);
+    for (int d = 0; d < 8; ++d) mul_basis(xpow(32ull + 128ull * (uint64_t)d), c.fbasis[d]);
     return c;
 }
 

@@ -29,6 +29,16 @@ constexpr uint32_t kSOff = 128u;                             // S half of a row
 constexpr uint32_t kRBase = kTableBytes;
 constexpr uint32_t kRBytes = 6u * 4u * 256u * 4u;            // 24 KiB
 constexpr uint32_t kLdsBytes = kRBase + kRBytes;             // 90112 B of the 160 KiB
+// Finish tables F_d (batch kernel, G <= 8, in place of R_k): p -> p * x^(32 +
+// 128*d) mod P for d < G, i.e. Q -> P and the lane's shift to the end of the
+// buffer (d = 16-byte blocks after its last block) in ONE 4-lookup step.
+// Index row b (256 B stride, 128 B used): word d*4 + t (G = 8) or
+// (d*4 + t)*2 + r2 (G = 4, r2 = (lane/4)&1). In a lookup instruction the 8
+// lanes of a group read 8 distinct d (d = const - gl mod G) and the groups
+// of a 32-lane half read distinct slices t = (i + q) % 4 (q = lane/8 % 4;
+// G = 4: two groups per q, told apart by r2): 32 distinct banks, no replicas.
+constexpr uint32_t kFBase = kTableBytes;
+constexpr uint32_t kLdsBytesF = kFBase + 65536u;             // 128 KiB
 constexpr int kBlock = 1024;                   // 16 waves, one workgroup per CU
 constexpr int kWaves = kBlock / 64;
 
@@ -36,6 +46,7 @@ constexpr int kWaves = kBlock / 64;
 struct LaneConsts {
     uint32_t kshift;           // x^(8*16*G) mod P: one row of the lane's column
     uint32_t basis[6][32];     // basis of x^(128 * 2^k) mod P, k = 0..5
+    uint32_t fbasis[8][32];    // basis of x^(32 + 128 * d) mod P, d < 8 (F_d tables)
 };
 
 // Seed application for uniform-length batches: crc32c_extend(d, n, s) =
@@ -192,17 +203,33 @@ __device__ __forceinline__ uint8_t load8(const uint8_t* p) { return *(g_u8*)p; }
 
 // Build the D and S tables in LDS (every workgroup; 1024 threads = one entry of
 // each table per thread).
+// FG = 0: R_k lane-combine tables; FG = 4 or 8: F_d finish tables for G = FG.
+template <int FG = 0>
 __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc) {
     const uint32_t tid = threadIdx.x;
     const uint32_t t = tid >> 8, b = tid & 255u;
-    // R_k[t][b] = (b << 8t) * x^(128*B*2^k): XOR of the basis words of b's bits
-    // (t is uniform per wavefront, so the basis reads are scalar).
+    if constexpr (FG == 0) {
+        // R_k[t][b] = (b << 8t) * x^(128*B*2^k): XOR of the basis words of b's
+        // bits (t is uniform per wavefront, so the basis reads are scalar).
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        uint32_t r = 0;
+        for (int k = 0; k < 6; ++k) {
+            uint32_t r = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & kc.basis[k][8 * t + j];
-        lds[kRBase / 4 + k * 1024 + t * 256 + b] = r;
+            for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & kc.basis[k][8 * t + j];
+            lds[kRBase / 4 + k * 1024 + t * 256 + b] = r;
+        }
+    } else {
+        // F_d: words w = 8*t' .. 8*t'+7 of row b (t' = tid >> 8, wave-uniform).
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = 8 * t + k;
+            const uint32_t d = FG == 8 ? w >> 2 : w >> 3;
+            const uint32_t ts = FG == 8 ? w & 3u : (w >> 1) & 3u;
+            uint32_t r = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & kc.fbasis[d][8 * ts + j];
+            lds[kFBase / 4 + b * 64 + w] = r;
+        }
     }
     const uint32_t v = b << (8 * t);
     const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
@@ -374,8 +401,27 @@ __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo
             for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
         return crc;
     }
-    pc = dstep(lds, pc, la);  // Q -> P
-    crc = group_reduce<G>(pc, (g.rlast + G - 1 - gl) & (G - 1), lds);
+    const uint32_t d = (g.rlast + G - 1 - gl) & (G - 1);
+    if constexpr (G <= 8) {
+        // Q * x^(32 + 128 d) through F_d: one table step (round 2 used a D step
+        // and log2(G) R_k levels, 16 lookups in a dependent chain).
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t q = (lane >> 3) & 3u;
+        const uint32_t dof = G == 8 ? d * 16u : d * 32u + ((lane >> 2) & 1u) * 4u;
+        uint32_t f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t ts = (i + q) & 3u;
+            const uint32_t fo = dof + (G == 8 ? ts * 4u : ts * 8u);
+            f[i] = lds_word(lds, __builtin_amdgcn_perm(pc, fo, la.sel[i]) + kFBase);
+        }
+        crc = xor3(xor3(f[0], f[1], f[2]), f[3], 0u);
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
+    } else {
+        pc = dstep(lds, pc, la);  // Q -> P
+        crc = group_reduce<G>(pc, d, lds);
+    }
     if (gl == 0)
         for (const uint8_t* q = g.eb; q < g.e; ++q) crc = bytestep(lds, crc, load8(q), la);
     return crc;
@@ -395,8 +441,8 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
 
 template <int G, int U = 4, bool MSG = false>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-    build_tables(lds, kc);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(G <= 8 ? kLdsBytesF : kLdsBytes) / 4];
+    build_tables<G <= 8 ? G : 0>(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
     const uint32_t lane = threadIdx.x & 63u;

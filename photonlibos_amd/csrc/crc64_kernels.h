@@ -270,9 +270,25 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
             const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);
             const uint8_t* lp = a0 + 16 * gl;
             uint2 pc = make_uint2(0, 0);
+            // Row 0, the lead rows ((full-1) % U, so the U-row loop ends at the
+            // last full row), the first step's U rows and the partial last row
+            // are issued together: no row is loaded on its own and waited for.
+            const uint32_t lead = full >= 1 ? (uint32_t)((full - 1) % U) : 0u;
+            uint4 w0, wl[U - 1], cur[U], wp;
+            if (gl < nb) w0 = load16(lp);
+#pragma unroll
+            for (int u = 0; u < U - 1; ++u)
+                if ((uint32_t)u < lead) wl[u] = load16(lp + (1 + u) * (16 * G));
+            const bool steps = 1 + lead + U <= full;
+            if (steps) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (1 + lead + u) * (16 * G));
+            }
+            const bool part = full >= 1 && full < rows && full * G + gl < nb;
+            if (part) wp = load16(lp + full * (16 * G));
             // Row 0 (head: masked leading bytes + inverted init).
             if (gl < nb) {
-                uint4 w = load16(lp);
+                uint4 w = w0;
                 if (gl < 2) {
                     const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
                     const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
@@ -280,7 +296,10 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                 }
                 pc = lag16_64(lds, w, la);
             }
-            uint64_t row = 1;
+#pragma unroll
+            for (int u = 0; u < U - 1; ++u)
+                if ((uint32_t)u < lead) pc = sstep64(lds, pc, la, lag16_64(lds, wl[u], la));
+            uint64_t row = 1 + lead;
             // U lagged blocks (independent) then U row shifts (the carried chain).
             auto column_step = [&](const uint4(&w)[U]) {
                 uint2 c[U];
@@ -289,10 +308,7 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
 #pragma unroll
                 for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
             };
-            if (row + U <= full) {
-                uint4 cur[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (row + u) * (16 * G));
+            if (steps) {
                 for (; row + 2 * U <= full; row += U) {
                     uint4 nxt[U];
 #pragma unroll
@@ -302,11 +318,8 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                     for (int u = 0; u < U; ++u) cur[u] = nxt[u];
                 }
                 column_step(cur);
-                row += U;
             }
-            for (; row < full; ++row) pc = sstep64(lds, pc, la, lag16_64(lds, load16(lp + row * (16 * G)), la));
-            if (full >= 1 && full < rows && full * G + gl < nb)
-                pc = sstep64(lds, pc, la, lag16_64(lds, load16(lp + full * (16 * G)), la));
+            if (part) pc = sstep64(lds, pc, la, lag16_64(lds, wp, la));
             pc = dstep64(lds, pc, la);  // Q -> P
             reg = group_reduce64<G>(u64of(pc), (rlast + G - 1 - gl) & (G - 1), lds);
             if (gl == 0)
