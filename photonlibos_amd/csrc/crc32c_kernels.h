@@ -180,6 +180,22 @@ __device__ __forceinline__ uint32_t head_word(uint32_t w, int off, int s0, uint3
     return w;
 }
 
+// head_word without branches (selects only): every lane can run it (lanes
+// whose words lie past the first data word get k <= -4: unchanged), so the
+// head needs no divergent region, whose join made the compiler wait for ALL
+// loads in flight (vmcnt(0)) instead of row 0 alone.
+__device__ __forceinline__ uint32_t head_word_sel(uint32_t w, int off, int s0, uint32_t seed) {
+    const int k = s0 - off;  // the data starts k bytes into this word
+    const int kc = k < -3 ? -3 : k > 3 ? 3 : k;
+    const int kk = k < 0 ? 0 : k > 4 ? 4 : k;
+    // bytes >= k survive; the seed's bytes land at byte offset k (64-bit
+    // shifts, no per-case shift amounts: the compiler keeps it straight-line)
+    const uint32_t keep = (uint32_t)(0xffffffffull << (8 * kk));
+    const uint32_t in = (uint32_t)(k + 3) <= 6u ? 0xffffffffu : 0u;
+    const uint32_t sv = (uint32_t)((((uint64_t)seed) << 32) >> (32 - 8 * kc)) & in;
+    return (w & keep) ^ sv;
+}
+
 __device__ __forceinline__ uint32_t mul_basis_dev(uint32_t p, const uint32_t* basis) {
     uint32_t r = 0;
 #pragma unroll
@@ -299,6 +315,7 @@ __device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
 // (Q -> P, lane combine, ragged tail).
 struct BufGeo {
     const uint8_t* lp;  // this lane's block in row 0
+    const uint8_t* a0;  // the aligned start (always a readable 16-byte block when !tiny)
     const uint8_t* eb;  // end of the last whole 16-byte block
     const uint8_t* e;   // end of the buffer
     uint64_t nb;        // 16-byte blocks from the aligned start
@@ -322,6 +339,7 @@ __device__ __forceinline__ BufGeo buf_geo(const uint8_t* p, uint64_t n, uint32_t
     g.rows = (g.nb + G - 1) / G;
     g.rlast = (uint32_t)(g.nb - (g.rows ? g.rows - 1 : 0) * G);
     g.lp = a0 + 16 * gl;
+    g.a0 = a0;
     return g;
 }
 
@@ -333,14 +351,18 @@ struct BufPre {
 
 // Issue row 0 and the first step's U rows (vmcnt counts in order: waiting
 // for row 0 does not wait for the others).
+// Loads are unconditional inside a non-tiny buffer: a lane with no block in
+// row 0, or a buffer too short for a first step, re-reads the aligned start
+// (in bounds; the values are discarded), so there is no divergent region
+// around the loads and every later wait counts exactly.
 template <int G, int U>
 __device__ __forceinline__ void buf_preload(const BufGeo& g, uint32_t gl, BufPre<U>& pre) {
     if (g.tiny) return;
-    if (gl < g.nb) pre.w0 = load16(g.lp);
-    if (1 + U <= g.full) {
+    const uint8_t* p0 = gl < g.nb ? g.lp : g.a0;
+    pre.w0 = load16(p0);
+    const bool step = 1 + U <= g.full;
 #pragma unroll
-        for (int u = 0; u < U; ++u) pre.cur[u] = load16(g.lp + (1 + u) * (16 * G));
-    }
+    for (int u = 0; u < U; ++u) pre.cur[u] = load16(step ? g.lp + (1 + u) * (16 * G) : p0);
 }
 
 // The lane's lagged column partial Q over every row (the preloaded ones first).
@@ -348,19 +370,16 @@ template <int G, int U>
 __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& g, const BufPre<U>& pre,
                                              uint32_t seed, uint32_t gl, const LaneAddr& la) {
     if (g.tiny) return 0;
-    uint32_t pc = 0;
-    if (gl < g.nb) {
-        // Row 0 holds the head: masked leading bytes + seed.
-        uint4 w = pre.w0;
-        if (gl < 2) {
-            const int off = (int)gl * 16;
-            w.x = head_word(w.x, off, g.s0, seed);
-            w.y = head_word(w.y, off + 4, g.s0, seed);
-            w.z = head_word(w.z, off + 8, g.s0, seed);
-            w.w = head_word(w.w, off + 12, g.s0, seed);
-        }
-        pc = lag16(lds, w, la);
-    }
+    // Row 0 holds the head: masked leading bytes + seed (branch-free; lanes
+    // without a block in row 0 feed a zero block, whose lagged CRC is 0).
+    uint4 w = pre.w0;
+    const int off = (int)gl * 16;
+    w.x = head_word_sel(w.x, off, g.s0, seed);
+    w.y = head_word_sel(w.y, off + 4, g.s0, seed);
+    w.z = head_word_sel(w.z, off + 8, g.s0, seed);
+    w.w = head_word_sel(w.w, off + 12, g.s0, seed);
+    if (gl >= g.nb) w = make_uint4(0, 0, 0, 0);
+    uint32_t pc = lag16(lds, w, la);
     // Full rows 1..full-1: U rows per step, the next U in flight. (Measured
     // and dropped: the loop unrolled by two with two register sets, no copy
     // on the loop edge: 9 % fewer instructions, C2 -2.5 points, C3 +0.6.)
