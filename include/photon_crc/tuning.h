@@ -53,6 +53,9 @@ int photon_crc64_set_interleave(int partials);
  * the two-kernel form. */
 int photon_crc_set_msg_mode(int mode);
 
+/* Rows per step of the one-kernel message form (tuning): 2 (default) or 4. */
+int photon_crc_set_msg_rows(int rows_per_step);
+
 /* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
  * each lane reads two consecutive 16-byte blocks per row, one row shift per
  * 32 bytes (lanes per buffer <= 32; overrides the interleave). */
@@ -77,6 +80,7 @@ void photon_crc_test_fail_next(int n);
  *   6 device row shifts x^(8*16*G), G = 4..64 (5)
  *   7 device lane-combine x^(128*2^k) (image of x^0, 6)
  *   8 host slicing table T[b] (crc.cpp:82-97, 256)
+ *   9 device finish tables x^(32+128*d), d < 8 (image of x^0, 8)
  * Returns the number of words written to out[n], or a negative error. */
 int photon_crc_test_tables(int which, uint32_t* out, int n);
 

@@ -486,6 +486,11 @@ def set_msg_mode(mode):
     _check(lib().photon_crc_set_msg_mode(mode))
 
 
+def set_msg_rows(u):
+    """Rows per step of the one-kernel message form (2 or 4; tuning)."""
+    _check(lib().photon_crc_set_msg_rows(u))
+
+
 def set_stream64_run_blocks(b):
     """CRC-64 streaming kernel: 16-byte blocks per lane run (1, 2)."""
     _check(lib().photon_crc64_set_run_blocks(b))

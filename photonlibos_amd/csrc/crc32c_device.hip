@@ -71,7 +71,14 @@ std::atomic<int> g_lanes_override{0};
 // Batch kernel: rows per step of the generic kernel (2, 4, 8), or 0 = the
 // fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
 // the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
-std::atomic<int> g_generic_u{4};
+#ifndef PCRC_GENERIC_U
+#define PCRC_GENERIC_U 4
+#endif
+std::atomic<int> g_generic_u{PCRC_GENERIC_U};
+// Rows per step of the one-kernel message form: 2 measured better than 4 on
+// C5 (64 Ki messages x 8 x 8 KiB: +0.35 points per-segment, +0.8 chained)
+// while strided batches keep 4 (C2 -6, C3 -1.2, C4 -0.9 with 2).
+std::atomic<int> g_msg_u{2};
 std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
 // Streaming kernel shape, 0 = off (the default: with the conflict-free rotated
 // tables the generic kernel measures faster on every config,
@@ -690,6 +697,11 @@ int photon_crc_test_tables(int which, uint32_t* out, int n) {
         for (int k = 0; k < 6; ++k) out[k] = c.basis[k][31];
         return 6;
     }
+    if (which == 9) {  // finish tables F_d (G <= 8): image of x^0 under x^(32+128d), d < 8
+        const LaneConsts& c = lane_consts(8);
+        for (int d = 0; d < 8; ++d) out[d] = c.fbasis[d][31];
+        return 8;
+    }
     return fail(-EINVAL, "bad table id");
 }
 
@@ -715,6 +727,12 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
 int photon_crc_set_msg_mode(int mode) {
     if (mode < 0 || mode > 2) return fail(-EINVAL, "message mode must be 0 (auto), 1 (fused) or 2 (two kernels)");
     g_msg_mode.store(mode, std::memory_order_relaxed);
+    return 0;
+}
+
+int photon_crc_set_msg_rows(int rows_per_step) {
+    if (rows_per_step != 2 && rows_per_step != 4) return fail(-EINVAL, "message rows per step must be 2 or 4");
+    g_msg_u.store(rows_per_step, std::memory_order_relaxed);
     return 0;
 }
 
@@ -998,15 +1016,22 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
         uint64_t grid = ((nmsg + gpw - 1) / gpw + kWaves - 1) / kWaves;
         if (grid > (uint64_t)cus) grid = cus;
         const LaneConsts& kc = lane_consts(g);
-#define LM(GG) \
-    hipLaunchKernelGGL((crc32c_batch_kernel<GG, 4, true>), dim3(grid), dim3(kBlock), 0, st, a, kc, pow_table())
-        switch (g) {
-            case 64: LM(64); break;
-            case 32: LM(32); break;
-            case 16: LM(16); break;
-            case 8: LM(8); break;
-            default: LM(4); break;
+#define LM(GG, UU) \
+    hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU, true>), dim3(grid), dim3(kBlock), 0, st, a, kc, pow_table())
+#define LMG(UU)                     \
+    switch (g) {                    \
+        case 64: LM(64, UU); break; \
+        case 32: LM(32, UU); break; \
+        case 16: LM(16, UU); break; \
+        case 8: LM(8, UU); break;   \
+        default: LM(4, UU); break;  \
+    }
+        if (g_msg_u.load(std::memory_order_relaxed) == 2) {
+            LMG(2)
+        } else {
+            LMG(4)
         }
+#undef LMG
 #undef LM
         e = hipGetLastError();
         return e == hipSuccess ? 0 : hip_fail(e, "crc32c_batch_kernel<msg> launch");

@@ -267,7 +267,13 @@ void knob_flipper() {
                 if (rng() & 1) { photon_crc_set_stream_config(0, 0, 0); g_k_stream = 0; }
                 else { photon_crc_set_stream_config(1, 4, 3); g_k_stream = 1; }
                 break;
-            case 3: { int v = (int)(rng() % 3); photon_crc_set_msg_mode(v); g_k_msg = v; break; }
+            case 3: {
+                int v = (int)(rng() % 3);
+                photon_crc_set_msg_mode(v);
+                photon_crc_set_msg_rows(rng() & 1 ? 2 : 4);
+                g_k_msg = v;
+                break;
+            }
             case 4:
                 if (rng() & 1) { photon_crc64_set_stream_config(0, 0); g_k_s64 = 0; }
                 else { photon_crc64_set_stream_config(4, 3); g_k_s64 = 1; }
@@ -282,6 +288,7 @@ void knob_flipper() {
     photon_crc_set_generic_rows(4);
     photon_crc_set_stream_config(0, 0, 0);
     photon_crc_set_msg_mode(0);
+    photon_crc_set_msg_rows(2);
     photon_crc64_set_stream_config(0, 0);
     photon_crc64_set_interleave(1);
     printf("knob flips: %ld\n", flips);

@@ -39,6 +39,8 @@ def test_device_kernel_constants_equal_oracle_powers(oracle, ref_vectors):
     # lane-combine bases x^(128*2^k): k >= 0 are entries 4.. of x^(8*2^i)
     lsh = ref_vectors["lshift_table_sw"]
     assert _table(7) == [lsh[4 + k] for k in range(6)]
+    # finish tables F_d of lane groups <= 8: Q -> P (x^32) and the lane shift x^(128d)
+    assert _table(9) == [oracle.pow32(32 + 128 * d) for d in range(8)]
 
 
 def test_slicing_table_equals_oracle(oracle):

@@ -32,6 +32,7 @@ def _reset():
     ck.set_generic_rows(4)
     ck.set_stream_config(0, 0, 0)
     ck.set_msg_mode(0)
+    ck.set_msg_rows(2)
     ck.set_stream64_run_blocks(1)
     ck.set_stream64_interleave(1)
     ck.set_stream64_config(0, 0)
@@ -104,9 +105,10 @@ def test_fuzz_strided_batches(dev_pool, oracle, round_):
 def test_fuzz_messages(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(3000 + round_)
-    for mode in (0, 1, 2):
+    for mode, mrows in ((0, 2), (1, 2), (1, 4), (2, 2)):
         for lanes in (0, 8, 64):
             ck.set_msg_mode(mode)
+            ck.set_msg_rows(mrows)
             ck.set_lanes_per_buffer(lanes)
             nmsg = rnd.randrange(1, 400)
             iov, start, msgs = [], [0], []
