@@ -31,7 +31,8 @@ int photon_crc_set_lanes_per_buffer(int g);
  * the current tables); run_blocks = 0 turns it off again. */
 int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
 
-/* Batch kernel variant (testing / tuning): 2, 4 (default) or 8 = the generic
+/* Batch kernel variant (testing / tuning): -1 (default) = rows per step by
+ * lane-group size (2 for 16-lane groups, else 4); 2, 4 or 8 = the generic
  * kernel with that many rows per step; 0 = the fused kernel (four rows per
  * step with the row shifts folded into the tables). */
 int photon_crc_set_generic_rows(int rows_per_step);

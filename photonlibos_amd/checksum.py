@@ -476,8 +476,8 @@ def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
 
 
 def set_generic_rows(u):
-    """Batch kernel variant: 2, 4 (default), 8 = rows per step of the generic
-    kernel; 0 = the fused 4-row kernel."""
+    """Batch kernel variant: -1 (default) = by lane-group size; 2, 4, 8 = rows
+    per step of the generic kernel; 0 = the fused 4-row kernel."""
     _check(lib().photon_crc_set_generic_rows(u))
 
 

@@ -71,10 +71,9 @@ std::atomic<int> g_lanes_override{0};
 // Batch kernel: rows per step of the generic kernel (2, 4, 8), or 0 = the
 // fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
 // the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
-#ifndef PCRC_GENERIC_U
-#define PCRC_GENERIC_U 4
-#endif
-std::atomic<int> g_generic_u{PCRC_GENERIC_U};
+// Rows per step of the generic batch kernel: -1 = by lane-group size
+// (batch_rows), else 2, 4, 8, or 0 = the fused kernel.
+std::atomic<int> g_generic_u{-1};
 // Rows per step of the one-kernel message form: 2 measured better than 4 on
 // C5 (64 Ki messages x 8 x 8 KiB: +0.35 points per-segment, +0.8 chained)
 // while strided batches keep 4 (C2 -6, C3 -1.2, C4 -0.9 with 2).
@@ -350,18 +349,32 @@ const FusedConsts& fused_consts(int g) {
     return tab[g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2];
 }
 
-// lanes: 0 = by typical_len (choose_lanes), else the lane-group size.
+// Lane-group size of the CRC32C generic batch kernel: as choose_lanes, but
+// 4-8 KiB buffers take 16 lanes (with 2 rows per step, batch_rows): C3 (1 Mi x
+// 4 KiB) 85.5 % vs 83.7 % for 8 lanes x 4 rows (profiles/r02_tune_lanes_rows.jsonl).
+int batch_lanes(uint64_t typical_len) {
+    if (const int g = g_lanes_override.load(std::memory_order_relaxed)) return g;
+    if (typical_len >= 4096 && typical_len < 8192) return 16;
+    return choose_lanes(typical_len);
+}
+
+int batch_rows(int g) {
+    const int u = g_generic_u.load(std::memory_order_relaxed);
+    return u >= 0 ? u : g == 16 ? 2 : 4;
+}
+
+// lanes: 0 = by typical_len (batch_lanes), else the lane-group size.
 int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, int lanes = 0) {
     if (a.count == 0) return 0;
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const int g = lanes ? lanes : choose_lanes(typical_len);
+    const int g = lanes ? lanes : batch_lanes(typical_len);
     const uint64_t gpw = 64 / g;
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
     if (grid > (uint64_t)cus) grid = cus;
-    const int rows_per_step = g_generic_u.load(std::memory_order_relaxed);
+    const int rows_per_step = batch_rows(g);
     if (rows_per_step == 0) {
         const FusedConsts& fc = fused_consts(g);
 #define LF(GG) hipLaunchKernelGGL((crc32c_fused_kernel<GG>), dim3(grid), dim3(kBlock), 0, stream, a, fc)
@@ -672,7 +685,7 @@ int photon_crc_set_lanes_per_buffer(int g) {
     return 0;
 }
 
-int photon_crc_lanes_for(uint64_t nbytes) { return choose_lanes(nbytes); }
+int photon_crc_lanes_for(uint64_t nbytes) { return batch_lanes(nbytes); }
 
 void photon_crc_test_fail_next(int n) { g_fail_next = n > 0 ? n : 0; }
 
@@ -706,8 +719,8 @@ int photon_crc_test_tables(int which, uint32_t* out, int n) {
 }
 
 int photon_crc_set_generic_rows(int rows_per_step) {
-    if (rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
-        return fail(-EINVAL, "rows per step must be 0 (fused kernel), 2, 4 or 8");
+    if (rows_per_step != -1 && rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
+        return fail(-EINVAL, "rows per step must be -1 (auto), 0 (fused kernel), 2, 4 or 8");
     g_generic_u.store(rows_per_step, std::memory_order_relaxed);
     return 0;
 }

@@ -69,7 +69,7 @@ def make(v, lanes):
     def f():
         ck.set_lanes_per_buffer(lanes)
         if v.startswith("generic"):
-            ck.set_generic_rows(int(v.split(":")[1]) if ":" in v else 4)
+            ck.set_generic_rows(int(v.split(":")[1]) if ":" in v else -1)
             ck.set_stream_config(0)
         else:
             _, b, u, d = v.split(":")
@@ -99,7 +99,7 @@ ck.set_stream_config(0, 0, 0)
 ck.set_stream64_config(0, 0)
 ck.set_stream64_interleave(1)
 ck.set_stream64_run_blocks(1)
-ck.set_generic_rows(4)
+ck.set_generic_rows(-1)
 ck.set_lanes_per_buffer(0)
 rows = []
 for k, ms in res.items():

@@ -59,7 +59,7 @@ std::atomic<long> g_checked{0}, g_bad{0}, g_err{0};
     } while (0)
 
 // Knob state as set by the flipper (for the mismatch report only).
-std::atomic<int> g_k_lanes{0}, g_k_rows{4}, g_k_stream{0}, g_k_msg{0}, g_k_s64{0}, g_k_il{1};
+std::atomic<int> g_k_lanes{0}, g_k_rows{-1}, g_k_stream{0}, g_k_msg{0}, g_k_s64{0}, g_k_il{1};
 
 void check_at(bool ok, const char* what, uint64_t a, uint64_t b, uint64_t c) {
     g_checked.fetch_add(1);
@@ -257,12 +257,12 @@ void submitter(int t) {
 void knob_flipper() {
     std::mt19937 rng(7);
     const int lanes[] = {0, 4, 8, 16, 32, 64};
-    const int rows[] = {0, 2, 4, 8};
+    const int rows[] = {-1, 0, 2, 4, 8};
     long flips = 0;
     while (!g_stop.load()) {
         switch (rng() % 6) {
             case 0: { int v = lanes[rng() % 6]; photon_crc_set_lanes_per_buffer(v); g_k_lanes = v; break; }
-            case 1: { int v = rows[rng() % 4]; photon_crc_set_generic_rows(v); g_k_rows = v; break; }
+            case 1: { int v = rows[rng() % 5]; photon_crc_set_generic_rows(v); g_k_rows = v; break; }
             case 2:
                 if (rng() & 1) { photon_crc_set_stream_config(0, 0, 0); g_k_stream = 0; }
                 else { photon_crc_set_stream_config(1, 4, 3); g_k_stream = 1; }
@@ -285,7 +285,7 @@ void knob_flipper() {
     }
     // back to the defaults
     photon_crc_set_lanes_per_buffer(0);
-    photon_crc_set_generic_rows(4);
+    photon_crc_set_generic_rows(-1);
     photon_crc_set_stream_config(0, 0, 0);
     photon_crc_set_msg_mode(0);
     photon_crc_set_msg_rows(2);

@@ -29,7 +29,7 @@ def dev_pool():
 def _reset():
     yield
     ck.set_lanes_per_buffer(0)
-    ck.set_generic_rows(4)
+    ck.set_generic_rows(-1)
     ck.set_stream_config(0, 0, 0)
     ck.set_msg_mode(0)
     ck.set_msg_rows(2)

@@ -30,7 +30,7 @@ def _reset_lanes():
     yield
     ck.set_lanes_per_buffer(0)
     ck.set_stream_config(0, 0, 0)
-    ck.set_generic_rows(4)
+    ck.set_generic_rows(-1)
     ck.set_msg_mode(0)
 
 
@@ -202,7 +202,7 @@ def test_full_c2_4gib(torch_dev, oracle):
     ck.set_stream_config(0, 0, 0)
     ck.set_generic_rows(0)  # the fused kernel
     e = run_strided(torch_dev, d, nbytes, nbytes, count)
-    ck.set_generic_rows(4)
+    ck.set_generic_rows(-1)
     assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, e)
     rnd = random.Random(2)
     for i in [0, 1, count - 1] + [rnd.randrange(count) for _ in range(61)]:
