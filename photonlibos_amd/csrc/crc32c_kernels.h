@@ -273,6 +273,22 @@ __device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
 
 // Shift lane partials to the end of the body (d blocks of 16 bytes) and
 // XOR-reduce over the G lanes of the group.
+// XOR over the G lanes of an aligned lane group, result in EVERY lane of
+// the group. Steps inside a 16-lane row are DPP moves (VALU: quad_perm
+// [1,0,3,2], [2,3,0,1], then row_half_mirror and row_mirror, which pair each
+// quad / half-row with the other one); only 32- and 64-lane groups use
+// ds_bpermute (__shfl_xor), which costs an LDS round trip.
+template <int G>
+__device__ __forceinline__ uint32_t group_xor(uint32_t v) {
+    if constexpr (G >= 2) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    if constexpr (G >= 4) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    if constexpr (G >= 8) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    if constexpr (G >= 16) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+    if constexpr (G >= 32) v ^= (uint32_t)__shfl_xor((int)v, 16, 64);
+    if constexpr (G >= 64) v ^= (uint32_t)__shfl_xor((int)v, 32, 64);
+    return v;
+}
+
 template <int G>
 __device__ __forceinline__ uint32_t group_reduce(uint32_t pc, uint32_t d, const uint32_t* lds) {
     constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
@@ -285,9 +301,7 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t pc, uint32_t d, const 
                                 R[768 + (pc >> 24)], 0u);
         pc = ((d >> k) & 1u) ? m : pc;
     }
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
-    return pc;
+    return group_xor<G>(pc);
 }
 
 __device__ __forceinline__ uint32_t wave_id() {
@@ -408,7 +422,9 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
 }
 
 // Q -> P, shift to the end of the blocks and XOR-reduce over the group, then
-// the ragged tail (< 16 bytes); tiny buffers byte-serially. Valid on gl == 0.
+// the ragged tail (< 16 bytes); tiny buffers byte-serially. Valid on EVERY
+// lane of the group (the byte-serial parts run on all of them: same bytes,
+// same loads), so message chains need no broadcast from the first lane.
 template <int G>
 __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo& g, uint32_t pc,
                                                const uint8_t* p, uint64_t n, uint32_t seed, uint32_t gl,
@@ -416,8 +432,7 @@ __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo
     uint32_t crc;
     if (g.tiny) {
         crc = seed;
-        if (gl == 0)
-            for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
+        for (uint64_t k = 0; k < n; ++k) crc = bytestep(lds, crc, load8(p + k), la);
         return crc;
     }
     const uint32_t d = (g.rlast + G - 1 - gl) & (G - 1);
@@ -434,20 +449,17 @@ __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo
             const uint32_t fo = dof + (G == 8 ? ts * 4u : ts * 8u);
             f[i] = lds_word(lds, __builtin_amdgcn_perm(pc, fo, la.sel[i]) + kFBase);
         }
-        crc = xor3(xor3(f[0], f[1], f[2]), f[3], 0u);
-#pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o, 64);
+        crc = group_xor<G>(xor3(xor3(f[0], f[1], f[2]), f[3], 0u));
     } else {
         pc = dstep(lds, pc, la);  // Q -> P
         crc = group_reduce<G>(pc, d, lds);
     }
-    if (gl == 0)
-        for (const uint8_t* q = g.eb; q < g.e; ++q) crc = bytestep(lds, crc, load8(q), la);
+    for (const uint8_t* q = g.eb; q < g.e; ++q) crc = bytestep(lds, crc, load8(q), la);
     return crc;
 }
 
 // CRC-32C of one buffer (seed applied) by a group of G lanes, unpipelined;
-// the result is valid on the group's first lane (gl == 0).
+// the result is valid on every lane of the group.
 template <int G, int U>
 __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_t* p, uint64_t n, uint32_t seed,
                                                uint32_t gl, const LaneAddr& la) {
@@ -496,11 +508,9 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             if (!args.out) {
                 // No per-segment CRCs wanted: chain through the seed
                 // (crc32c_extend(seg, n, acc), Crc32Hasher::extend_hash).
-                for (uint64_t sg = s0; sg < s1; ++sg) {
-                    const uint32_t seed = (uint32_t)__shfl((int)acc, (int)(threadIdx.x & 63u & ~(uint32_t)(G - 1)), 64);
+                for (uint64_t sg = s0; sg < s1; ++sg)
                     acc = buffer_crc<G, U>(lds, static_cast<const uint8_t*>(args.iov[sg].base), args.iov[sg].len,
-                                           seed, gl, la);
-                }
+                                           acc, gl, la);
             } else {
                 // Per-segment CRCs (seed 0) and the fold acc = acc * K ^ c,
                 // K = x^(8 len) (crc32c_combine, crc.cpp:393-405). The multiply
@@ -515,15 +525,13 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                 // front of the next segment's loads): lane j of the group keeps
                 // the CRC of segment s0 + j (mod G), and the group stores G
                 // consecutive CRCs with one coalesced store.
-                const uint32_t leader = threadIdx.x & 63u & ~(uint32_t)(G - 1);
                 uint32_t pend = 0;
                 for (uint64_t sg = s0; sg < s1; ++sg) {
                     const uint8_t* p = static_cast<const uint8_t*>(args.iov[sg].base);
                     const uint64_t n = args.iov[sg].len;
                     const uint32_t c = buffer_crc<G, U>(lds, p, n, 0u, gl, la);
                     const uint32_t j = (uint32_t)((sg - s0) & (G - 1));
-                    const uint32_t cb = (uint32_t)__shfl((int)c, (int)leader, 64);
-                    if (gl == j) pend = cb;
+                    if (gl == j) pend = c;
                     if (j == G - 1 || sg + 1 == s1) {
                         const uint64_t first = sg - j;
                         if (gl <= j) args.out[first + gl] = pend;
@@ -538,23 +546,18 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                             }
                             klen = n;
                         }
-                        const uint32_t a = (uint32_t)__shfl((int)acc, (int)leader, 64);
                         uint32_t part = 0;
 #pragma unroll
-                        for (int w = 0; w < kFoldW; ++w) part ^= ((a >> (gl * kFoldW + w)) & 1u) ? kb[w] : 0u;
-#pragma unroll
-                        for (int o = G / 2; o > 0; o >>= 1) part ^= (uint32_t)__shfl_xor((int)part, o, 64);
-                        acc = part ^ c;  // valid on the group's first lane, where c is
+                        for (int w = 0; w < kFoldW; ++w) part ^= ((acc >> (gl * kFoldW + w)) & 1u) ? kb[w] : 0u;
+                        acc = group_xor<G>(part) ^ c;  // acc and c are valid on every lane of the group
                     } else {
                         // 4-lane groups (segments < 2 KiB): 8 basis words per
-                        // lane would spill; the first lane multiplies.
-                        if (gl == 0) {
-                            if (n != klen) {
-                                kb[0] = xpow8_tab(n, pt);
-                                klen = n;
-                            }
-                            acc = mulmod(acc, kb[0]) ^ c;
+                        // lane would spill; every lane multiplies.
+                        if (n != klen) {
+                            kb[0] = xpow8_tab(n, pt);
+                            klen = n;
                         }
+                        acc = mulmod(acc, kb[0]) ^ c;
                     }
                 }
             }
@@ -744,9 +747,7 @@ __device__ __forceinline__ uint32_t group_reduce_f(uint32_t pc, uint32_t d, cons
                                 R[768 + (pc >> 24)], 0u);
         pc = ((d >> k) & 1u) ? m : pc;
     }
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) pc ^= (uint32_t)__shfl_xor((int)pc, o, 64);
-    return pc;
+    return group_xor<G>(pc);
 }
 
 template <int G>

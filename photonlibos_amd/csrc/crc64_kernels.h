@@ -216,13 +216,7 @@ template <int G>
 __device__ __forceinline__ uint64_t group_reduce64(uint64_t pc, uint32_t d, const uint32_t* lds) {
     constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
     pc = shift64<LOG2G>(pc, d, lds);
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)pc, o, 64);
-        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(pc >> 32), o, 64);
-        pc ^= ((uint64_t)hi32 << 32) | lo32;
-    }
-    return pc;
+    return ((uint64_t)group_xor<G>((uint32_t)(pc >> 32)) << 32) | group_xor<G>((uint32_t)pc);
 }
 
 // Any pointer / length / seed (iovec batches, ragged and unaligned buffers).
