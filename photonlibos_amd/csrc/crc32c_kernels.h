@@ -508,9 +508,16 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             if (!args.out) {
                 // No per-segment CRCs wanted: chain through the seed
                 // (crc32c_extend(seg, n, acc), Crc32Hasher::extend_hash).
-                for (uint64_t sg = s0; sg < s1; ++sg)
-                    acc = buffer_crc<G, U>(lds, static_cast<const uint8_t*>(args.iov[sg].base), args.iov[sg].len,
-                                           acc, gl, la);
+                photon_crc_iovec nx = {nullptr, 0};
+                if (s0 < s1) nx = args.iov[s0];
+                for (uint64_t sg = s0; sg < s1; ++sg) {
+                    // The next segment's descriptor is loaded before this
+                    // segment's rows (unconditionally: the last one re-reads
+                    // itself), so it has arrived when the next segment starts.
+                    const photon_crc_iovec cur = nx;
+                    nx = args.iov[sg + 1 < s1 ? sg + 1 : sg];
+                    acc = buffer_crc<G, U>(lds, static_cast<const uint8_t*>(cur.base), cur.len, acc, gl, la);
+                }
             } else {
                 // Per-segment CRCs (seed 0) and the fold acc = acc * K ^ c,
                 // K = x^(8 len) (crc32c_combine, crc.cpp:393-405). The multiply
@@ -526,9 +533,13 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                 // the CRC of segment s0 + j (mod G), and the group stores G
                 // consecutive CRCs with one coalesced store.
                 uint32_t pend = 0;
+                photon_crc_iovec nx = {nullptr, 0};
+                if (s0 < s1) nx = args.iov[s0];
                 for (uint64_t sg = s0; sg < s1; ++sg) {
-                    const uint8_t* p = static_cast<const uint8_t*>(args.iov[sg].base);
-                    const uint64_t n = args.iov[sg].len;
+                    const photon_crc_iovec cur = nx;  // (prefetched as above)
+                    nx = args.iov[sg + 1 < s1 ? sg + 1 : sg];
+                    const uint8_t* p = static_cast<const uint8_t*>(cur.base);
+                    const uint64_t n = cur.len;
                     const uint32_t c = buffer_crc<G, U>(lds, p, n, 0u, gl, la);
                     const uint32_t j = (uint32_t)((sg - s0) & (G - 1));
                     if (gl == j) pend = c;
