@@ -240,6 +240,7 @@ int scratch_free(void* p, hipStream_t st) {
 LaneConsts make_lane_consts(int g, int b) {
     LaneConsts c;
     c.kshift = xpow(8ull * 16ull * (uint64_t)b * (uint64_t)g);
+    mul_basis(c.kshift, c.sbasis);
     for (int k = 0; k < 6; ++k) mul_basis(xpow((128ull * (uint64_t)b) << k), c.basis[k]);
     for (int d = 0; d < 8; ++d) mul_basis(xpow(32ull + 128ull * (uint64_t)d), c.fbasis[d]);
     return c;
@@ -418,8 +419,7 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
 LaneConsts64 make_lane_consts64(int g) {
     LaneConsts64 c;
     c.kshift = xpow64(8ull * 16ull * (uint64_t)g);
-    for (int k = 0; k < 6; ++k)
-        for (int i = 0; i < 64; ++i) c.basis[k][i] = mulmod64(1ull << i, xpow64(128ull << k));
+    for (int i = 0; i < 64; ++i) c.sbasis[i] = mulmod64(1ull << i, c.kshift);
     return c;
 }
 

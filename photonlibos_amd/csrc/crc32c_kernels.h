@@ -45,6 +45,7 @@ constexpr int kWaves = kBlock / 64;
 // Kernel constants computed on the host (gf2.h) per lanes-per-buffer G.
 struct LaneConsts {
     uint32_t kshift;           // x^(8*16*G) mod P: one row of the lane's column
+    uint32_t sbasis[32];       // basis of kshift (S table entries by select-XOR)
     uint32_t basis[6][32];     // basis of x^(128 * 2^k) mod P, k = 0..5
     uint32_t fbasis[8][32];    // basis of x^(32 + 128 * d) mod P, d < 8 (F_d tables)
 };
@@ -217,6 +218,30 @@ __device__ __forceinline__ uint4 load16(const uint8_t* p) {
 
 __device__ __forceinline__ uint8_t load8(const uint8_t* p) { return *(g_u8*)p; }
 
+// Basis of a multiplication by a fixed constant (image of every register bit),
+// computed at compile time: a table entry (b << 8t) * K is then the XOR of 8
+// basis words (16 VALU) instead of a 32-step bit-serial multiply per entry --
+// the prologue of every launch builds 1024 D and 1024 S entries per workgroup.
+struct Basis32 {
+    uint32_t w[32];
+};
+constexpr Basis32 make_basis32(uint32_t k) {
+    Basis32 r{};
+    for (int i = 0; i < 32; ++i) r.w[i] = mulmod(1u << i, k);
+    return r;
+}
+__constant__ const Basis32 kBasisD32 = make_basis32(kPoly);  // x^32 mod P
+
+// (b << 8t) * K from its basis: byte b selects 8 of the 32 words (t is
+// uniform per wavefront, so the basis reads are scalar).
+template <typename B>
+__device__ __forceinline__ uint32_t basis_entry(const B& basis, uint32_t t, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & basis[8 * t + j];
+    return r;
+}
+
 // Build the D and S tables in LDS (every workgroup; 1024 threads = one entry of
 // each table per thread).
 // FG = 0: R_k lane-combine tables; FG = 4 or 8: F_d finish tables for G = FG.
@@ -247,9 +272,8 @@ __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc
             lds[kFBase / 4 + b * 64 + w] = r;
         }
     }
-    const uint32_t v = b << (8 * t);
-    const uint32_t dv = mulmod(v, 0x82f63b78u);  // x^32 mod P
-    const uint32_t sv = mulmod(v, kc.kshift);
+    const uint32_t dv = basis_entry(kBasisD32.w, t, b);  // (b << 8t) * x^32
+    const uint32_t sv = basis_entry(kc.sbasis, t, b);    // (b << 8t) * x^(8*16*G)
     const uint32_t base = ((b << 8) + (t << 5)) >> 2;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {

@@ -31,7 +31,7 @@ constexpr uint32_t k64LdsBytes = k64RBase + 6u * 16u * 16u * 8u;  // 143360 B
 
 struct LaneConsts64 {
     uint64_t kshift;           // x^(8*16*G) mod P64
-    uint64_t basis[6][64];     // basis of x^(128 * 2^k)
+    uint64_t sbasis[64];       // basis of kshift (S64 entries by select-XOR)
 };
 
 struct SeedConsts64 {
@@ -175,13 +175,37 @@ __device__ __forceinline__ uint64_t head_word64(uint64_t w, int off, int s0, uin
     return w;
 }
 
+// Compile-time basis of x^64 mod P64 (= the reflected polynomial): D64
+// entries by select-XOR of 8 words instead of a 64-step bit-serial multiply
+// (which made the prologue ~15 us longer than CRC32C's per launch).
+struct Basis64 {
+    uint64_t w[64];
+};
+constexpr Basis64 make_basis64(uint64_t k) {
+    Basis64 r{};
+    for (int i = 0; i < 64; ++i) r.w[i] = mulmod64(1ull << i, k);
+    return r;
+}
+__constant__ const Basis64 kBasisD64 = make_basis64(kPoly64);
+// Lane-combine multipliers x^(128*2^k), k < 6 (independent of G).
+__constant__ const Basis64 kBasisR64[6] = {make_basis64(xpow64(128)),  make_basis64(xpow64(256)),
+                                           make_basis64(xpow64(512)),  make_basis64(xpow64(1024)),
+                                           make_basis64(xpow64(2048)), make_basis64(xpow64(4096))};
+
+template <typename B>
+__device__ __forceinline__ uint64_t basis_entry64(const B& basis, uint32_t t, uint32_t b) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r ^= (0ull - ((b >> j) & 1u)) & basis[8 * t + j];
+    return r;
+}
+
 __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64& kc) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t e = tid; e < 2048u; e += kBlock) {
-        const uint32_t t = e >> 8, b = e & 255u;
-        const uint64_t v = (uint64_t)b << (8 * t);
-        const uint2 dv = u2of(mulmod64(v, kPoly64 /* x^64 mod P64 = the reflected polynomial */));
-        const uint2 sv = u2of(mulmod64(v, kc.kshift));
+        const uint32_t t = e >> 8, b = e & 255u;  // t is uniform per wavefront
+        const uint2 dv = u2of(basis_entry64(kBasisD64.w, t, b));
+        const uint2 sv = u2of(basis_entry64(kc.sbasis, t, b));
         const uint32_t base = (b << 8) + (t << 5);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -194,7 +218,7 @@ __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64
         const uint32_t k = e >> 8, m = (e >> 4) & 15u, v = e & 15u;
         uint64_t r = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & kc.basis[k][4 * m + j];
+        for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & kBasisR64[k].w[4 * m + j];
         *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64RBase + e * 8u) = u2of(r);
     }
     __syncthreads();

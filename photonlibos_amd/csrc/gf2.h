@@ -9,9 +9,9 @@
 #include <stdint.h>
 
 #ifdef __HIPCC__
-#define PCRC_HD __host__ __device__ inline
+#define PCRC_HD __host__ __device__ constexpr inline
 #else
-#define PCRC_HD inline
+#define PCRC_HD constexpr inline
 #endif
 
 namespace pcrc {

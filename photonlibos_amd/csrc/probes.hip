@@ -199,6 +199,7 @@ int probe_crc_wave_times(const void* base, uint64_t nbytes, uint64_t count, uint
     using namespace pcrc;
     LaneConsts kc;
     kc.kshift = xpow(8ull * 16ull * (uint64_t)g);
+    mul_basis(kc.kshift, kc.sbasis);
     for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), kc.basis[k]);
     BatchArgs a{};
     a.base = static_cast<const uint8_t*>(base);
@@ -245,6 +246,7 @@ int probe_crc_ablate(const void* base, uint64_t nbytes, uint64_t count, uint32_t
     constexpr int G = 32;
     LaneConsts kc;
     kc.kshift = xpow(8ull * 16ull * G);
+    mul_basis(kc.kshift, kc.sbasis);
     for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), kc.basis[k]);
     UniformArgs a{static_cast<const uint8_t*>(base), nbytes, nbytes / (16ull * G), count, out};
     const uint64_t waves = (count + 1) / 2;
@@ -272,8 +274,7 @@ int probe_crc64_ablate(const void* base, uint64_t nbytes, uint64_t count, uint64
     constexpr int G = 32;
     LaneConsts64 kc;
     kc.kshift = xpow64(8ull * 16ull * G);
-    for (int k = 0; k < 6; ++k)
-        for (int i = 0; i < 64; ++i) kc.basis[k][i] = mulmod64(1ull << i, xpow64(128ull << k));
+    for (int i = 0; i < 64; ++i) kc.sbasis[i] = mulmod64(1ull << i, kc.kshift);
     Uniform64Args a{static_cast<const uint8_t*>(base), nbytes, nbytes / (16ull * G), count, out, 0};
     const uint64_t waves = (count + 1) / 2;
     uint64_t grid = (waves + 15) / 16;
