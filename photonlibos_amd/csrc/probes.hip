@@ -67,7 +67,7 @@ __global__ __launch_bounds__(1024) void rows_kernel(const uint8_t* base, uint64_
 // workgroups, nt loads. What does a buffer size / lane-group geometry read at?
 template <int G, int U>
 __global__ __launch_bounds__(1024) void group_rows_kernel(const uint8_t* base, uint64_t stride, uint64_t rows,
-                                                         uint64_t count, uint32_t* sink) {
+                                                         uint64_t count, uint32_t* sink, const uint64_t* slot) {
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1), grp = lane / G;
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(1024) void group_rows_kernel(const uint8_t* base, u
     for (uint64_t wv = blockIdx.x * 16ull + wave; wv * GPW < count; wv += nwaves) {
         const uint64_t b = wv * GPW + grp;
         if (b >= count) continue;
-        const uint8_t* p = base + b * stride + 16 * gl;
+        const uint8_t* p = base + (slot ? slot[b] : b) * stride + 16 * gl;
         uint64_t r = 0;
         u32x4 cur[U];
 #pragma unroll
@@ -294,18 +294,28 @@ int probe_crc64_ablate(const void* base, uint64_t nbytes, uint64_t count, uint64
 }
 
 // group_rows_kernel<G, U> over count buffers of rows*16*G bytes (rows % U == 0).
-int probe_group_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink, int blocks,
-                     int g, int u, void* stream) {
+// slot (optional, device): buffer i is at base + slot[i] * stride (the C5
+// layout: segments in a permuted slot pool).
+int probe_group_rows_slots(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink,
+                           int blocks, int g, int u, const uint64_t* slot, void* stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint8_t* b = static_cast<const uint8_t*>(base);
-#define GR(GG, UU) hipLaunchKernelGGL((group_rows_kernel<GG, UU>), dim3(blocks), dim3(1024), 0, s, b, stride, rows, count, sink)
-    if (u == 8) {
+#define GR(GG, UU) \
+    hipLaunchKernelGGL((group_rows_kernel<GG, UU>), dim3(blocks), dim3(1024), 0, s, b, stride, rows, count, sink, slot)
+    if (u == 2) {
+        switch (g) { case 4: GR(4, 2); break; case 8: GR(8, 2); break; case 16: GR(16, 2); break; case 32: GR(32, 2); break; default: GR(64, 2); }
+    } else if (u == 8) {
         switch (g) { case 4: GR(4, 8); break; case 8: GR(8, 8); break; case 16: GR(16, 8); break; case 32: GR(32, 8); break; default: GR(64, 8); }
     } else {
         switch (g) { case 4: GR(4, 4); break; case 8: GR(8, 4); break; case 16: GR(16, 4); break; case 32: GR(32, 4); break; default: GR(64, 4); }
     }
 #undef GR
     return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int probe_group_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink, int blocks,
+                     int g, int u, void* stream) {
+    return probe_group_rows_slots(base, stride, rows, count, sink, blocks, g, u, nullptr, stream);
 }
 
 int probe_read_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink, int blocks,
