@@ -38,7 +38,8 @@ def timed(fn, reps=20):
     return a.elapsed_time(b) / reps
 
 
-SHAPES = {"c3": (4096, 1 << 20, (8, 16, 32)), "c2": (65536, 65536, (8, 32, 64)), "c5": (8192, 1 << 19, (8, 16))}
+SHAPES = {"c3": (4096, 1 << 20, (8, 16, 32)), "c2": (65536, 65536, (8, 16, 32, 64)), "c5": (8192, 1 << 19, (8, 16)),
+          "c4": (1 << 20, 4096, (16, 32, 64))}
 wanted = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c3", "c2"]
 
 
