@@ -231,6 +231,8 @@ constexpr Basis32 make_basis32(uint32_t k) {
     return r;
 }
 __constant__ const Basis32 kBasisD32 = make_basis32(kPoly);  // x^32 mod P
+static_assert(make_basis32(kPoly).w[31] == kPoly, "bit 31 is x^0: its image under x^32 is x^32 mod P");
+static_assert(make_basis32(kOne).w[7] == (1u << 7), "multiplying by x^0 keeps every bit");
 
 // (b << 8t) * K from its basis: byte b selects 8 of the 32 words (t is
 // uniform per wavefront, so the basis reads are scalar).

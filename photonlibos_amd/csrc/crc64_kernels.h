@@ -187,6 +187,7 @@ constexpr Basis64 make_basis64(uint64_t k) {
     return r;
 }
 __constant__ const Basis64 kBasisD64 = make_basis64(kPoly64);
+static_assert(make_basis64(kPoly64).w[63] == kPoly64, "bit 63 is x^0: its image under x^64 is x^64 mod P64");
 // Lane-combine multipliers x^(128*2^k), k < 6 (independent of G).
 __constant__ const Basis64 kBasisR64[6] = {make_basis64(xpow64(128)),  make_basis64(xpow64(256)),
                                            make_basis64(xpow64(512)),  make_basis64(xpow64(1024)),

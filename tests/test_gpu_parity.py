@@ -41,7 +41,7 @@ MSG_MODES = [0, 1, 2]
 
 # Batch kernel variants: 4 = the generic kernel (default), 0 = the fused
 # 4-row kernel (a tuning option).
-VARIANTS = [4, 0]
+VARIANTS = [-1, 2, 4, 0]  # rows per step: auto (the product default), 2, 4, fused kernel
 
 
 STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (1, 4, 1), (1, 4, 2), (1, 2, 2),
