@@ -13,6 +13,7 @@ One "step" = one pass of the hot path over one batch (BASELINE.json configs):
   c5_chain: the C5 shape, one CRC per message chained through the seed
       (Crc32Hasher::extend_hash, rpc/serialize.h:244-251), no segment CRCs
   c2_crc64: the C2 shape with CRC-64/ECMA (next row f2)
+  c3_crc64: the C3 shape with CRC-64/ECMA
   --h2d / --rpc-batch / --rpc-latency / --file-records: host-memory rates
       for DESIGN.md, never `value`.
 
@@ -65,6 +66,8 @@ CONFIGS = {
                               "segments through the seed)"),
     "c2_crc64": dict(kind="strided64", nbytes=65536, count=65536,
                      workload="C2 shape, CRC-64/ECMA (next row): 65536 x 64 KiB, device-resident, per GPU"),
+    "c3_crc64": dict(kind="strided64", nbytes=4096, count=1 << 20,
+                     workload="C3 shape, CRC-64/ECMA (next row): 1048576 x 4 KiB, device-resident, per GPU"),
 }
 
 
