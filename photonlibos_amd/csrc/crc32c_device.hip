@@ -1014,7 +1014,7 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
     const int g = lanes ? lanes : choose_lanes(8192);
     const uint64_t gpw = 64 / (uint64_t)g;
     // (With per-segment CRCs requested the fused form folds with the group-
-    // spread multiply of crc32c_batch_kernel<G, U, true>.)
+    // spread multiply of crc32c_batch_kernel<G, U, 2>.)
     const int mode = g_msg_mode.load(std::memory_order_relaxed);
     const bool fused = mode == 1 || (mode == 0 && nmsg >= 4096 * gpw && nseg <= 64 * nmsg);
     if (fused) {
@@ -1029,8 +1029,13 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
         uint64_t grid = ((nmsg + gpw - 1) / gpw + kWaves - 1) / kWaves;
         if (grid > (uint64_t)cus) grid = cus;
         const LaneConsts& kc = lane_consts(g);
-#define LM(GG, UU) \
-    hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU, true>), dim3(grid), dim3(kBlock), 0, st, a, kc, pow_table())
+#define LM(GG, UU)                                                                                            \
+    do {                                                                                                      \
+        if (a.out)                                                                                            \
+            hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU, 2>), dim3(grid), dim3(kBlock), 0, st, a, kc, pow_table()); \
+        else                                                                                                  \
+            hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU, 1>), dim3(grid), dim3(kBlock), 0, st, a, kc, pow_table()); \
+    } while (0)
 #define LMG(UU)                     \
     switch (g) {                    \
         case 64: LM(64, UU); break; \

@@ -65,7 +65,7 @@ struct BatchArgs {
     const uint32_t* seeds;     // optional
     uint32_t* out;
     uint32_t seed0;
-    // Message mode (crc32c_batch_kernel<G, U, true>): unit m = message m,
+    // Message mode (crc32c_batch_kernel<G, U, 1|2>): unit m = message m,
     // segments iov[msg_start[m] .. msg_start[m+1]); out[] = per-segment CRCs
     // (seed 0), msg_out[m] = the chained CRC from seed_m (seeds[m] or seed0).
     const uint64_t* msg_start;
@@ -496,7 +496,11 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
     return buf_finish<G>(lds, g, pc, p, n, seed, gl, la);
 }
 
-template <int G, int U = 4, bool MSG = false>
+// MSG: 0 = buffer batch, 1 = messages chained through the seed, 2 = messages
+// with per-segment CRCs + fold (separate instantiations: the two message
+// forms in one kernel shared one register allocation, and each is faster
+// compiled alone).
+template <int G, int U = 4, int MSG = 0>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[(G <= 8 ? kLdsBytesF : kLdsBytes) / 4];
     build_tables<G <= 8 ? G : 0>(lds, kc);
@@ -531,7 +535,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                 s1 = args.msg_start[m + 1];
                 if (args.seeds) acc = args.seeds[m];
             }
-            if (!args.out) {
+            if constexpr (MSG == 1) {
                 // No per-segment CRCs wanted: chain through the seed
                 // (crc32c_extend(seg, n, acc), Crc32Hasher::extend_hash).
                 photon_crc_iovec nx = {nullptr, 0};
@@ -558,21 +562,10 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                 // front of the next segment's loads): lane j of the group keeps
                 // the CRC of segment s0 + j (mod G), and the group stores G
                 // consecutive CRCs with one coalesced store.
-                uint32_t pend = 0;
-                photon_crc_iovec nx = {nullptr, 0};
-                if (s0 < s1) nx = args.iov[s0];
-                for (uint64_t sg = s0; sg < s1; ++sg) {
-                    const photon_crc_iovec cur = nx;  // (prefetched as above)
-                    nx = args.iov[sg + 1 < s1 ? sg + 1 : sg];
-                    const uint8_t* p = static_cast<const uint8_t*>(cur.base);
-                    const uint64_t n = cur.len;
-                    const uint32_t c = buffer_crc<G, U>(lds, p, n, 0u, gl, la);
-                    const uint32_t j = (uint32_t)((sg - s0) & (G - 1));
-                    if (gl == j) pend = c;
-                    if (j == G - 1 || sg + 1 == s1) {
-                        const uint64_t first = sg - j;
-                        if (gl <= j) args.out[first + gl] = pend;
-                    }
+                // The fold of segment k runs after segment k+1's first loads are
+                // issued (its DPP reduction and select-XORs then overlap them
+                // instead of delaying them).
+                auto fold = [&](uint32_t c, uint64_t n) {
                     if constexpr (G >= 8) {
                         if (n != klen) {
                             const uint32_t kn = xpow8_tab(n, pt);
@@ -596,7 +589,34 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                         }
                         acc = mulmod(acc, kb[0]) ^ c;
                     }
+                };
+                uint32_t pend = 0, cprev = 0;
+                uint64_t nprev = 0;
+                bool have = false;
+                photon_crc_iovec nx = {nullptr, 0};
+                if (s0 < s1) nx = args.iov[s0];
+                for (uint64_t sg = s0; sg < s1; ++sg) {
+                    const photon_crc_iovec cur = nx;  // (prefetched as above)
+                    nx = args.iov[sg + 1 < s1 ? sg + 1 : sg];
+                    const uint8_t* p = static_cast<const uint8_t*>(cur.base);
+                    const uint64_t n = cur.len;
+                    const BufGeo g = buf_geo<G>(p, n, gl);
+                    BufPre<U> pre;
+                    buf_preload<G, U>(g, gl, pre);
+                    if (have) fold(cprev, nprev);
+                    const uint32_t pc = buf_body<G, U>(lds, g, pre, 0u, gl, la);
+                    const uint32_t c = buf_finish<G>(lds, g, pc, p, n, 0u, gl, la);
+                    const uint32_t j = (uint32_t)((sg - s0) & (G - 1));
+                    if (gl == j) pend = c;
+                    if (j == G - 1 || sg + 1 == s1) {
+                        const uint64_t first = sg - j;
+                        if (gl <= j) args.out[first + gl] = pend;
+                    }
+                    cprev = c;
+                    nprev = n;
+                    have = true;
                 }
+                if (have) fold(cprev, nprev);
             }
             if (active && gl == 0) args.msg_out[m] = acc;
         }

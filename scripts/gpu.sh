@@ -11,6 +11,8 @@
 #   scripts/gpu.sh probe SCRIPT [ARGS]   python scripts/SCRIPT ARGS (bench-only probes)
 #   scripts/gpu.sh ab LIB ROUNDS CONFIG.. A/B of another build of the library (PHOTON_CRC_LIB=LIB)
 #                                        against the in-tree one, alternating, fresh process each
+#                                        (a run whose self-check fails -- ablation builds -- is
+#                                        recorded with "ok": false, not a failure)
 # Several commands chain with "::", e.g.
 #   scripts/gpu.sh tests :: bench --steps 20 --warmup 5 :: prof c2
 set -o pipefail
@@ -58,7 +60,8 @@ run_one() {
           for side in new old; do
             local envv=""; [ $side = old ] && envv="PHOTON_CRC_LIB=$lib"
             env $envv timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-live-pmc --no-shape64 \
-              > $O/ab_tmp.json 2>> $O/ab.err || { echo "ab $c $side failed"; tail -5 $O/ab.err; return 1; }
+              > $O/ab_tmp.json 2>> $O/ab.err || [ "$(wc -l < $O/ab_tmp.json)" -gt 0 ] \
+              || { echo "ab $c $side failed"; tail -5 $O/ab.err; return 1; }  # (self-check false still prints its line: ablation builds)
             python -c "import json,sys; d=json.loads(open('$O/ab_tmp.json').read().splitlines()[-1]); r=d['roofline']; print(json.dumps({'round': $r, 'config': '$c', 'side': '$side', 'value': d['value'], 'frac_kernel': r['frac_kernel'], 'frac_steady': r['frac_steady_median_launch'], 'ok': d['self_check']}))" | tee -a $O/ab.jsonl
           done
         done
