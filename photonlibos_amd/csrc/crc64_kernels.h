@@ -28,6 +28,19 @@ constexpr uint32_t k64SBase = 65536u;
 // (16 positions x 16 values x 8 B = 2 KiB per k): used once per buffer.
 constexpr uint32_t k64RBase = 131072u;
 constexpr uint32_t k64LdsBytes = k64RBase + 6u * 16u * 16u * 8u;  // 143360 B
+// Finish tables of the batch kernel (in place of R64_k): the lane's partial Q
+// (= P * x^-64) times x^(64 + 128 d), d = 16-byte blocks after its last block,
+// d < G, split d = 8 dh + dl:
+//   A_dl: p -> p * x^(64 + 128 dl), dl < 8 (Q -> P and the low lane shift)
+//   B_dh: p -> p * x^(1024 dh), 1 <= dh < G/8
+// nibble-sliced, 2 KiB per table, layout [value v][position t] (entry at
+// v*128 + t*8): lane l reads position t = (i + l) % 16 in lookup i, so a
+// 32-lane half hits bank pair (v%2)*32 + 2t: at most 2-way conflicts. One (G
+// <= 8) or two dependent 16-lookup levels instead of a D step plus log2(G)
+// 16-lookup R64 levels (88 lookups at G = 32, 56 at G = 8).
+constexpr uint32_t k64FBase = 131072u;
+constexpr uint32_t k64FBBase = k64FBase + 8u * 2048u;
+constexpr uint32_t k64FLdsBytes = k64FBBase + 7u * 2048u;  // 161792 B of the 163840
 
 struct LaneConsts64 {
     uint64_t kshift;           // x^(8*16*G) mod P64
@@ -193,6 +206,17 @@ __constant__ const Basis64 kBasisR64[6] = {make_basis64(xpow64(128)),  make_basi
                                            make_basis64(xpow64(512)),  make_basis64(xpow64(1024)),
                                            make_basis64(xpow64(2048)), make_basis64(xpow64(4096))};
 
+// Finish multipliers (A_dl, B_dh above).
+__constant__ const Basis64 kBasisA64[8] = {
+    make_basis64(xpow64(64)),       make_basis64(xpow64(64 + 128)),     make_basis64(xpow64(64 + 2 * 128)),
+    make_basis64(xpow64(64 + 3 * 128)), make_basis64(xpow64(64 + 4 * 128)), make_basis64(xpow64(64 + 5 * 128)),
+    make_basis64(xpow64(64 + 6 * 128)), make_basis64(xpow64(64 + 7 * 128))};
+__constant__ const Basis64 kBasisB64[7] = {make_basis64(xpow64(1024)),     make_basis64(xpow64(2 * 1024)),
+                                           make_basis64(xpow64(3 * 1024)), make_basis64(xpow64(4 * 1024)),
+                                           make_basis64(xpow64(5 * 1024)), make_basis64(xpow64(6 * 1024)),
+                                           make_basis64(xpow64(7 * 1024))};
+static_assert(xpow64(64) == kPoly64, "x^64 mod P64 is the reflected polynomial");
+
 template <typename B>
 __device__ __forceinline__ uint64_t basis_entry64(const B& basis, uint32_t t, uint32_t b) {
     uint64_t r = 0;
@@ -201,6 +225,8 @@ __device__ __forceinline__ uint64_t basis_entry64(const B& basis, uint32_t t, ui
     return r;
 }
 
+// FIN = 0: R64_k lane-combine tables; FIN = G: the finish tables A_dl, B_dh.
+template <int FIN = 0>
 __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64& kc) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t e = tid; e < 2048u; e += kBlock) {
@@ -214,13 +240,27 @@ __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64
             *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64SBase + base + r * 8) = sv;
         }
     }
-    // R64_k[m][v] = (v << 4m) * x^(128*2^k): XOR of the basis words of v's bits.
-    for (uint32_t e = tid; e < 6u * 256u; e += kBlock) {
-        const uint32_t k = e >> 8, m = (e >> 4) & 15u, v = e & 15u;
-        uint64_t r = 0;
+    if constexpr (FIN == 0) {
+        // R64_k[m][v] = (v << 4m) * x^(128*2^k): XOR of the basis words of v's bits.
+        for (uint32_t e = tid; e < 6u * 256u; e += kBlock) {
+            const uint32_t k = e >> 8, m = (e >> 4) & 15u, v = e & 15u;
+            uint64_t r = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & kBasisR64[k].w[4 * m + j];
-        *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64RBase + e * 8u) = u2of(r);
+            for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & kBasisR64[k].w[4 * m + j];
+            *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64RBase + e * 8u) = u2of(r);
+        }
+    } else {
+        // Table k < 8: A_k; 8 <= k < 7 + FIN/8: B_(k-7). Entry (v, t) = (v << 4t) * K.
+        constexpr uint32_t ntab = 8u + (FIN > 8 ? FIN / 8 - 1 : 0);
+        for (uint32_t e = tid; e < ntab * 256u; e += kBlock) {
+            const uint32_t k = e >> 8, t = (e >> 4) & 15u, v = e & 15u;
+            const uint64_t* w = k < 8 ? kBasisA64[k].w : kBasisB64[k - 8].w;
+            uint64_t r = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r ^= (0ull - ((v >> j) & 1u)) & w[4 * t + j];
+            *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64FBase + k * 2048u + v * 128u + t * 8u) =
+                u2of(r);
+        }
     }
     __syncthreads();
 }
@@ -236,19 +276,43 @@ __device__ __forceinline__ uint64_t shift64(uint64_t pc, uint32_t d, const uint3
     return pc;
 }
 
-// Shift lane partials by x^(128*d) and XOR-reduce over the G lanes.
+// x * K through one nibble-sliced finish table at byte offset `base` (16
+// lookups; lane l reads position (i + l) % 16 in lookup i).
+__device__ __forceinline__ uint64_t nib_mul64(uint64_t x, const uint32_t* lds, uint32_t base, uint32_t lane) {
+    const uint32_t r = lane & 15u;
+    const uint32_t sh = 4u * r;
+    const uint64_t xr = (x >> sh) | (x << ((64u - sh) & 63u));  // nibble i of xr = nibble (i + r) % 16 of x
+    uint2 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t half = i < 8 ? (uint32_t)xr : (uint32_t)(xr >> 32);
+        const uint32_t nib = (half >> (4 * (i & 7))) & 15u;
+        v[i] = lds_u2(lds, base + nib * 128u + (((uint32_t)i + r) & 15u) * 8u);
+    }
+    uint32_t lo = xor3(xor3(v[0].x, v[1].x, v[2].x), xor3(v[3].x, v[4].x, v[5].x), xor3(v[6].x, v[7].x, v[8].x));
+    uint32_t hi = xor3(xor3(v[0].y, v[1].y, v[2].y), xor3(v[3].y, v[4].y, v[5].y), xor3(v[6].y, v[7].y, v[8].y));
+    lo = xor3(lo, xor3(v[9].x, v[10].x, v[11].x), xor3(v[12].x, v[13].x, v[14].x)) ^ v[15].x;
+    hi = xor3(hi, xor3(v[9].y, v[10].y, v[11].y), xor3(v[12].y, v[13].y, v[14].y)) ^ v[15].y;
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Q * x^(64 + 128 d), d < G (the finish tables; every lane runs every level).
 template <int G>
-__device__ __forceinline__ uint64_t group_reduce64(uint64_t pc, uint32_t d, const uint32_t* lds) {
-    constexpr int LOG2G = G == 64 ? 6 : G == 32 ? 5 : G == 16 ? 4 : G == 8 ? 3 : 2;
-    pc = shift64<LOG2G>(pc, d, lds);
-    return ((uint64_t)group_xor<G>((uint32_t)(pc >> 32)) << 32) | group_xor<G>((uint32_t)pc);
+__device__ __forceinline__ uint64_t finish64(uint2 q, uint32_t d, const uint32_t* lds, uint32_t lane) {
+    uint64_t x = nib_mul64(u64of(q), lds, k64FBase + (d & 7u) * 2048u, lane);
+    if constexpr (G > 8) {
+        const uint32_t dh = d >> 3;
+        const uint64_t y = nib_mul64(x, lds, k64FBBase + (dh ? dh - 1u : 0u) * 2048u, lane);
+        x = dh ? y : x;
+    }
+    return x;
 }
 
 // Any pointer / length / seed (iovec batches, ragged and unaligned buffers).
 template <int G>
 __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
-    build_tables64(lds, kc);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+    build_tables64<G>(lds, kc);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp = lane / G;
@@ -339,8 +403,9 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
                 column_step(cur);
             }
             if (part) pc = sstep64(lds, pc, la, lag16_64(lds, wp, la));
-            pc = dstep64(lds, pc, la);  // Q -> P
-            reg = group_reduce64<G>(u64of(pc), (rlast + G - 1 - gl) & (G - 1), lds);
+            // Q * x^(64 + 128 d) (Q -> P and the shift to the end of the blocks), XOR over the group.
+            const uint64_t f = finish64<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds, lane);
+            reg = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
             if (gl == 0)
                 for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
         }
