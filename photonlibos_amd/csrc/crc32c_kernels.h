@@ -39,6 +39,18 @@ constexpr uint32_t kLdsBytes = kRBase + kRBytes;             // 90112 B of the 1
 // G = 4: two groups per q, told apart by r2): 32 distinct banks, no replicas.
 constexpr uint32_t kFBase = kTableBytes;
 constexpr uint32_t kLdsBytesF = kFBase + 65536u;             // 128 KiB
+// Finish tables for G >= 16 (batch kernel, in place of R_k): d = 8*dh + dl,
+//   A_dl: p -> p * x^(32 + 128*dl), dl < 8 (Q -> P and the low lane shift)
+//   B_dh: p -> p * x^(1024*dh),     1 <= dh < G/8
+// 4 byte slices, one replica, [table][t][idx] (4 KiB each): two dependent
+// 4-lookup levels instead of a D step and log2(G) R_k levels (24 lookups in
+// 6 dependent levels at G = 32).
+constexpr uint32_t kABase = kTableBytes;
+constexpr uint32_t kBBase = kABase + 8u * 4096u;
+template <int G>
+constexpr uint32_t lds_bytes_for() {
+    return G <= 8 ? kLdsBytesF : kBBase + (uint32_t)(G / 8 - 1) * 4096u;  // 64: 124 KiB
+}
 constexpr int kBlock = 1024;                   // 16 waves, one workgroup per CU
 constexpr int kWaves = kBlock / 64;
 
@@ -234,6 +246,17 @@ __constant__ const Basis32 kBasisD32 = make_basis32(kPoly);  // x^32 mod P
 static_assert(make_basis32(kPoly).w[31] == kPoly, "bit 31 is x^0: its image under x^32 is x^32 mod P");
 static_assert(make_basis32(kOne).w[7] == (1u << 7), "multiplying by x^0 keeps every bit");
 
+// Finish multipliers of the G >= 16 tables (A_dl, B_dh above).
+__constant__ const Basis32 kBasisA32[8] = {
+    make_basis32(xpow(32)),           make_basis32(xpow(32 + 128)),     make_basis32(xpow(32 + 2 * 128)),
+    make_basis32(xpow(32 + 3 * 128)), make_basis32(xpow(32 + 4 * 128)), make_basis32(xpow(32 + 5 * 128)),
+    make_basis32(xpow(32 + 6 * 128)), make_basis32(xpow(32 + 7 * 128))};
+__constant__ const Basis32 kBasisB32[7] = {make_basis32(xpow(1024)),     make_basis32(xpow(2 * 1024)),
+                                           make_basis32(xpow(3 * 1024)), make_basis32(xpow(4 * 1024)),
+                                           make_basis32(xpow(5 * 1024)), make_basis32(xpow(6 * 1024)),
+                                           make_basis32(xpow(7 * 1024))};
+static_assert(xpow(32) == kPoly, "x^32 mod P is the reflected polynomial");
+
 // (b << 8t) * K from its basis: byte b selects 8 of the 32 words (t is
 // uniform per wavefront, so the basis reads are scalar).
 template <typename B>
@@ -246,12 +269,23 @@ __device__ __forceinline__ uint32_t basis_entry(const B& basis, uint32_t t, uint
 
 // Build the D and S tables in LDS (every workgroup; 1024 threads = one entry of
 // each table per thread).
-// FG = 0: R_k lane-combine tables; FG = 4 or 8: F_d finish tables for G = FG.
+// FG = 0: R_k lane-combine tables; FG = 4 or 8: F_d finish tables for G = FG;
+// FG >= 16: the A_dl / B_dh finish tables for G = FG.
 template <int FG = 0>
 __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc) {
     const uint32_t tid = threadIdx.x;
     const uint32_t t = tid >> 8, b = tid & 255u;
-    if constexpr (FG == 0) {
+    if constexpr (FG >= 16) {
+        // Table k (uniform) and slice t (uniform per wavefront): scalar basis reads.
+#pragma unroll
+        for (int k = 0; k < 8 + FG / 8 - 1; ++k) {
+            const uint32_t* w = k < 8 ? kBasisA32[k].w : kBasisB32[k - 8].w;
+            uint32_t r = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r ^= (0u - ((b >> j) & 1u)) & w[8 * t + j];
+            lds[kABase / 4 + k * 1024 + t * 256 + b] = r;
+        }
+    } else if constexpr (FG == 0) {
         // R_k[t][b] = (b << 8t) * x^(128*B*2^k): XOR of the basis words of b's
         // bits (t is uniform per wavefront, so the basis reads are scalar).
 #pragma unroll
@@ -477,8 +511,16 @@ __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo
         }
         crc = group_xor<G>(xor3(xor3(f[0], f[1], f[2]), f[3], 0u));
     } else {
-        pc = dstep(lds, pc, la);  // Q -> P
-        crc = group_reduce<G>(pc, d, lds);
+        // Q * x^(32 + 128 d): A_(d%8), then B_(d/8) when d >= 8 (every lane
+        // runs both levels; a select keeps the wavefront convergent).
+        const uint32_t* A = lds + kABase / 4 + (d & 7u) * 1024u;
+        uint32_t x = xor3(xor3(A[pc & 0xffu], A[256 + ((pc >> 8) & 0xffu)], A[512 + ((pc >> 16) & 0xffu)]),
+                          A[768 + (pc >> 24)], 0u);
+        const uint32_t dh = d >> 3;
+        const uint32_t* B = lds + kBBase / 4 + (dh ? dh - 1u : 0u) * 1024u;
+        const uint32_t y = xor3(xor3(B[x & 0xffu], B[256 + ((x >> 8) & 0xffu)], B[512 + ((x >> 16) & 0xffu)]),
+                                B[768 + (x >> 24)], 0u);
+        crc = group_xor<G>(dh ? y : x);
     }
     for (const uint8_t* q = g.eb; q < g.e; ++q) crc = bytestep(lds, crc, load8(q), la);
     return crc;
@@ -502,8 +544,8 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
 // compiled alone).
 template <int G, int U = 4, int MSG = 0>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(G <= 8 ? kLdsBytesF : kLdsBytes) / 4];
-    build_tables<G <= 8 ? G : 0>(lds, kc);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
+    build_tables<G>(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
     const uint32_t lane = threadIdx.x & 63u;

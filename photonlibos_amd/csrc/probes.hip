@@ -113,10 +113,10 @@ __global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::Batc
                                                                      uint64_t* t, uint32_t* ticket,
                                                                      uint32_t static_rounds) {
     using namespace pcrc;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
-    build_tables(lds, kc);
+    build_tables<G>(lds, kc);
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
