@@ -12,7 +12,8 @@
 #   scripts/gpu.sh ab LIB ROUNDS CONFIG.. A/B of another build of the library (PHOTON_CRC_LIB=LIB)
 #                                        against the in-tree one, alternating, fresh process each
 #                                        (a run whose self-check fails -- ablation builds -- is
-#                                        recorded with "ok": false, not a failure)
+#                                        recorded with "ok": false, not a failure); AB_NEW=LIB2 puts
+#                                        another build on the "new" side
 # Several commands chain with "::", e.g.
 #   scripts/gpu.sh tests :: bench --steps 20 --warmup 5 :: prof c2
 set -o pipefail
@@ -59,6 +60,7 @@ run_one() {
         for c in "$@"; do
           for side in new old; do
             local envv=""; [ $side = old ] && envv="PHOTON_CRC_LIB=$lib"
+            [ $side = new ] && [ -n "$AB_NEW" ] && envv="PHOTON_CRC_LIB=$AB_NEW"
             env $envv timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-live-pmc --no-shape64 \
               > $O/ab_tmp.json 2>> $O/ab.err || [ "$(wc -l < $O/ab_tmp.json)" -gt 0 ] \
               || { echo "ab $c $side failed"; tail -5 $O/ab.err; return 1; }  # (self-check false still prints its line: ablation builds)
