@@ -4,6 +4,10 @@
 #pragma once
 #include "crc32c_kernels.h"
 
+#ifndef PCRC64_U
+#define PCRC64_U 2  // rows per step of the CRC-64 batch kernel (2 > 4 by 0.9 points on the C2 shape; A/B builds: -DPCRC64_U=4)
+#endif
+
 namespace pcrc {
 
 // ============================================================ CRC-64/ECMA
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp = lane / G;
     constexpr int GPW = 64 / G;
-    constexpr int U = 4;
+    constexpr int U = PCRC64_U;
     const LaneAddr64 la = lane_addr64(lane);
 
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
