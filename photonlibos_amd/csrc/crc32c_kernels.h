@@ -565,6 +565,11 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         constexpr int kFoldW = G >= 32 ? 1 : G >= 8 ? 32 / G : 1;
         uint64_t klen = ~0ull;
         uint32_t kb[kFoldW];
+        // MSG == 2: segment-CRC stores are held back (up to two per lane) and
+        // issued when a third arrives or at the end of the wave's work -- in
+        // C5 (two rounds per wave) all of them after the last payload load.
+        uint32_t *sa0 = nullptr, *sa1 = nullptr;
+        uint32_t sv0 = 0, sv1 = 0;
 #pragma unroll
         for (int w = 0; w < kFoldW; ++w) kb[w] = 0;
         for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.nmsg; wv += nwaves) {
@@ -652,7 +657,23 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                     if (gl == j) pend = c;
                     if (j == G - 1 || sg + 1 == s1) {
                         const uint64_t first = sg - j;
-                        if (gl <= j) args.out[first + gl] = pend;
+                        if (gl <= j) {
+                            // Held back, two per lane, and written when a third
+                            // comes or the wave ends (see sa0 above).
+                            uint32_t* const dst = args.out + first + gl;
+                            if (sa1) {
+                                *sa0 = sv0;
+                                *sa1 = sv1;
+                                sa0 = sa1 = nullptr;
+                            }
+                            if (!sa0) {
+                                sa0 = dst;
+                                sv0 = pend;
+                            } else {
+                                sa1 = dst;
+                                sv1 = pend;
+                            }
+                        }
                     }
                     cprev = c;
                     nprev = n;
@@ -661,6 +682,10 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                 if (have) fold(cprev, nprev);
             }
             if (active && gl == 0) args.msg_out[m] = acc;
+        }
+        if constexpr (MSG == 2) {
+            if (sa0) *sa0 = sv0;
+            if (sa1) *sa1 = sv1;
         }
         return;
     }

@@ -132,6 +132,50 @@ def test_fuzz_messages(dev_pool, oracle, round_):
             got = out.cpu().numpy().view(np.uint32)
             for m, parts in enumerate(msgs):
                 assert got[m] == oracle.extend_chain(parts, seeds[m]), (mode, lanes, m)
+            if seg is not None and iov:
+                segs = seg.cpu().numpy().view(np.uint32)
+                flat = [p for parts in msgs for p in parts]
+                for k, part in enumerate(flat):
+                    assert segs[k] == oracle.crc32c(part, 0), (mode, lanes, k)
+
+
+@pytest.mark.parametrize("lanes", [0, 4, 8, 16, 64])
+def test_message_segment_crcs_many_rounds(dev_pool, oracle, lanes):
+    # Segment CRCs of the one-kernel message form, which holds a lane's
+    # segment-CRC stores back (two per lane) until a third arrives or the wave
+    # ends: messages of up to 40 segments (several store events per lane and
+    # message) and enough messages that every wave runs several rounds.
+    torch, host, d = dev_pool
+    rnd = random.Random(7000 + lanes)
+    ck.set_msg_mode(1)
+    ck.set_lanes_per_buffer(lanes)
+    iov, start, msgs = [], [0], []
+    nmsg = 120000 if lanes in (0, 4, 8) else 3000
+    for m in range(nmsg):
+        k = rnd.choice([1, 2, 3]) if m % 50 else rnd.randrange(17, 41)
+        parts = []
+        for _ in range(k):
+            n = rnd.randrange(0, 600) if lanes in (0, 4, 8) else rnd.randrange(0, 20000)
+            o = rnd.randrange(0, POOL - n)
+            iov.append((d.data_ptr() + o, n))
+            parts.append((o, n))
+        start.append(len(iov))
+        msgs.append(parts)
+    d_iov = torch.from_numpy(np.asarray(iov, np.uint64).view(np.int64)).cuda()
+    d_start = torch.from_numpy(np.asarray(start, np.uint64).view(np.int64)).cuda()
+    out = torch.zeros(nmsg, dtype=torch.int32, device="cuda")
+    seg = torch.full((len(iov),), -1, dtype=torch.int32, device="cuda")
+    ck.batch_msg_n(d_iov, d_start, nmsg, len(iov), seg, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    segs = seg.cpu().numpy().view(np.uint32)
+    k = 0
+    for m, parts in enumerate(msgs):
+        views = [host[o:o + n] for o, n in parts]
+        for v in views:
+            assert segs[k] == oracle.crc32c(v, 0), (lanes, m, k)
+            k += 1
+        assert got[m] == oracle.extend_chain(views, 0), (lanes, m)
 
 
 @pytest.mark.parametrize("round_", range(2 * SOAK))
