@@ -364,6 +364,30 @@ __device__ __forceinline__ uint32_t group_reduce(uint32_t pc, uint32_t d, const 
     return group_xor<G>(pc);
 }
 
+// Up to two pending 4-byte result stores of one lane (see the message kernel).
+struct HeldStores {
+    uint32_t *a0 = nullptr, *a1 = nullptr;
+    uint32_t v0 = 0, v1 = 0;
+    __device__ __forceinline__ void put(uint32_t* dst, uint32_t v) {
+        if (a1) {
+            *a0 = v0;
+            *a1 = v1;
+            a0 = a1 = nullptr;
+        }
+        if (!a0) {
+            a0 = dst;
+            v0 = v;
+        } else {
+            a1 = dst;
+            v1 = v;
+        }
+    }
+    __device__ __forceinline__ void flush() {
+        if (a0) *a0 = v0;
+        if (a1) *a1 = v1;
+    }
+};
+
 __device__ __forceinline__ uint32_t wave_id() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
@@ -565,11 +589,11 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         constexpr int kFoldW = G >= 32 ? 1 : G >= 8 ? 32 / G : 1;
         uint64_t klen = ~0ull;
         uint32_t kb[kFoldW];
-        // MSG == 2: segment-CRC stores are held back (up to two per lane) and
-        // issued when a third arrives or at the end of the wave's work -- in
-        // C5 (two rounds per wave) all of them after the last payload load.
-        uint32_t *sa0 = nullptr, *sa1 = nullptr;
-        uint32_t sv0 = 0, sv1 = 0;
+        // MSG == 2: segment-CRC stores are held back, up to two per lane,
+        // and issued when a third arrives or at the end of the wave's work --
+        // in C5 (two rounds per wave) all of them after the wave's last
+        // payload load. (Holding the message-CRC stores too: neutral.)
+        HeldStores seg_held;
 #pragma unroll
         for (int w = 0; w < kFoldW; ++w) kb[w] = 0;
         for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.nmsg; wv += nwaves) {
@@ -657,23 +681,9 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                     if (gl == j) pend = c;
                     if (j == G - 1 || sg + 1 == s1) {
                         const uint64_t first = sg - j;
-                        if (gl <= j) {
-                            // Held back, two per lane, and written when a third
-                            // comes or the wave ends (see sa0 above).
-                            uint32_t* const dst = args.out + first + gl;
-                            if (sa1) {
-                                *sa0 = sv0;
-                                *sa1 = sv1;
-                                sa0 = sa1 = nullptr;
-                            }
-                            if (!sa0) {
-                                sa0 = dst;
-                                sv0 = pend;
-                            } else {
-                                sa1 = dst;
-                                sv1 = pend;
-                            }
-                        }
+                        // Held back, two per lane, and written when a third
+                        // comes or the wave ends (see HeldStores above).
+                        if (gl <= j) seg_held.put(args.out + first + gl, pend);
                     }
                     cprev = c;
                     nprev = n;
@@ -683,10 +693,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             }
             if (active && gl == 0) args.msg_out[m] = acc;
         }
-        if constexpr (MSG == 2) {
-            if (sa0) *sa0 = sv0;
-            if (sa1) *sa1 = sv1;
-        }
+        seg_held.flush();
         return;
     }
     // (Measured and dropped: software-pipelining the wave's buffers -- the
