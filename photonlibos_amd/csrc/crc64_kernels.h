@@ -19,7 +19,8 @@ namespace pcrc {
 //   D64: x -> x * x^64 mod P64, 8 byte slices x 256 x 4 replicas,
 //        layout [idx][slice t][lane%4] (256 B per index)             64 KiB
 //   S64: P -> P * x^(8*16*G), same layout, at +64 KiB                   64 KiB
-//   lane-combine tables x^(128*2^k), k < 6, nibble-sliced              12 KiB
+//   batch kernel: finish tables A_dl / B_dh, nibble-sliced       16-30 KiB
+//   streaming kernel: lane-combine tables x^(128*2^k), k < 6      12 KiB
 // Conflict-free lookups with only 4 replicas: lane l takes its 8 slices in
 // the rotated order t = (i + q) % 8, q = (l/4) % 8, so in every lookup
 // instruction i the 32 lanes of a group hit 32 distinct (t, replica) bank
@@ -29,7 +30,8 @@ namespace pcrc {
 // with off_i = ((i+q)%8)*32 + (l%4)*8 (+ 1<<16, selected for S).
 constexpr uint32_t k64SBase = 65536u;
 // Lane-combine tables R64_k: p -> p * x^(128*2^k), k < 6, NIBBLE-sliced
-// (16 positions x 16 values x 8 B = 2 KiB per k): used once per buffer.
+// (16 positions x 16 values x 8 B = 2 KiB per k): used once per buffer by the
+// streaming kernel (the batch kernel uses the finish tables below).
 constexpr uint32_t k64RBase = 131072u;
 constexpr uint32_t k64LdsBytes = k64RBase + 6u * 16u * 16u * 8u;  // 143360 B
 // Finish tables of the batch kernel (in place of R64_k): the lane's partial Q
