@@ -355,6 +355,29 @@ def test_host_batch_pipeline(torch_dev, oracle):
         assert np.array_equal(out2.numpy(), out.numpy()), ndev
 
 
+def test_host_batches_zero_length(torch_dev):
+    # nbytes == 0 with count > 0 is legal (crc32c_extend over
+    # 0 bytes returns the seed, crc.cpp:114-117) and once divided by zero in the
+    # host pipeline. Every host batch returns the seeds (or seed0).
+    count = 37
+    host = torch_dev.zeros(64, dtype=torch_dev.uint8, pin_memory=True)
+    seeds = np.arange(1, count + 1, dtype=np.uint32) * np.uint32(0x9E3779B1)
+    d_seeds = torch_dev.from_numpy(seeds.view(np.int32).copy()).pin_memory()
+    for fn in (lambda o, **kw: ck.host_batch_strided(host, 0, 0, count, o, **kw),
+               lambda o, **kw: ck.host_batch_strided_multi(host, 0, 0, count, o, **kw)):
+        out = torch_dev.zeros(count, dtype=torch_dev.int32, pin_memory=True)
+        fn(out, seeds=d_seeds)
+        assert np.array_equal(out.numpy().view(np.uint32), seeds)
+        out = torch_dev.zeros(count, dtype=torch_dev.int32, pin_memory=True)
+        fn(out, seed=0xCAFEF00D)
+        assert set(out.numpy().view(np.uint32).tolist()) == {0xCAFEF00D}
+    seeds64 = np.arange(1, count + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    d_seeds64 = torch_dev.from_numpy(seeds64.view(np.int64).copy()).pin_memory()
+    out64 = torch_dev.zeros(count, dtype=torch_dev.int64, pin_memory=True)
+    ck.host_batch64_strided(host, 0, 0, count, out64, seeds=d_seeds64)
+    assert np.array_equal(out64.numpy().view(np.uint64), seeds64)
+
+
 def test_device_shards(torch_dev, oracle):
     # photon_crc32c_batch_strided_shards: two shards (halves, different seeds)
     # enqueued on the device(s); equal to one batch per half.
