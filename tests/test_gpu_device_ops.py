@@ -218,6 +218,39 @@ def test_device_dispatch_dropin(torch_dev, oracle):
     assert ck.crc32c_extend_at(hbuf.ctypes.data, n, 77) == expect
 
 
+def test_device_dispatch_series_follows_saved_host_engine(torch_dev, oracle):
+    # a routed crc32c_series on device memory follows the
+    # host engine it replaced -- crc32c_series_sw computes real CRCs for parts
+    # under 8 bytes (crc.cpp:474-478), crc32c_series_hw gives 0 for them
+    # (crc.cpp:481-500).
+    import ctypes
+    torch = torch_dev
+    L = ck.lib()
+    slot = ctypes.c_void_p.in_dll(L, "crc32c_series_auto")
+    sw = ctypes.cast(L["_Z16crc32c_series_swPKhjjPj"], ctypes.c_void_p).value
+    hw = ctypes.cast(L["_Z16crc32c_series_hwPKhjjPj"], ctypes.c_void_p).value
+    saved = slot.value
+    ps, nparts = 5, 301
+    dbuf = torch.empty(ps * nparts, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, ps * nparts, ps * nparts, 1, 0x5EED0500)
+    torch.cuda.synchronize()
+    host = dbuf.cpu().numpy()
+    real = [oracle.crc32c(host[i * ps:(i + 1) * ps]) for i in range(nparts)]
+    try:
+        for engine, want in ((sw, real), (hw, [0] * nparts)):
+            slot.value = engine
+            ck.set_device_dispatch(True)
+            assert slot.value not in (sw, hw)  # routed
+            out_h = np.zeros(nparts, np.uint32)
+            ck.crc32c_series_at(dbuf.data_ptr(), ps, nparts, out_h.ctypes.data)
+            assert list(out_h) == want
+            ck.set_device_dispatch(False)
+            assert slot.value == engine  # the saved engine is restored
+    finally:
+        ck.set_device_dispatch(False)
+        slot.value = saved
+
+
 def test_extend_device_over_4gib(torch_dev):
     # One buffer larger than 2^32 bytes (64-bit lengths and offsets end to
     # end): the split/fold path equals the series + combine_series identity.
