@@ -124,6 +124,34 @@ uint32_t or_crc32c_sw(const uint8_t *p, size_t n, uint32_t crc) {
     return crc;
 }
 
+/* Batch drivers for the full-size parity tests (tests/test_gpu_fullsize.py):
+ * plain loops over or_crc32c_sw, so a caller can fan a 4 GiB batch out over
+ * threads (ctypes drops the GIL). Call or_crc32c_table() once first: the
+ * lazy table build is not thread-safe. */
+void or_crc32c_strided(const uint8_t *base, uint64_t stride, uint64_t nbytes, uint64_t count, uint32_t seed,
+                       uint32_t *out) {
+    for (uint64_t i = 0; i < count; ++i) out[i] = or_crc32c_sw(base + i * stride, nbytes, seed);
+}
+
+/* iov[2k] = host address, iov[2k+1] = length (struct iovec). */
+void or_crc32c_iov(const uint64_t *iov, uint64_t count, uint32_t *out) {
+    for (uint64_t i = 0; i < count; ++i)
+        out[i] = or_crc32c_sw((const uint8_t *)(uintptr_t)iov[2 * i], (size_t)iov[2 * i + 1], 0);
+}
+
+/* Crc32Hasher::extend_hash over messages (rpc/serialize.h:244-247): message m
+ * chains crc32c_extend over segments msg_start[m] .. msg_start[m+1]-1 from
+ * seeds[m] (or seed0 when seeds is NULL). */
+void or_crc32c_msg_chain(const uint64_t *iov, const uint64_t *msg_start, uint64_t nmsg, const uint32_t *seeds,
+                         uint32_t seed0, uint32_t *out) {
+    for (uint64_t m = 0; m < nmsg; ++m) {
+        uint32_t c = seeds ? seeds[m] : seed0;
+        for (uint64_t s = msg_start[m]; s < msg_start[m + 1]; ++s)
+            c = or_crc32c_sw((const uint8_t *)(uintptr_t)iov[2 * s], (size_t)iov[2 * s + 1], c);
+        out[m] = c;
+    }
+}
+
 /* crc_apply_shifts with the software shift tables; crc.cpp:372-380. */
 static uint32_t or_apply_lshift_sw(uint32_t crc, uint64_t len) {
     for (; len; len &= len - 1) crc = or_clmul_modp32(crc, or_crc32c_lshift_sw((unsigned)__builtin_ctzll(len)));
@@ -210,6 +238,12 @@ uint64_t or_crc64ecma_sw(const uint8_t *p, size_t n, uint64_t crc) {
     uint64_t c = ~crc;
     for (size_t i = 0; i < n; ++i) c = or_tab64[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
     return ~c;
+}
+
+/* Batch driver (as or_crc32c_strided; call or_crc64ecma_sw once first). */
+void or_crc64ecma_strided(const uint8_t *base, uint64_t stride, uint64_t nbytes, uint64_t count, uint64_t seed,
+                          uint64_t *out) {
+    for (uint64_t i = 0; i < count; ++i) out[i] = or_crc64ecma_sw(base + i * stride, nbytes, seed);
 }
 
 /* (a*b) mod P for the 64-bit table generator; crc_tables.cpp:48-58. */

@@ -88,24 +88,35 @@ PCRC_HW inline uint32_t hw_mul(uint32_t a, uint32_t k) {
 }
 
 // Three independent crc32q chains over [0,L), [L,2L), [2L,3L), merged as
-// crcA * x^(16L) + crcB * x^(8L) + crcC. kA/kB are the hw_mul operands.
+// crcA * x^(16L) + crcB * x^(8L) + crcC. kA/kB are the hw_mul operands. The
+// two carry-less products are XORed into chain C's LAST word instead of being
+// reduced on their own (crc32q(c, w ^ t) = crc32q(c, w) ^ crc32q(0, t), and
+// crc32q(0, clmul(a, k)) = a * k * x^33): the merge then costs one PCLMUL on
+// the critical path, not PCLMUL + crc32q.
 template <size_t L>
 PCRC_HW inline uint32_t hw_3way(const uint8_t* p, uint32_t crc, uint32_t kA, uint32_t kB) {
     uint32_t a = crc, b = 0, c = 0;
-    for (size_t i = 0; i < L; i += 8) {
+    for (size_t i = 0; i < L - 8; i += 8) {
         a = hw_word(a, load64(p + i));
         b = hw_word(b, load64(p + L + i));
         c = hw_word(c, load64(p + 2 * L + i));
     }
-    return hw_mul(a, kA) ^ hw_mul(b, kB) ^ c;
+    a = hw_word(a, load64(p + L - 8));
+    b = hw_word(b, load64(p + 2 * L - 8));
+    const __m128i t = _mm_xor_si128(_mm_clmulepi64_si128(_mm_cvtsi32_si128((int)a), _mm_cvtsi32_si128((int)kA), 0x00),
+                                    _mm_clmulepi64_si128(_mm_cvtsi32_si128((int)b), _mm_cvtsi32_si128((int)kB), 0x00));
+    return hw_word(c, load64(p + 3 * L - 8) ^ (uint64_t)_mm_cvtsi128_si64(t));
 }
 
 struct HwConsts {
-    uint32_t k4096a, k4096b, k512a, k512b, k64a, k64b;
+    uint32_t k4096a, k4096b, k512a, k512b, k256a, k256b, k128a, k128b, k64a, k64b;
 };
 HwConsts g_hw;
 
-PCRC_HW uint32_t hw_engine(const uint8_t* p, size_t n, uint32_t crc) {
+// SSE4.2 + PCLMUL engine (any x86-64 with those): 3-way crc32q blocks of 12
+// KiB while they last, then 1.5 KiB, then one block each of 768, 384 and 192
+// bytes -- a 4 KiB buffer takes 4 merges, not 7.
+PCRC_HW uint32_t hw_portable_engine(const uint8_t* p, size_t n, uint32_t crc) {
     if (!n) return crc;
     // Align to 8 bytes so the word loop walks aligned words.
     while (n && ((uintptr_t)p & 7)) {
@@ -122,7 +133,17 @@ PCRC_HW uint32_t hw_engine(const uint8_t* p, size_t n, uint32_t crc) {
         p += 3 * 512;
         n -= 3 * 512;
     }
-    while (n >= 3 * 64) {
+    if (n >= 3 * 256) {
+        crc = hw_3way<256>(p, crc, g_hw.k256a, g_hw.k256b);
+        p += 3 * 256;
+        n -= 3 * 256;
+    }
+    if (n >= 3 * 128) {
+        crc = hw_3way<128>(p, crc, g_hw.k128a, g_hw.k128b);
+        p += 3 * 128;
+        n -= 3 * 128;
+    }
+    if (n >= 3 * 64) {
         crc = hw_3way<64>(p, crc, g_hw.k64a, g_hw.k64b);
         p += 3 * 64;
         n -= 3 * 64;
@@ -130,6 +151,115 @@ PCRC_HW uint32_t hw_engine(const uint8_t* p, size_t n, uint32_t crc) {
     for (; n >= 8; p += 8, n -= 8) crc = hw_word(crc, load64(p));
     for (; n; --n) crc = hw_byte(crc, *p++);
     return crc;
+}
+
+// ------------------------------------------------------ AVX-512 VPCLMULQDQ path
+// For CPUs with 512-bit carry-less multiply (Zen 4/5 EPYC such as the GPU
+// boxes' 9575F, Ice Lake and later Xeons). Folding instead of crc32q chains:
+// the buffer is read 64 bytes per register, four registers (256 B) per step,
+// and each 128-bit lane S (first 8 bytes H = the higher powers, last 8 bytes L)
+// is moved D bytes forward as
+//     S * x^(8D) = H * x^(8D+64) + L * x^(8D)   (mod P)
+// with two PCLMULs against x^(8D+63) and x^(8D-1) (a carry-less product of
+// reflected operands reads as the product times x) and XORed into the data D
+// bytes later. What is left at the end is one 128-bit value V whose CRC is
+// V(x) * x^32 mod P = two crc32q of its halves; the seed is XORed into the
+// first four data bytes (init-value linearity, as the GPU kernels do).
+// Same results as every other engine; no table, no reference code.
+#define PCRC_V512 __attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,vpclmulqdq,pclmul,sse4.2")))
+
+struct alignas(64) V512Consts {
+    uint64_t k256[8];  // every 128-bit lane: {x^(8*256+63), x^(8*256-1)} as 64-bit reflected words
+    uint64_t k192[8];
+    uint64_t k128[8];
+    uint64_t k64[8];
+    uint64_t kred[8];  // lanes 0, 1, 2: moves of 48, 32, 16 bytes; lane 3: 0
+    uint64_t k16[2];
+};
+V512Consts g_v;
+bool g_has_v512 = false;
+constexpr size_t kV512Min = 256;  // shorter buffers take the crc32q engine
+
+void fold_consts(uint64_t* k, uint64_t bytes) {
+    // a 32-bit reflected value v (bit i = x^(31-i)) as a 64-bit reflected word: v << 32
+    k[0] = (uint64_t)xpow(8 * bytes + 63) << 32;
+    k[1] = (uint64_t)xpow(8 * bytes - 1) << 32;
+}
+
+void build_v512_consts() {
+    for (int l = 0; l < 4; ++l) {
+        fold_consts(g_v.k256 + 2 * l, 256);
+        fold_consts(g_v.k192 + 2 * l, 192);
+        fold_consts(g_v.k128 + 2 * l, 128);
+        fold_consts(g_v.k64 + 2 * l, 64);
+    }
+    fold_consts(g_v.kred + 0, 48);
+    fold_consts(g_v.kred + 2, 32);
+    fold_consts(g_v.kred + 4, 16);
+    g_v.kred[6] = g_v.kred[7] = 0;
+    fold_consts(g_v.k16, 16);
+}
+
+PCRC_V512 inline __m512i fold512(__m512i a, __m512i k, __m512i d) {
+    return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(a, k, 0x00), _mm512_clmulepi64_epi128(a, k, 0x11), d,
+                                     0x96);
+}
+
+PCRC_V512 inline __m128i fold128(__m128i a, __m128i k, __m128i d) {
+    return _mm_ternarylogic_epi64(_mm_clmulepi64_si128(a, k, 0x00), _mm_clmulepi64_si128(a, k, 0x11), d, 0x96);
+}
+
+PCRC_V512 uint32_t v512_engine(const uint8_t* p, size_t n, uint32_t crc) {
+    // n >= kV512Min
+    const __m512i k256 = _mm512_load_si512(g_v.k256);
+    __m512i a0 = _mm512_xor_si512(_mm512_loadu_si512(p), _mm512_zextsi128_si512(_mm_cvtsi32_si128((int)crc)));
+    __m512i a1 = _mm512_loadu_si512(p + 64);
+    __m512i a2 = _mm512_loadu_si512(p + 128);
+    __m512i a3 = _mm512_loadu_si512(p + 192);
+    p += 256;
+    n -= 256;
+    for (; n >= 256; p += 256, n -= 256) {
+        a0 = fold512(a0, k256, _mm512_loadu_si512(p));
+        a1 = fold512(a1, k256, _mm512_loadu_si512(p + 64));
+        a2 = fold512(a2, k256, _mm512_loadu_si512(p + 128));
+        a3 = fold512(a3, k256, _mm512_loadu_si512(p + 192));
+    }
+    // The four registers onto the last one's position, then whole 64-byte blocks.
+    const __m512i k64 = _mm512_load_si512(g_v.k64);
+    __m512i r = fold512(a0, _mm512_load_si512(g_v.k192), a3);
+    r = fold512(a1, _mm512_load_si512(g_v.k128), r);
+    r = fold512(a2, k64, r);
+    for (; n >= 64; p += 64, n -= 64) r = fold512(r, k64, _mm512_loadu_si512(p));
+    // Four lanes onto the last one.
+    const __m512i kr = _mm512_load_si512(g_v.kred);
+    const __m512i t = _mm512_xor_si512(_mm512_clmulepi64_epi128(r, kr, 0x00), _mm512_clmulepi64_epi128(r, kr, 0x11));
+    __m128i x = _mm_ternarylogic_epi64(_mm512_castsi512_si128(t), _mm512_extracti64x2_epi64(t, 1),
+                                       _mm512_extracti64x2_epi64(t, 2), 0x96);
+    x = _mm_xor_si128(x, _mm512_extracti64x2_epi64(r, 3));
+    const __m128i k16 = _mm_load_si128(reinterpret_cast<const __m128i*>(g_v.k16));
+    for (; n >= 16; p += 16, n -= 16) x = fold128(x, k16, _mm_loadu_si128(reinterpret_cast<const __m128i*>(p)));
+    uint32_t c = (uint32_t)_mm_crc32_u64(0, (uint64_t)_mm_cvtsi128_si64(x));
+    c = (uint32_t)_mm_crc32_u64(c, (uint64_t)_mm_extract_epi64(x, 1));
+    if (n >= 8) {
+        c = (uint32_t)_mm_crc32_u64(c, load64(p));
+        p += 8;
+        n -= 8;
+    }
+    for (; n; --n) c = _mm_crc32_u8(c, *p++);
+    return c;
+}
+
+bool cpu_has_v512() {
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+           __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512dq") &&
+           __builtin_cpu_supports("vpclmulqdq") && __builtin_cpu_supports("pclmul") &&
+           __builtin_cpu_supports("sse4.2");
+}
+
+// crc32c_hw: the fastest engine this CPU has.
+uint32_t hw_engine(const uint8_t* p, size_t n, uint32_t crc) {
+    if (g_has_v512 && n >= kV512Min) return v512_engine(p, n, crc);
+    return hw_portable_engine(p, n, crc);
 }
 
 PCRC_HW uint32_t hw_simple_engine(const uint8_t* p, size_t n, uint32_t crc) {
@@ -201,7 +331,7 @@ uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t crc) {
 }
 
 uint32_t crc32c_hw(const uint8_t* p, size_t n, uint32_t crc) { return hw_engine(p, n, crc); }
-uint32_t crc32c_hw_portable(const uint8_t* p, size_t n, uint32_t crc) { return hw_engine(p, n, crc); }
+uint32_t crc32c_hw_portable(const uint8_t* p, size_t n, uint32_t crc) { return hw_portable_engine(p, n, crc); }
 uint32_t crc32c_hw_simple(const uint8_t* p, size_t n, uint32_t crc) { return hw_simple_engine(p, n, crc); }
 
 void crc32c_series_sw(const uint8_t* buffer, uint32_t part_size, uint32_t n_parts, uint32_t* crc_parts) {
@@ -269,9 +399,15 @@ __attribute__((constructor(101))) static void photon_crc_cpu_init() {
     g_hw.k4096b = xpow(8ull * 4096 - 33);
     g_hw.k512a = xpow(8ull * 2 * 512 - 33);
     g_hw.k512b = xpow(8ull * 512 - 33);
+    g_hw.k256a = xpow(8ull * 2 * 256 - 33);
+    g_hw.k256b = xpow(8ull * 256 - 33);
+    g_hw.k128a = xpow(8ull * 2 * 128 - 33);
+    g_hw.k128b = xpow(8ull * 128 - 33);
     g_hw.k64a = xpow(8ull * 2 * 64 - 33);
     g_hw.k64b = xpow(8ull * 64 - 33);
+    build_v512_consts();
     __builtin_cpu_init();
+    g_has_v512 = cpu_has_hw() && cpu_has_v512() && !getenv("PHOTON_CRC_NO_AVX512");
     if (cpu_has_hw()) {
         crc32c_auto = crc32c_hw;
         crc32c_series_auto = crc32c_series_hw;

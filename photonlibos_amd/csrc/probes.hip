@@ -190,7 +190,104 @@ __global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::Batc
     }
 }
 
+// Per-wave stamps as crc_wave_times_kernel writes them (6 words per wave).
+struct WaveStamp {
+    uint64_t t0, c0;
+    __device__ __forceinline__ WaveStamp() : t0(__builtin_amdgcn_s_memrealtime()), c0(__builtin_amdgcn_s_memtime()) {}
+    __device__ __forceinline__ void store(uint64_t* t, uint64_t gw) const {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime();
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63u) == 0) {
+            t[6 * gw] = t0;
+            t[6 * gw + 1] = t1;
+            t[6 * gw + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+            t[6 * gw + 3] = __builtin_amdgcn_s_getreg(20 | (3 << 11));
+            t[6 * gw + 4] = c0;
+            t[6 * gw + 5] = c1;
+        }
+    }
+};
+
+// DVFS control: the product's read_stream_kernel
+// (crc32c_kernels.h, grid-stride, 8 loads in flight per thread) and the CRC
+// kernel's own lane-group row pattern (group_rows_kernel) with the same
+// per-wave clock stamps as crc_wave_times_kernel, so the ramp of a read-only
+// body can be set beside the CRC body's.
+__global__ __launch_bounds__(256) void read_stream_stamped_kernel(const uint8_t* p, uint64_t nvec, uint32_t* sink,
+                                                                  uint64_t* t) {
+    const WaveStamp ws;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = tid;
+    for (; i + 7 * nth < nvec; i += 8 * nth) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = pcrc::load16(p + 16 * (i + k * nth));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < nvec; i += nth) {
+        const uint4 v = pcrc::load16(p + 16 * i);
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    sink[tid] = acc;
+    ws.store(t, tid >> 6);
+}
+
+template <int G, int U>
+__global__ __launch_bounds__(1024) void group_rows_stamped_kernel(const uint8_t* base, uint64_t stride, uint64_t rows,
+                                                                 uint64_t count, uint32_t* sink, uint64_t* t) {
+    const WaveStamp ws;
+    constexpr int GPW = 64 / G;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1), grp = lane / G;
+    const uint64_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 16;
+    uint32_t acc = 0;
+    for (uint64_t wv = blockIdx.x * 16ull + wave; wv * GPW < count; wv += nwaves) {
+        const uint64_t b = wv * GPW + grp;
+        if (b >= count) continue;
+        const uint8_t* p = base + b * stride + 16 * gl;
+        uint64_t r = 0;
+        u32x4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = ld<true>(p + (uint64_t)u * 16 * G);
+        for (; r + 2 * U <= rows; r += U) {
+            u32x4 nxt[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = ld<true>(p + (r + U + u) * 16 * G);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc ^= cur[u].x ^ cur[u].y ^ cur[u].z ^ cur[u].w;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= cur[u].x ^ cur[u].y ^ cur[u].z ^ cur[u].w;
+    }
+    sink[blockIdx.x * 1024ull + threadIdx.x] = acc;
+    ws.store(t, blockIdx.x * 16ull + wave);
+}
+
 extern "C" {
+
+// read_stream_stamped_kernel: grid = blocks x 256 threads (the product's
+// photon_crc_util_read_stream uses cus * 8); t holds 6 words per wave.
+int probe_read_stream_stamped(const void* p, uint64_t nbytes, uint32_t* sink, uint64_t* t, int blocks,
+                              void* stream) {
+    hipLaunchKernelGGL(read_stream_stamped_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t*>(p), nbytes / 16, sink, t);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// group_rows_stamped_kernel<32, 4> (the C2 CRC kernel's pattern): rows of 512 B.
+int probe_group_rows_stamped(const void* base, uint64_t stride, uint64_t rows, uint64_t count, uint32_t* sink,
+                             uint64_t* t, int blocks, void* stream) {
+    hipLaunchKernelGGL((group_rows_stamped_kernel<32, 4>), dim3(blocks), dim3(1024), 0,
+                       static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(base), stride, rows, count, sink,
+                       t);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 // crc_wave_times_kernel over a strided batch; `t` holds 6 * grid * 16 words,
 // `ticket` 256 words (zeroed here on the stream before the launch).

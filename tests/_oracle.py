@@ -8,7 +8,7 @@ import numpy as np
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _L = ctypes.CDLL(os.path.join(_REPO, "oracle", "lib", "libcrc_oracle.so"), use_errno=True)
 
-_u32, _u64, _sz, _p = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_char_p
+_u32, _u64, _sz, _p, _vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_void_p
 for name, res, args in [
     ("or_crc32c_sw", _u32, [_p, _sz, _u32]),
     ("or_crc32c_bitwise", _u32, [_p, _sz, _u32]),
@@ -25,6 +25,11 @@ for name, res, args in [
     ("or_crc32c_series_hw", None, [_p, _u32, _u32, ctypes.POINTER(_u32)]),
     ("or_crc32c_trim", _u32, [_u32, _u32, _u32, _u32, _u32, _u32]),
     ("or_crc64ecma_sw", _u64, [_p, _sz, _u64]),
+    ("or_crc32c_table", _vp, [ctypes.c_int]),
+    ("or_crc32c_strided", None, [_vp, _u64, _u64, _u64, _u32, _vp]),
+    ("or_crc64ecma_strided", None, [_vp, _u64, _u64, _u64, _u64, _vp]),
+    ("or_crc32c_iov", None, [_vp, _u64, _vp]),
+    ("or_crc32c_msg_chain", None, [_vp, _vp, _u64, _vp, _u32, _vp]),
 ]:
     f = getattr(_L, name)
     f.restype = res
@@ -91,3 +96,87 @@ def extend_chain(segments, seed=0):
     for s in segments:
         c = crc32c(s, c)
     return c
+
+
+# ---------------------------------------------------------------- batches
+# Full-size parity (tests/test_gpu_fullsize.py): the same oracle functions in
+# C loops, fanned out over a thread pool (ctypes releases the GIL). Host
+# arrays are passed by address, never copied.
+
+def _threads():
+    # the GPU box gives a job 16 CPUs; nproc shows the whole machine there
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def _fan_out(count, fn, threads=None):
+    from concurrent.futures import ThreadPoolExecutor
+    t = threads or _threads()
+    cuts = [count * k // t for k in range(t + 1)]
+    with ThreadPoolExecutor(t) as ex:
+        list(ex.map(lambda k: fn(cuts[k], cuts[k + 1]), range(t)))
+
+
+def crc32c_strided(host, stride, nbytes, count, seed=0):
+    """CRC32C of `count` buffers at host[i*stride : i*stride+nbytes] (numpy uint8)."""
+    assert host.dtype == np.uint8 and host.flags.c_contiguous
+    assert count == 0 or (count - 1) * stride + nbytes <= host.size
+    _L.or_crc32c_table(0)
+    out = np.zeros(count, np.uint32)
+    base = host.ctypes.data
+
+    def part(lo, hi):
+        if hi > lo:
+            _L.or_crc32c_strided(base + lo * stride, stride, nbytes, hi - lo, seed & 0xFFFFFFFF,
+                                 out.ctypes.data + 4 * lo)
+    _fan_out(count, part)
+    return out
+
+
+def crc64ecma_strided(host, stride, nbytes, count, seed=0):
+    assert host.dtype == np.uint8 and host.flags.c_contiguous
+    assert count == 0 or (count - 1) * stride + nbytes <= host.size
+    crc64ecma(b"")  # builds the table before the threads start
+    out = np.zeros(count, np.uint64)
+    base = host.ctypes.data
+
+    def part(lo, hi):
+        if hi > lo:
+            _L.or_crc64ecma_strided(base + lo * stride, stride, nbytes, hi - lo, seed, out.ctypes.data + 8 * lo)
+    _fan_out(count, part)
+    return out
+
+
+def crc32c_iov(iov):
+    """Seed-0 CRC32C of every {host address, length} row of `iov` (uint64, shape (n, 2))."""
+    iov = np.ascontiguousarray(iov, np.uint64)
+    _L.or_crc32c_table(0)
+    n = iov.shape[0]
+    out = np.zeros(n, np.uint32)
+
+    def part(lo, hi):
+        if hi > lo:
+            _L.or_crc32c_iov(iov.ctypes.data + 16 * lo, hi - lo, out.ctypes.data + 4 * lo)
+    _fan_out(n, part)
+    return out
+
+
+def msg_chain(iov, msg_start, seeds=None, seed0=0):
+    """extend_chain per message over host iovecs: message m = segments msg_start[m]..msg_start[m+1]-1."""
+    iov = np.ascontiguousarray(iov, np.uint64)
+    msg_start = np.ascontiguousarray(msg_start, np.uint64)
+    seeds = None if seeds is None else np.ascontiguousarray(seeds, np.uint32)
+    _L.or_crc32c_table(0)
+    nmsg = msg_start.size - 1
+    out = np.zeros(nmsg, np.uint32)
+
+    def part(lo, hi):
+        if hi > lo:
+            _L.or_crc32c_msg_chain(iov.ctypes.data, msg_start.ctypes.data + 8 * lo, hi - lo,
+                                   None if seeds is None else seeds.ctypes.data + 4 * lo, seed0 & 0xFFFFFFFF,
+                                   out.ctypes.data + 4 * lo)
+    _fan_out(nmsg, part)
+    return out

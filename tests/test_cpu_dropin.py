@@ -137,3 +137,20 @@ def test_device_dispatch_keeps_host_results(alphabet):
     finally:
         ck.set_device_dispatch(False)
     assert ck.is_crc32c_hw_available()
+
+
+@pytest.mark.parametrize("engine", ["crc32c_hw", "crc32c_hw_portable"])
+def test_every_length_offset_seed(engine, oracle):
+    # Every length 0..1100 and a spread up to 70 K at 5 misalignments with
+    # seeds: covers each tier edge of the 3-way crc32q engine (192/384/768/
+    # 1536/12288 B) and of the AVX-512 folding engine (256-B steps, 64- and
+    # 16-byte tails) that crc32c_hw uses on CPUs with VPCLMULQDQ.
+    f = getattr(ck, engine)
+    host = datagen.stream_bytes(0xF01D, 80000 + 64)
+    rnd = random.Random(9)
+    lens = list(range(0, 1101)) + [rnd.randrange(1100, 70000) for _ in range(150)] + [12287, 12288, 12289, 65536]
+    for n in lens:
+        for off in (0, 1, 7, 8, 13):
+            seed = rnd.getrandbits(32) if n % 2 else 0
+            view = host[off:off + n]
+            assert f(view, seed) == oracle.crc32c(view, seed), (engine, n, off)

@@ -151,3 +151,29 @@ def test_extend_chain_equals_reference_checked_message(oracle):
         body = bytearray(datagen.stream_bytes(m["body"][0], m["body"][1]).tobytes())
         body[-4:] = b"\0\0\0\0"
         assert oracle.extend_chain(data + [bytes(body)], 0) == m["checksum"]
+
+
+def test_batch_drivers_match_single_calls(oracle):
+    # The threaded batch drivers the full-size GPU tests use (or_crc32c_strided,
+    # or_crc64ecma_strided, or_crc32c_iov, or_crc32c_msg_chain) equal the
+    # pinned single-buffer functions on odd strides, lengths and seeds.
+    host = datagen.stream_bytes(0xBA7C, 1 << 20)
+    for nbytes, stride, count, seed in ((100, 113, 900, 0), (4096, 4096, 200, 0xFFFFFFFF), (0, 7, 5, 9)):
+        got = oracle.crc32c_strided(host, stride, nbytes, count, seed)
+        want = [oracle.crc32c(host[i * stride:i * stride + nbytes], seed) for i in range(count)]
+        assert got.tolist() == want
+        got64 = oracle.crc64ecma_strided(host, stride, nbytes, count, seed)
+        assert got64.tolist() == [oracle.crc64ecma(host[i * stride:i * stride + nbytes], seed) for i in range(count)]
+    rnd = np.random.default_rng(5)
+    offs = rnd.integers(0, (1 << 20) - 20000, 500)
+    lens = rnd.integers(0, 20000, 500)
+    iov = np.stack([np.uint64(host.ctypes.data) + offs.astype(np.uint64), lens.astype(np.uint64)], 1)
+    assert oracle.crc32c_iov(iov).tolist() == [oracle.crc32c(host[o:o + n]) for o, n in zip(offs, lens)]
+    start = np.array([0, 0, 3, 3, 10, 250, 500], np.uint64)
+    seeds = np.array([1, 2, 3, 0xFFFFFFFF, 5, 6], np.uint32)
+    want = [oracle.extend_chain([host[offs[k]:offs[k] + lens[k]] for k in range(int(start[m]), int(start[m + 1]))],
+                                int(seeds[m])) for m in range(6)]
+    assert oracle.msg_chain(iov, start, seeds).tolist() == want
+    assert oracle.msg_chain(iov, start, None, 7).tolist() == [
+        oracle.extend_chain([host[offs[k]:offs[k] + lens[k]] for k in range(int(start[m]), int(start[m + 1]))], 7)
+        for m in range(6)]
