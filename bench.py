@@ -15,7 +15,8 @@ One "step" = one pass of the hot path over one batch (BASELINE.json configs):
   c2_crc64: the C2 shape with CRC-64/ECMA (next row f2)
   c3_crc64: the C3 shape with CRC-64/ECMA
   --h2d / --rpc-batch / --rpc-latency / --file-records: host-memory rates
-      for DESIGN.md, never `value`.
+      for DESIGN.md, never `value`; --extend: one long device buffer (the
+      reference's perf shape) and the routed drop-in's costs, also DESIGN.md.
 
 Multi-GPU: one process per GPU. The driver launches
 `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`;
@@ -88,6 +89,8 @@ def parse(argv=None):
     ap.add_argument("--file-records", action="store_true", help="file records through the pread pipeline (DESIGN.md)")
     ap.add_argument("--rpc-batch", action="store_true", help="CheckedMessage batch over pinned host payloads (DESIGN.md)")
     ap.add_argument("--rpc-latency", action="store_true", help="submit+wait latency of small CheckedMessage batches")
+    ap.add_argument("--extend", action="store_true",
+                    help="one long device buffer at base+1 (1 GiB rate, 128 KiB latency, routed drop-in cost)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -536,6 +539,82 @@ def run_rpc_latency(args, stream):
                       "rows": rows}))
 
 
+def run_extend(args, stream):
+    """One long device buffer (photon_crc32c_extend_device, the routed drop-in
+    crc32c_extend on device memory): the reference's own perf shape
+    (common/checksum/test/test_checksum.cpp:125-168 times one 128 KiB and one
+    1 GiB buffer at buf+1). 1 GiB: GiB/s and % of 8 TB/s from HIP events
+    around each call on the launch stream; 128 KiB: latency per call (enqueue
+    + wait); the routed drop-in crc32c_extend on a device pointer (sync); and
+    the price of routing on HOST pointers (hipPointerGetAttributes per call,
+    C1's 4 KiB buffers), dispatch off vs on. Reported in DESIGN.md, never `value`."""
+    import ctypes
+    res = {"metric": "photon_crc32c_extend_device: one long device buffer at base+1 (reference perf shape)"}
+    n = 1 << 30
+    d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, n + 64, n + 64, 1, 0x5EED0900, stream=stream)
+    out = torch.zeros(64, dtype=torch.int32, device="cuda")
+    for label, nbytes, steps in (("1GiB", n, max(10, min(args.steps, 50))), ("128KiB", 128 << 10, 200)):
+        ms = []
+        for k in range(steps + 5):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            ck.extend_device(d.data_ptr() + 1, nbytes, 0, out[k % 64:k % 64 + 1], stream=stream)
+            b.record(stream)
+            ms.append((a, b))
+        torch.cuda.synchronize()
+        t = np.array([a.elapsed_time(b) for a, b in ms[5:]])
+        # enqueue + wait latency, one call at a time
+        lat = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            ck.extend_device(d.data_ptr() + 1, nbytes, 0, out[:1], stream=stream)
+            stream.synchronize()
+            lat.append(time.perf_counter() - t0)
+        gbps = nbytes / (float(np.mean(t)) * 1e-3) / 1e9
+        res[label] = {"bytes": nbytes, "kernel_ms_mean": round(float(np.mean(t)), 4),
+                      "kernel_ms_median": round(float(np.median(t)), 4), "GiB_per_s": round(gbps * 1e9 / GIB, 1),
+                      "frac_of_8TBps": round(gbps / HBM_PEAK_GBPS, 4),
+                      "call_wait_us_median": round(float(np.median(lat)) * 1e6, 1)}
+    want = ck.crc32c_hw(d[1:1 + (128 << 10)].cpu().numpy().tobytes())
+    ck.extend_device(d.data_ptr() + 1, 128 << 10, 0, out[:1], stream=stream)
+    torch.cuda.synchronize()
+    ok = int(out[0].item()) & 0xFFFFFFFF == want
+    # Routed drop-in: crc32c_extend through crc32c_auto on a device pointer
+    # (default stream, synchronous), and the routing probe's price on host
+    # pointers (C1: 1024 x 4 KiB).
+    ck.set_device_dispatch(True)
+    routed = []
+    for _ in range(50):
+        t0 = time.perf_counter()
+        r = ck.crc32c_extend_at(d.data_ptr() + 1, 128 << 10, 0)
+        routed.append(time.perf_counter() - t0)
+    ok = ok and r == want
+    ck.set_device_dispatch(False)
+    hbuf = np.frombuffer(d[:1024 * 4096].cpu().numpy().tobytes(), np.uint8)
+    base = hbuf.ctypes.data
+
+    def per_call_us(on):
+        ck.set_device_dispatch(on)
+        fn = ck._auto("crc32c_auto", ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                                                       ctypes.c_uint32))
+        best = 1e9
+        for _ in range(5):
+            t0 = time.perf_counter()
+            for i in range(1024):
+                fn(base + i * 4096, 4096, 0)
+            best = min(best, time.perf_counter() - t0)
+        ck.set_device_dispatch(False)
+        return best / 1024 * 1e6
+    off_us, on_us = per_call_us(False), per_call_us(True)
+    res["routed_crc32c_extend_128KiB_device_us_median"] = round(float(np.median(routed)) * 1e6, 1)
+    res["host_pointer_call_us"] = {"dispatch_off": round(off_us, 3), "dispatch_on": round(on_us, 3),
+                                   "note": "C1 (1024 x 4 KiB host buffers) through crc32c_auto from Python "
+                                           "ctypes; the difference is the per-call hipPointerGetAttributes probe"}
+    res["self_check"] = ok
+    print(json.dumps(res))
+
+
 def run_file_records(args):
     """§8(f) row 4: CRC32C of the 4 KiB records of a 1 GiB file (page-cache
     hot, buffered pread into pinned chunks + GPU pipeline), end to end.
@@ -623,7 +702,7 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not (args.pmc_child or args.h2d or args.rpc_batch or args.rpc_latency
-                                   or args.file_records):
+                                   or args.file_records or args.extend):
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
         return 2
     global ck
@@ -646,10 +725,12 @@ def main(argv=None):
     torch.cuda.set_device(device)
     ck.set_lanes_per_buffer(args.lanes)
     stream = torch.cuda.current_stream()
-    if args.h2d or args.rpc_batch or args.rpc_latency or args.file_records:
+    if args.h2d or args.rpc_batch or args.rpc_latency or args.file_records or args.extend:
         if rank == 0:
             if args.h2d:
                 run_h2d(args, stream)
+            elif args.extend:
+                run_extend(args, stream)
             elif args.rpc_batch:
                 run_rpc_batch(args, stream)
             elif args.rpc_latency:

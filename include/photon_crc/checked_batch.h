@@ -22,8 +22,24 @@
  *    crc32c_combine fold, the photon_crc32c_batch_msg_n kernels) and compares.
  *    The same batch serves the send side (add_checksum, serialize.h:258-261):
  *    add with expected = 0 and read the computed value.
- *    Result i == Crc32Hasher::extend_hash over message i's segments then its
- *    body (serialize.h:244-252), seed 0.
+ *    Result i == what the reference's validate_checksum(iov, body, len)
+ *    returns for message i:
+ *    - by default `body` is the message object itself, as
+ *      DeserializerIOV::deserialize passes it (t->validate_checksum(iov, t,
+ *      sizeof(*t)), serialize.h:462-463), whose first 4 bytes are m_checksum
+ *      (the CheckedMessage<> base of every Photon message struct).
+ *      Crc32Hasher accumulates the payload's CRC into m_checksum and then
+ *      hashes the body holding it; a CRC whose init equals its first data
+ *      word equals the CRC (init 0) of the data with that word zeroed, so the
+ *      reference's checksum is crc32c(body with m_checksum = 0): the payload
+ *      does NOT enter it (tests/golden/ioalloc_binding.json: the reference's
+ *      own template over reference IOVectors). The batch reproduces that: it
+ *      zeroes m_checksum (validate_checksum's second line) and checksums the
+ *      body; payload segments are not read.
+ *    - PHOTON_CRC_BATCH_DETACHED_BODY: `body` is a separate buffer (not the
+ *      object holding m_checksum) or absent: Crc32Hasher::extend_hash over
+ *      the payload segments, then the body, seed 0 (serialize.h:244-252;
+ *      also the default's result when body is NULL, e.g. rpc.h:106).
  *
  * Memory rules: every segment and body must be device-accessible (pinned by
  * this allocator or any hipHostMalloc / hipHostRegister, or device memory);
@@ -77,6 +93,7 @@ typedef struct photon_crc_msg_batch photon_crc_msg_batch;
 #define PHOTON_CRC_BATCH_TRUSTED 1u /* skip the per-segment accessibility check */
 #define PHOTON_CRC_BATCH_STAGED 2u  /* copy descriptors H2D and verdicts D2H instead of
                                        the kernels reading / writing the pinned staging */
+#define PHOTON_CRC_BATCH_DETACHED_BODY 4u /* bodies are separate buffers: hash payload, then body */
 
 /* A batch on the current device with room for max_messages messages and
  * max_segments segments in total (bodies count as segments). NULL on error. */
@@ -85,9 +102,11 @@ void photon_crc_msg_batch_destroy(photon_crc_msg_batch* b);
 
 /* Append one message: its payload iovector (iov[iovcnt], struct iovec layout)
  * followed by `body` (skipped when NULL or body_length == 0, as
- * validate_checksum does) and the checksum it must match. Returns the
- * message's index (>= 0) or -ENOSPC / -EFAULT / -EBUSY (submitted, not yet
- * reset) / -EINVAL. */
+ * validate_checksum does) and the checksum it must match. Unless the batch
+ * is DETACHED_BODY, a body is the message object: its first 4 bytes
+ * (m_checksum) are set to 0 here, as validate_checksum does, and only the
+ * body is checksummed (see 2. above). Returns the message's index (>= 0) or
+ * -ENOSPC / -EFAULT / -EBUSY (submitted, not yet reset) / -EINVAL. */
 int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec* iov, uint32_t iovcnt,
                                  const void* body, uint64_t body_length, uint32_t expected);
 
@@ -97,9 +116,11 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
  * PHOTON_CRC_BATCH_STAGED the descriptors are copied H2D and the results
  * D2H around it). If `done` is non-NULL it is called once the results are on
  * the host, from a HIP runtime thread (it may call photon::semaphore::signal,
- * thread/thread.h:511-520); it must not call HIP. A completed batch may be
- * submitted again (its payloads re-read, e.g. after they were refilled);
- * -EBUSY while a submit is still running. */
+ * thread/thread.h:511-520, and photon_crc_msg_batch_result, which then needs
+ * no HIP call); it must not call HIP, nor submit / reset / destroy this batch.
+ * A completed batch may be submitted again (its payloads re-read, e.g. after
+ * they were refilled); -EBUSY while a submit is still running or its `done`
+ * callback has not returned yet (reset too; destroy waits for it). */
 int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*done)(void* arg), void* arg);
 
 /* Wait for the submitted batch. Returns the number of messages whose checksum

@@ -61,6 +61,12 @@ int photon_crc_device_count(void);
 /* Text of the last error on this thread ("" if none). */
 const char* photon_crc_last_error(void);
 
+/* Device scratch the library keeps between calls (segment CRCs of two-kernel
+ * message batches, long-buffer state): idle buffers over 64 MiB, and idle
+ * scratch beyond 256 MiB per device, are freed automatically; this frees
+ * every idle buffer whose last use has completed. Returns the bytes freed. */
+int64_t photon_crc_scratch_release(void);
+
 /* (i) Equal-length buffers: buffer i = d_base + i*stride, nbytes each.
  * seed_i = d_seeds ? d_seeds[i] : seed0. d_out[count] receives the CRCs. */
 int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,

@@ -46,6 +46,7 @@ class PinnedAlloc:
 
 TRUSTED = 1
 STAGED = 2  # descriptors H2D / verdicts D2H instead of zero-copy staging
+DETACHED_BODY = 4  # bodies are separate buffers: payload then body (not the message object)
 
 
 class MessageBatch:
@@ -77,8 +78,16 @@ class MessageBatch:
             raise CrcError(rc, lib().photon_crc_last_error().decode(errors="replace"))
         return rc
 
-    def submit(self, stream=None):
-        _check(lib().photon_crc_msg_batch_submit(self._b, stream, None, None))
+    _DONE = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+    def submit(self, stream=None, done=None):
+        """One GPU submit of every message added. `done` (optional, no
+        arguments) runs on a HIP runtime thread once the verdicts are on the
+        host; it must not call HIP, submit, reset or close this batch."""
+        cb = self._DONE(lambda _arg: done()) if done is not None else None
+        self._cb = cb  # keep the ctypes trampoline alive while HIP may call it
+        _check(lib().photon_crc_msg_batch_submit(self._b, stream, ctypes.cast(cb, ctypes.c_void_p) if cb else None,
+                                                 None))
 
     def wait(self):
         rc = lib().photon_crc_msg_batch_wait(self._b)

@@ -514,3 +514,8 @@ def read_stream(base, nbytes, sink, sink_words, stream=None):
 def fill_splitmix(base, stride, nbytes, count, seed_base, stream=None):
     """Test/bench utility: device buffers = photonlibos_amd.datagen streams."""
     _check(lib().photon_crc_util_fill_splitmix(_ptr(base), stride, nbytes, count, seed_base, _stream(stream)))
+
+
+def scratch_release():
+    """Free the device scratch buffers the library keeps idle (bytes freed)."""
+    return int(lib().photon_crc_scratch_release())

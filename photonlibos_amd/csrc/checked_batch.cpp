@@ -11,9 +11,12 @@
 #include <errno.h>
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
+#include <string.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -81,9 +84,18 @@ void* pin(size_t bytes) {
 const void* device_address(const void* p, uint64_t n, bool* host) {
     *host = true;
     {
+        // Pinned-pool memory: [p, p+n) must lie inside ONE live block
+        // (the slab alone let a segment run past its IOAlloc block).
         Pool& P = pool();
         std::lock_guard<std::mutex> lk(P.mu);
-        if (P.find(reinterpret_cast<uintptr_t>(p), n) != P.slabs.end()) return p;
+        const uintptr_t q = reinterpret_cast<uintptr_t>(p);
+        auto it = P.find(q, 1);
+        if (it != P.slabs.end()) {
+            const uint64_t bsz = it->second.cls < 0 ? it->second.size : 1ull << it->second.cls;
+            const uintptr_t blk = it->first + (q - it->first) / bsz * bsz;
+            if (!P.live.count(blk) || n > bsz || q - blk > bsz - n) return nullptr;
+            return p;
+        }
     }
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -104,8 +116,19 @@ const void* device_address(const void* p, uint64_t n, bool* host) {
         } else {
             (void)hipGetLastError();
         }
-    } else if (registered_range_check(p, n) == 0) {
-        return nullptr;
+    } else {
+        // Host memory: against its photon_crc_host_register registration, else
+        // against its hipHostMalloc allocation when HIP reports the range.
+        const int reg = registered_range_check(p, n);
+        if (reg == 0) return nullptr;
+        void* lo = nullptr;
+        size_t size = 0;
+        if (reg < 0 && hipMemGetAddressRange(&lo, &size, const_cast<void*>(p)) == hipSuccess && size) {
+            const uintptr_t q = reinterpret_cast<uintptr_t>(p), b0 = reinterpret_cast<uintptr_t>(lo);
+            if (q < b0 || n > size || q - b0 > size - n) return nullptr;
+        } else if (reg < 0) {
+            (void)hipGetLastError();
+        }
     }
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) {
         *host = false;
@@ -155,8 +178,17 @@ struct photon_crc_msg_batch {
     hipEvent_t done_ev = nullptr;
     uint64_t nmsg = 0, nseg = 0;
     uint64_t host_bytes = 0, total_bytes = 0;  // payload in host memory / all (lane choice)
-    bool submitted = false, completed = false;
-    int64_t mismatches = 0;
+    bool submitted = false;
+    std::atomic<bool> completed{false};    // results on the host and counted
+    std::atomic<int64_t> mismatches{0};
+    // Completion callback of the latest submit: done_ev fires
+    // before the host function runs, so a batch is only free for the next
+    // submit / reset / destroy once the callback has RETURNED as well; until
+    // then those calls return -EBUSY (destroy waits), so the next run cannot
+    // overwrite the verdicts the callback is reading.
+    void (*user_done)(void*) = nullptr;
+    void* user_arg = nullptr;
+    std::atomic<int> cb_running{0};
 };
 
 namespace {
@@ -172,17 +204,33 @@ void free_batch(photon_crc_msg_batch* b) {
     delete b;
 }
 
+// Count the mismatches of a finished run (results already on the host).
+void settle(photon_crc_msg_batch* b) {
+    int64_t bad = 0;
+    for (uint64_t i = 0; i < b->nmsg; ++i) bad += b->h_out[i] != b->h_expect[i];
+    b->mismatches.store(bad, std::memory_order_relaxed);
+    b->completed.store(true, std::memory_order_release);
+}
+
+// The host function of a submit with a callback: runs after done_ev (stream
+// order), so the verdicts are on the host. It settles the batch WITHOUT any
+// HIP call (host functions must not call HIP), so result() inside the
+// callback needs none either, then runs the user's callback.
+void done_trampoline(void* p) {
+    auto* b = static_cast<photon_crc_msg_batch*>(p);
+    if (!b->completed.load(std::memory_order_acquire)) settle(b);
+    b->user_done(b->user_arg);
+    b->cb_running.store(0, std::memory_order_release);
+}
+
 // Results are on the host: count mismatches once.
 int64_t finish(photon_crc_msg_batch* b) {
-    if (!b->completed) {
+    if (!b->completed.load(std::memory_order_acquire)) {
         hipError_t e = hipEventSynchronize(b->done_ev);
         if (e != hipSuccess) return report_hip_error(e, "hipEventSynchronize");
-        int64_t bad = 0;
-        for (uint64_t i = 0; i < b->nmsg; ++i) bad += b->h_out[i] != b->h_expect[i];
-        b->mismatches = bad;
-        b->completed = true;
+        settle(b);
     }
-    return b->mismatches;
+    return b->mismatches.load(std::memory_order_relaxed);
 }
 
 }  // namespace
@@ -318,6 +366,7 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
 void photon_crc_msg_batch_destroy(photon_crc_msg_batch* b) {
     if (!b) return;
     if (b->submitted && !b->completed) (void)hipEventSynchronize(b->done_ev);
+    while (b->cb_running.load(std::memory_order_acquire)) std::this_thread::yield();  // its callback returns first
     free_batch(b);
 }
 
@@ -326,25 +375,48 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
     if (!b || (iovcnt && !iov)) return report_error(-EINVAL, "null batch or iovector");
     if (b->submitted) return report_error(-EBUSY, "batch already submitted; reset it first");
     const bool has_body = body && body_length;  // serialize.h:271
-    if (b->nmsg >= b->max_msg || b->nseg + iovcnt + (has_body ? 1 : 0) > b->max_seg)
-        return report_error(-ENOSPC, "batch is full");
+    // The body is the message object itself (DeserializerIOV::deserialize
+    // passes t, serialize.h:462-463) unless the batch is DETACHED_BODY: then
+    // Crc32Hasher accumulates the payload's CRC INTO m_checksum, which is the
+    // body's first 4 bytes (the CheckedMessage<> base of a Photon message),
+    // and hashes the body with it. A CRC whose init equals its first data
+    // word is the CRC (init 0) of the data with that word zeroed, so the
+    // reference's value is crc32c(body with m_checksum = 0) and the payload
+    // does not enter it (tests/golden/ioalloc_binding.json).
+    const bool object_body = has_body && !(b->flags & PHOTON_CRC_BATCH_DETACHED_BODY);
+    if (object_body && body_length < 4) return report_error(-EINVAL, "message body shorter than its m_checksum");
+    const uint32_t nput = object_body ? 1 : iovcnt + (has_body ? 1 : 0);
+    if (b->nmsg >= b->max_msg || b->nseg + nput > b->max_seg) return report_error(-ENOSPC, "batch is full");
     const bool trusted = b->flags & PHOTON_CRC_BATCH_TRUSTED;
     uint64_t s = b->nseg;
     uint64_t host = 0, total = 0;
-    auto put = [&](const void* p, uint64_t n) -> int {
+    auto put = [&](const void* p, uint64_t n, bool zero_field) -> int {
         if (!n) return 0;  // crc32c_extend over 0 bytes is the identity
         bool in_host = true;  // trusted batches: assume RPC payloads in pinned host memory
         const void* d = trusted ? p : device_address(p, n, &in_host);
         if (!d) return report_error(-EFAULT, "segment is not device-accessible (pin it: photon_crc_pinned_allocate)");
+        if (zero_field) {  // validate_checksum's `m_checksum = Hasher::init_value()` (serialize.h:268)
+            if (in_host) {
+                memset(const_cast<void*>(p), 0, 4);
+            } else {
+                static const uint32_t zero = 0;
+                hipError_t e = hipMemcpy(const_cast<void*>(d), &zero, 4, hipMemcpyHostToDevice);
+                if (e != hipSuccess) return report_hip_error(e, "hipMemcpy(m_checksum = 0)");
+            }
+        }
         b->h_iov[s++] = photon_crc_iovec{d, n};
         total += n;
         if (in_host) host += n;
         return 0;
     };
-    for (uint32_t k = 0; k < iovcnt; ++k)
-        if (int rc = put(iov[k].base, iov[k].len)) return rc;
-    if (has_body)
-        if (int rc = put(body, body_length)) return rc;
+    if (object_body) {
+        if (int rc = put(body, body_length, true)) return rc;
+    } else {
+        for (uint32_t k = 0; k < iovcnt; ++k)
+            if (int rc = put(iov[k].base, iov[k].len, false)) return rc;
+        if (has_body)
+            if (int rc = put(body, body_length, false)) return rc;
+    }
     b->nseg = s;
     b->host_bytes += host;
     b->total_bytes += total;
@@ -355,6 +427,8 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
 
 int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*done)(void* arg), void* arg) {
     if (!b) return report_error(-EINVAL, "null batch");
+    if (b->cb_running.load(std::memory_order_acquire))
+        return report_error(-EBUSY, "completion callback of the previous submit still running");
     if (b->submitted && !b->completed) {
         // A caller driven by the `done` callback never called wait(): if the
         // previous submit has finished, settle it and go on; -EBUSY only while
@@ -365,6 +439,7 @@ int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*do
         int64_t frc = finish(b);
         if (frc < 0) return (int)frc;
     }
+    b->completed.store(false, std::memory_order_relaxed);  // before anything of this run is enqueued
     DeviceScope scope(b->dev);
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e = hipSuccess;
@@ -385,10 +460,15 @@ int photon_crc_msg_batch_submit(photon_crc_msg_batch* b, void* stream, void (*do
         }
     }
     e = hipEventRecord(b->done_ev, st);
-    if (e == hipSuccess && done) e = hipLaunchHostFunc(st, done, arg);
+    if (e == hipSuccess && done) {
+        b->user_done = done;
+        b->user_arg = arg;
+        b->cb_running.store(1, std::memory_order_release);
+        e = hipLaunchHostFunc(st, done_trampoline, b);
+        if (e != hipSuccess) b->cb_running.store(0, std::memory_order_release);
+    }
     if (e != hipSuccess) return report_hip_error(e, "completion");
     b->submitted = true;
-    b->completed = false;
     return 0;
 }
 
@@ -416,14 +496,17 @@ uint64_t photon_crc_msg_batch_count(const photon_crc_msg_batch* b) { return b ? 
 
 int photon_crc_msg_batch_reset(photon_crc_msg_batch* b) {
     if (!b) return report_error(-EINVAL, "null batch");
+    if (b->cb_running.load(std::memory_order_acquire))
+        return report_error(-EBUSY, "completion callback of the previous submit still running");
     if (b->submitted && !b->completed) {
         int64_t rc = finish(b);
         if (rc < 0) return (int)rc;
     }
     b->nmsg = b->nseg = 0;
     b->host_bytes = b->total_bytes = 0;
-    b->submitted = b->completed = false;
-    b->mismatches = 0;
+    b->submitted = false;
+    b->completed.store(false, std::memory_order_relaxed);
+    b->mismatches.store(0, std::memory_order_relaxed);
     return 0;
 }
 

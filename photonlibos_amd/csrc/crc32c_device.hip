@@ -169,11 +169,15 @@ struct ScratchBuf {
     uint64_t cap;
     hipEvent_t last;  // recorded after the latest use
     bool busy;
+    bool zeroed;      // a state buffer: zero when created, and every user leaves it zero
 };
 std::mutex g_scr_mu;
 std::vector<ScratchBuf*> g_scr;
+int64_t scratch_trim_locked(bool all);
 
-int scratch_alloc(void** p, uint64_t bytes, hipStream_t st) {
+// zeroed: a small state buffer (the long-buffer kernel's accumulator and
+// ticket) that is zero when leased; the kernel that uses it leaves it zero.
+int scratch_alloc(void** p, uint64_t bytes, hipStream_t st, bool zeroed = false) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
@@ -181,8 +185,9 @@ int scratch_alloc(void** p, uint64_t bytes, hipStream_t st) {
     bool wait = false;
     {
         std::lock_guard<std::mutex> lk(g_scr_mu);
+        (void)scratch_trim_locked(false);
         for (ScratchBuf* b : g_scr) {
-            if (b->busy || b->dev != dev || b->cap < bytes) continue;
+            if (b->busy || b->dev != dev || b->cap < bytes || b->zeroed != zeroed) continue;
             const bool done = hipEventQuery(b->last) == hipSuccess;
             if (!lease || (done && wait)) {
                 lease = b;
@@ -193,12 +198,17 @@ int scratch_alloc(void** p, uint64_t bytes, hipStream_t st) {
         if (lease) lease->busy = true;
     }
     if (!lease) {
-        auto* b = new ScratchBuf{dev, nullptr, 0, nullptr, true};
-        uint64_t cap = 1u << 20;
+        auto* b = new ScratchBuf{dev, nullptr, 0, nullptr, true, zeroed};
+        uint64_t cap = zeroed ? 256u : 1u << 20;
         while (cap < bytes) cap <<= 1;
         if ((e = hipMalloc(&b->p, cap)) != hipSuccess) {
             delete b;
             return hip_fail(e, "hipMalloc(scratch)");
+        }
+        if (zeroed && (e = hipMemset(b->p, 0, cap)) != hipSuccess) {
+            (void)hipFree(b->p);
+            delete b;
+            return hip_fail(e, "hipMemset(state)");
         }
         if ((e = hipEventCreateWithFlags(&b->last, hipEventDisableTiming)) != hipSuccess) {
             (void)hipFree(b->p);
@@ -216,6 +226,38 @@ int scratch_alloc(void** p, uint64_t bytes, hipStream_t st) {
     }
     *p = lease->p;
     return 0;
+}
+
+// Buffers kept for reuse are capped (a buffer used to keep the
+// size of the largest request it ever served for the life of the process):
+// an idle buffer above kScratchKeep bytes, or any idle buffer beyond
+// kScratchMaxIdle bytes of idle scratch on its device, is freed by the next
+// lease once its last use has completed. photon_crc_scratch_release() frees
+// every idle buffer whose work has completed.
+constexpr uint64_t kScratchKeep = 64ull << 20;
+constexpr uint64_t kScratchMaxIdle = 256ull << 20;
+
+// Free idle buffers whose last use has completed: all of them (`all`), or the
+// oversized ones and those beyond the idle cap. Caller holds g_scr_mu.
+int64_t scratch_trim_locked(bool all) {
+    int64_t freed = 0;
+    std::vector<uint64_t> idle_dev(64, 0);
+    for (auto it = g_scr.begin(); it != g_scr.end();) {
+        ScratchBuf* b = *it;
+        const bool idle = !b->busy && hipEventQuery(b->last) == hipSuccess;
+        uint64_t& kept = idle_dev[b->dev & 63];
+        if (idle && (all || b->cap > kScratchKeep || kept + b->cap > kScratchMaxIdle)) {
+            (void)hipEventDestroy(b->last);
+            (void)hipFree(b->p);
+            freed += (int64_t)b->cap;
+            delete b;
+            it = g_scr.erase(it);
+            continue;
+        }
+        if (idle) kept += b->cap;
+        ++it;
+    }
+    return freed;
 }
 
 // Return a lease: its buffer may be reused once the work enqueued on `st`
@@ -650,6 +692,79 @@ int pipe_init(HostPipe& p) {
         p.ready = true;
     }
     return 0;
+}
+
+// One long buffer (photon_crc32c_extend_device, photon_crc64ecma_extend_device):
+// T chunks (the first one shorter), one per wavefront of the long kernels.
+// Up to 256 KiB: at most 16 chunks of >= 4 KiB, one workgroup, the result
+// written directly (latency). Above: chunks of >= 16 KiB (4 KiB multiples),
+// as many as the grid has waves (16 per CU; VERDICT r2: the piece batch used
+// to fill half, or an eighth, of the chip), T <= 4096 (the two 64-entry power
+// tables of the kernels).
+struct LongPlan {
+    uint64_t chunk, first, nchunks, grid;
+};
+
+LongPlan long_plan(uint64_t n, int cus) {
+    const bool small = n <= (256u << 10);
+    uint64_t waves = small ? 16 : 16ull * (uint64_t)cus;
+    if (waves > 4096) waves = 4096;
+    uint64_t chunk = ((n + waves - 1) / waves + 4095) & ~4095ull;
+    const uint64_t lo = small ? 4096 : 16384;
+    if (chunk < lo) chunk = lo;
+    LongPlan p;
+    p.chunk = chunk;
+    p.nchunks = n ? (n + chunk - 1) / chunk : 1;
+    p.first = n - (p.nchunks - 1) * chunk;
+    p.grid = (p.nchunks + kWaves - 1) / kWaves;
+    return p;
+}
+
+// X^j and X^(64 j), j < 64, X = x^(8 * chunk) (CRC-32C or CRC-64/ECMA),
+// computed on first use per chunk size and kept (callers repeat sizes).
+struct LongPowers {
+    uint32_t p32[64], q32[64];
+    uint64_t p64[64], q64[64];
+};
+
+const LongPowers& long_powers(uint64_t chunk, bool crc64) {
+    static std::mutex mu;
+    static std::vector<std::pair<uint64_t, LongPowers*>> cache[2];
+    thread_local LongPowers overflow;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto& e : cache[crc64])
+            if (e.first == chunk) return *e.second;
+    }
+    LongPowers* t = new LongPowers();
+    if (crc64) {
+        const uint64_t y = xpow64(8 * chunk), y64 = xpow64(512 * chunk);
+        t->p64[0] = t->q64[0] = kOne64;
+        for (int j = 1; j < 64; ++j) {
+            t->p64[j] = mulmod64(t->p64[j - 1], y);
+            t->q64[j] = mulmod64(t->q64[j - 1], y64);
+        }
+    } else {
+        const uint32_t x = xpow(8 * chunk), x64 = xpow(512 * chunk);
+        t->p32[0] = t->q32[0] = kOne;
+        for (int j = 1; j < 64; ++j) {
+            t->p32[j] = mulmod(t->p32[j - 1], x);
+            t->q32[j] = mulmod(t->q32[j - 1], x64);
+        }
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : cache[crc64])
+        if (e.first == chunk) {
+            delete t;
+            return *e.second;
+        }
+    if (cache[crc64].size() >= 256) {  // many distinct sizes: compute per call
+        overflow = *t;
+        delete t;
+        return overflow;
+    }
+    cache[crc64].emplace_back(chunk, t);
+    return *t;
 }
 
 }  // namespace
@@ -1177,41 +1292,32 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
                                    void* stream) {
     if (!d_out || (!d_data && nbytes)) return fail(-EINVAL, "null buffer or output");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // Pieces as photon_crc32c_extend_device: >= 16 KiB, 4 KiB multiples, <= 4096.
-    uint64_t piece = (nbytes + 4095) / 4096;
-    piece = (piece + 4095) & ~4095ull;
-    if (piece < (16u << 10)) piece = 16u << 10;
-    const uint64_t k = nbytes ? (nbytes + piece - 1) / piece : 1;
-    if (k == 1)  // (nbytes == 0 gives the seed, as crc64ecma_extend does)
-        return photon_crc64ecma_batch_strided(d_data, nbytes, nbytes, 1, seed, nullptr, d_out, stream);
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    void* scratch = nullptr;
-    if (int rc = scratch_alloc(&scratch, k * sizeof(photon_crc_iovec) + k * 8, st)) return rc;
-    hipError_t e;
-    auto* iov = static_cast<photon_crc_iovec*>(scratch);
-    auto* crcs = reinterpret_cast<uint64_t*>(iov + k);
-    hipLaunchKernelGGL(crc32c_split_kernel, dim3((k + 255) / 256), dim3(256), 0, st,
-                       static_cast<const uint8_t*>(d_data), nbytes, piece, k, iov);
-    e = hipGetLastError();
-    int rc = e == hipSuccess ? 0 : hip_fail(e, "split kernel launch");
-    if (!rc) {
-        Batch64Args a{};
-        a.iov = iov;
-        a.count = k;
-        a.out = crcs;
-        a.seed0 = 0;
-        rc = launch_batch64(a, piece, st);
+    const LongPlan lp = long_plan(nbytes, cus);
+    const LongPowers& pw = long_powers(lp.chunk, true);
+    Long64Args a{};
+    a.data = static_cast<const uint8_t*>(d_data);
+    a.first = lp.first;
+    a.chunk = lp.chunk;
+    a.nchunks = lp.nchunks;
+    a.seed = seed;
+    a.out = d_out;
+    memcpy(a.xp, pw.p64, sizeof(a.xp));
+    memcpy(a.xq, pw.q64, sizeof(a.xq));
+    void* state = nullptr;  // {accumulator, ticket}, left zeroed by the kernel
+    if (lp.grid > 1) {
+        if (int rc = scratch_alloc(&state, 16, st, true)) return rc;
+        a.acc = static_cast<uint64_t*>(state);
     }
-    if (!rc) {
-        hipLaunchKernelGGL(crc64_fold_pieces_kernel, dim3(1), dim3(1024), 0, st, crcs, k, piece,
-                           nbytes - (k - 1) * piece, seed, nbytes, xpow64(8 * piece), d_out, pow_table64());
-        e = hipGetLastError();
-        if (e != hipSuccess) rc = hip_fail(e, "crc64_fold_pieces_kernel launch");
+    hipLaunchKernelGGL(crc64_long_kernel, dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(64));
+    const hipError_t e = hipGetLastError();
+    int rc = e == hipSuccess ? 0 : hip_fail(e, "crc64_long_kernel launch");
+    if (state) {
+        const int frc = scratch_free(state, st);
+        if (!rc) rc = frc;
     }
-    const int frc = scratch_free(scratch, st);
-    if (!rc) rc = frc;
     return rc;
 }
 
@@ -1286,44 +1392,38 @@ int photon_crc32c_trim_batch(const photon_crc_component* d_all, const photon_crc
 int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, void* stream) {
     if (!d_out || (!d_data && nbytes)) return fail(-EINVAL, "null buffer or output");
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // Pieces: >= 16 KiB, 4 KiB multiples (whole rows for every lane group),
-    // at most 4096 of them (enough waves to fill 256 CUs).
-    uint64_t piece = (nbytes + 4095) / 4096;
-    piece = (piece + 4095) & ~4095ull;
-    if (piece < (16u << 10)) piece = 16u << 10;
-    const uint64_t k = nbytes ? (nbytes + piece - 1) / piece : 1;
-    if (k == 1)  // (nbytes == 0 gives the seed, as crc32c_extend does)
-        return photon_crc32c_batch_strided(d_data, nbytes, nbytes, 1, seed, nullptr, d_out, stream);
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    // Stream-ordered scratch: k descriptors + k piece CRCs.
-    void* scratch = nullptr;
-    if (int rc = scratch_alloc(&scratch, k * sizeof(photon_crc_iovec) + k * 4, st)) return rc;
-    hipError_t e;
-    auto* iov = static_cast<photon_crc_iovec*>(scratch);
-    auto* crcs = reinterpret_cast<uint32_t*>(iov + k);
-    hipLaunchKernelGGL(crc32c_split_kernel, dim3((k + 255) / 256), dim3(256), 0, st,
-                       static_cast<const uint8_t*>(d_data), nbytes, piece, k, iov);
-    e = hipGetLastError();
-    int rc = e == hipSuccess ? 0 : hip_fail(e, "crc32c_split_kernel launch");
-    if (!rc) {
-        BatchArgs a{};
-        a.iov = iov;
-        a.count = k;
-        a.out = crcs;
-        rc = launch_batch(a, piece, st);
+    const LongPlan lp = long_plan(nbytes, cus);
+    const LongPowers& pw = long_powers(lp.chunk, false);
+    LongArgs a{};
+    a.data = static_cast<const uint8_t*>(d_data);
+    a.first = lp.first;
+    a.chunk = lp.chunk;
+    a.nchunks = lp.nchunks;
+    a.seed = seed;
+    a.out = d_out;
+    memcpy(a.xp, pw.p32, sizeof(a.xp));
+    memcpy(a.xq, pw.q32, sizeof(a.xq));
+    void* state = nullptr;  // {accumulator, ticket}, left zeroed by the kernel
+    if (lp.grid > 1) {
+        if (int rc = scratch_alloc(&state, 8, st, true)) return rc;
+        a.acc = static_cast<uint32_t*>(state);
     }
-    if (!rc) rc = photon_crc32c_combine_series_device(crcs, (uint32_t)piece, (uint32_t)(k - 1), d_out, stream);
-    if (!rc) {
-        hipLaunchKernelGGL(crc32c_extend_finish_kernel, dim3(1), dim3(1), 0, st, d_out, crcs + (k - 1),
-                           nbytes - (k - 1) * piece, seed, nbytes, pow_table());
-        e = hipGetLastError();
-        if (e != hipSuccess) rc = hip_fail(e, "crc32c_extend_finish_kernel launch");
+    hipLaunchKernelGGL((crc32c_long_kernel<4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(64));
+    const hipError_t e = hipGetLastError();
+    int rc = e == hipSuccess ? 0 : hip_fail(e, "crc32c_long_kernel launch");
+    if (state) {
+        const int frc = scratch_free(state, st);
+        if (!rc) rc = frc;
     }
-    const int frc = scratch_free(scratch, st);
-    if (!rc) rc = frc;
     return rc;
+}
+
+int64_t photon_crc_scratch_release(void) {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    return scratch_trim_locked(true);
 }
 
 int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
@@ -1374,6 +1474,13 @@ uint32_t (*g_host_crc)(const uint8_t*, size_t, uint32_t) = nullptr;
 uint64_t (*g_host_crc64)(const uint8_t*, size_t, uint64_t) = nullptr;
 void (*g_host_series)(const uint8_t*, uint32_t, uint32_t, uint32_t*) = nullptr;
 uint32_t (*g_host_cseries)(uint32_t*, uint32_t, uint32_t) = nullptr;
+
+// The saved host engines, read by the routed wrappers (written before the
+// routed pointers are published, see photon_crc_set_device_dispatch).
+template <typename F>
+F host_engine(F* slot) {
+    return __atomic_load_n(slot, __ATOMIC_RELAXED);
+}
 
 // Device owning `p`, or -1 for host / unregistered memory.
 int device_of(const void* p) {
@@ -1433,7 +1540,8 @@ void for_host_chunks(const uint8_t* p, size_t n, const char* what, F f) {
 }
 
 uint32_t host_crc_of_device(const uint8_t* p, size_t n, uint32_t crc) {
-    for_host_chunks(p, n, "crc32c_extend", [&](const uint8_t* h, size_t k) { crc = g_host_crc(h, k, crc); });
+    const auto eng = host_engine(&g_host_crc);
+    for_host_chunks(p, n, "crc32c_extend", [&](const uint8_t* h, size_t k) { crc = eng(h, k, crc); });
     return crc;
 }
 
@@ -1458,7 +1566,7 @@ int with_scratch(uint64_t bytes, void* h_out, uint64_t out_bytes, F f) {
 
 uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     const int dev = n ? device_of(p) : -1;
-    if (dev < 0) return g_host_crc(p, n, crc);
+    if (dev < 0) return host_engine(&g_host_crc)(p, n, crc);
     DeviceScope scope(dev);
     uint32_t r = 0;
     int rc = with_scratch(4, &r, 4, [&](void* d) {
@@ -1471,12 +1579,12 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
 
 void dispatch_series(const uint8_t* buf, uint32_t part, uint32_t n, uint32_t* parts) {
     const int dev = (part && n) ? device_of(buf) : -1;
-    if (dev < 0) return g_host_series(buf, part, n, parts);
+    if (dev < 0) return host_engine(&g_host_series)(buf, part, n, parts);
     DeviceScope scope(dev);
     // The device form keeps the SSE4.2 engine's rule (parts < 8 B give 0,
     // crc.cpp:481-500); when the saved host engine is crc32c_series_sw those
     // parts get their real CRCs (crc.cpp:474-478), so run the plain batch.
-    const bool sw = g_host_series == crc32c_series_sw;
+    const bool sw = host_engine(&g_host_series) == crc32c_series_sw;
     auto run = [&](uint32_t* out) {
         return sw ? photon_crc32c_batch_strided(buf, part, part, n, 0, nullptr, out, nullptr)
                   : photon_crc32c_series_device(buf, part, n, out, nullptr);
@@ -1499,7 +1607,7 @@ void dispatch_series(const uint8_t* buf, uint32_t part, uint32_t n, uint32_t* pa
         // whole parts only: gather across chunk edges into part_buf
         part_buf.insert(part_buf.end(), hp, hp + k);
         size_t whole = part_buf.size() / part;
-        g_host_series(part_buf.data(), part, (uint32_t)whole, h.data() + i);
+        host_engine(&g_host_series)(part_buf.data(), part, (uint32_t)whole, h.data() + i);
         i += whole;
         part_buf.erase(part_buf.begin(), part_buf.begin() + whole * part);
     });
@@ -1513,7 +1621,7 @@ void dispatch_series(const uint8_t* buf, uint32_t part, uint32_t n, uint32_t* pa
 
 uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
     const int dev = n ? device_of(crc) : -1;
-    if (dev < 0) return g_host_cseries(crc, part, n);
+    if (dev < 0) return host_engine(&g_host_cseries)(crc, part, n);
     DeviceScope scope(dev);
     uint32_t r = 0;
     int rc = with_scratch(4, &r, 4, [&](void* d) {
@@ -1524,12 +1632,12 @@ uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
     std::vector<uint32_t> h(n);
     hipError_t e = hipMemcpy(h.data(), crc, 4ull * n, hipMemcpyDeviceToHost);
     if (e != hipSuccess) routed_abort("crc32c_combine_series", e);
-    return g_host_cseries(h.data(), part, n);
+    return host_engine(&g_host_cseries)(h.data(), part, n);
 }
 
 uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     const int dev = n ? device_of(p) : -1;
-    if (dev < 0) return g_host_crc64(p, n, crc);
+    if (dev < 0) return host_engine(&g_host_crc64)(p, n, crc);
     DeviceScope scope(dev);
     uint64_t r = 0;
     int rc = with_scratch(8, &r, 8, [&](void* d) {
@@ -1537,31 +1645,43 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     });
     if (!rc) return r;
     routed_failure("crc64ecma_extend", rc);
-    for_host_chunks(p, n, "crc64ecma_extend", [&](const uint8_t* h, size_t k) { crc = g_host_crc64(h, k, crc); });
+    const auto eng = host_engine(&g_host_crc64);
+    for_host_chunks(p, n, "crc64ecma_extend", [&](const uint8_t* h, size_t k) { crc = eng(h, k, crc); });
     return crc;
 }
 
 }  // namespace
 }  // namespace pcrc
 
+// The reference writes its dispatch pointers once, before main (crc.cpp:137-175),
+// and callers read them with plain loads through the inline wrappers of
+// crc32c.h (which this library keeps unchanged). Switching them at run time
+// while other threads call through them is therefore done
+// with single aligned RELEASE stores of whole pointers: a concurrent caller
+// loads either the old or the new engine -- never a torn pointer -- and both
+// give the same CRC for every input (the routed wrappers send host pointers
+// to the saved host engine, which is published before the routed pointer and
+// never cleared). A caller that loaded the routed pointer just before a
+// switch-off still runs the routed wrapper once, with the same result.
 extern "C" int photon_crc_set_device_dispatch(int on) {
     using namespace pcrc;
     std::lock_guard<std::mutex> lk(g_dispatch_mu);
     if (on && !g_dispatch_on) {
-        g_host_crc = crc32c_auto;
-        g_host_series = crc32c_series_auto;
-        g_host_cseries = crc32c_combine_series_auto;
-        crc32c_auto = dispatch_crc;
-        crc32c_series_auto = dispatch_series;
-        crc32c_combine_series_auto = dispatch_combine_series;
-        g_host_crc64 = crc64ecma_auto;
-        crc64ecma_auto = dispatch_crc64;
+        __atomic_store_n(&g_host_crc, __atomic_load_n(&crc32c_auto, __ATOMIC_ACQUIRE), __ATOMIC_RELAXED);
+        __atomic_store_n(&g_host_series, __atomic_load_n(&crc32c_series_auto, __ATOMIC_ACQUIRE), __ATOMIC_RELAXED);
+        __atomic_store_n(&g_host_cseries, __atomic_load_n(&crc32c_combine_series_auto, __ATOMIC_ACQUIRE),
+                         __ATOMIC_RELAXED);
+        __atomic_store_n(&g_host_crc64, __atomic_load_n(&crc64ecma_auto, __ATOMIC_ACQUIRE), __ATOMIC_RELAXED);
+        __atomic_store_n(&crc32c_auto, &dispatch_crc, __ATOMIC_RELEASE);
+        __atomic_store_n(&crc32c_series_auto, &dispatch_series, __ATOMIC_RELEASE);
+        __atomic_store_n(&crc32c_combine_series_auto, &dispatch_combine_series, __ATOMIC_RELEASE);
+        __atomic_store_n(&crc64ecma_auto, &dispatch_crc64, __ATOMIC_RELEASE);
         g_dispatch_on = true;
     } else if (!on && g_dispatch_on) {
-        crc32c_auto = g_host_crc;
-        crc32c_series_auto = g_host_series;
-        crc32c_combine_series_auto = g_host_cseries;
-        crc64ecma_auto = g_host_crc64;
+        __atomic_store_n(&crc32c_auto, g_host_crc, __ATOMIC_RELEASE);
+        __atomic_store_n(&crc32c_series_auto, g_host_series, __ATOMIC_RELEASE);
+        __atomic_store_n(&crc32c_combine_series_auto, g_host_cseries, __ATOMIC_RELEASE);
+        __atomic_store_n(&crc64ecma_auto, g_host_crc64, __ATOMIC_RELEASE);
         g_dispatch_on = false;
     }
     return g_dispatch_err.exchange(0) ? -EIO : 0;

@@ -11,6 +11,14 @@
 #ifndef PCRC_LANE_SEL
 #define PCRC_LANE_SEL 1  // per-lane v_perm selectors instead of rotating the word (+0.3 % on C2)
 #endif
+// buf_body's row loop (A/B variants): 0 = one register set
+// copied cur <- nxt on the loop edge (the default); 1 = the compiler's unroll
+// by two (no copies; the next step's loads issued before this step's land:
+// 8 rows in flight); 2 = two register sets by hand, the next step's loads
+// issued only once this step's have landed (4 rows in flight, no copies).
+#ifndef PCRC_BODY
+#define PCRC_BODY 0
+#endif
 
 namespace pcrc {
 
@@ -478,15 +486,44 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
     w.w = head_word_sel(w.w, off + 12, g.s0, seed);
     if (gl >= g.nb) w = make_uint4(0, 0, 0, 0);
     uint32_t pc = lag16(lds, w, la);
-    // Full rows 1..full-1: U rows per step, the next U in flight. (Measured
-    // and dropped: the loop unrolled by two with two register sets, no copy
-    // on the loop edge: 9 % fewer instructions, C2 -2.5 points, C3 +0.6.)
+    // Full rows 1..full-1: U rows per step, the next U in flight.
     uint64_t row = 1;
     const uint8_t* lp = g.lp;
     if (row + U <= g.full) {
+#if PCRC_BODY == 2
+        uint4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = pre.cur[u];
+        auto issue = [&](uint4(&w)[U]) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the step about to be reduced has landed
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = load16(lp + (row + U + u) * (16 * G));
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        for (;;) {
+            if (row + 2 * U > g.full) {
+                pc = lag_column_step<U>(lds, pc, a, la);
+                row += U;
+                break;
+            }
+            issue(b);
+            pc = lag_column_step<U>(lds, pc, a, la);
+            row += U;
+            if (row + 2 * U > g.full) {
+                pc = lag_column_step<U>(lds, pc, b, la);
+                row += U;
+                break;
+            }
+            issue(a);
+            pc = lag_column_step<U>(lds, pc, b, la);
+            row += U;
+        }
+#else
         uint4 cur[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = pre.cur[u];
+#pragma unroll PCRC_BODY + 1
         for (; row + 2 * U <= g.full; row += U) {
             uint4 nxt[U];
 #pragma unroll
@@ -497,6 +534,7 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
         }
         pc = lag_column_step<U>(lds, pc, cur, la);
         row += U;
+#endif
     }
     for (; row < g.full; ++row) pc = sstep(lds, pc, la, lag16(lds, load16(lp + row * (16 * G)), la));
     // Partial last row.
@@ -649,7 +687,12 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                         }
                         uint32_t part = 0;
 #pragma unroll
-                        for (int w = 0; w < kFoldW; ++w) part ^= ((acc >> (gl * kFoldW + w)) & 1u) ? kb[w] : 0u;
+                        for (int w = 0; w < kFoldW; ++w) {
+                            // bit >= 32 only for 64-lane groups (kb[w] = 0
+                            // there): clamp so the shift stays defined
+                            const uint32_t bit = gl * kFoldW + w;
+                            part ^= (bit < 32 && ((acc >> (bit & 31u)) & 1u)) ? kb[w] : 0u;
+                        }
                         acc = group_xor<G>(part) ^ c;  // acc and c are valid on every lane of the group
                     } else {
                         // 4-lane groups (segments < 2 KiB): 8 basis words per
@@ -1292,23 +1335,68 @@ __global__ void crc32c_trim_kernel(const photon_crc_component* all, const photon
     out[i] = crc;
 }
 
-// Split one long buffer into `k` pieces of `piece` bytes (the last one
-// shorter) for the batch kernel (photon_crc32c_extend_device).
-__global__ void crc32c_split_kernel(const uint8_t* data, uint64_t nbytes, uint64_t piece, uint64_t k,
-                                    photon_crc_iovec* iov) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
-    const uint64_t off = i * piece;
-    iov[i].base = data + off;
-    iov[i].len = i + 1 < k ? piece : nbytes - off;
-}
+// ------------------------------------------------------- one long buffer
+// photon_crc32c_extend_device (crc32c_extend, crc32c.h:30-33, over ONE
+// device buffer) in ONE launch that fills the chip. The buffer is cut into
+// T chunks, one per wavefront: chunk 0 = [0, first), chunk t >= 1 = [first +
+// (t-1)*chunk, first + t*chunk), so every chunk after the first is full and
+// ends (T-1-t)*chunk bytes before the end. A wave computes its chunk's CRC
+// (the seed in chunk 0 only; buffer_crc with 64 lanes) and shifts it to the
+// end of the buffer: crc_t * X^(T-1-t), X = x^(8*chunk), as two GF(2)
+// products by host-computed powers X^(m%64) and X^(64*(m/64)) (T <= 4096).
+// By linearity (crc.cpp:393-405) the buffer's CRC is the XOR of the shifted
+// chunk CRCs: waves XOR-reduce in registers and LDS, each workgroup XORs its
+// value into an accumulator word with one device-scope atomic, and the last
+// workgroup (ticket counter) writes the result and zeroes accumulator and
+// ticket. One workgroup (T <= 16) writes the result directly.
+struct LongArgs {
+    const uint8_t* data;
+    uint64_t first;     // bytes of chunk 0 (1..chunk; the whole buffer when T == 1)
+    uint64_t chunk;
+    uint64_t nchunks;   // T
+    uint32_t seed;
+    uint32_t* out;
+    uint32_t* acc;      // {accumulator, ticket}: zero before the launch (grid > 1 only)
+    uint32_t xp[64];    // X^j
+    uint32_t xq[64];    // X^(64 j)
+};
 
-// out = (out * x^(8*last_len) ^ last_crc) ^ seed * x^(8*nbytes): append the
-// last piece to the folded equal pieces and apply crc32c_extend's seed.
-__global__ void crc32c_extend_finish_kernel(uint32_t* out, const uint32_t* last_crc, uint64_t last_len,
-                                            uint32_t seed, uint64_t nbytes, PowTable pt) {
-    uint32_t c = shift_bytes_tab(*out, last_len, pt) ^ *last_crc;
-    *out = c ^ shift_bytes_tab(seed, nbytes, pt);
+template <int U>
+__global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneConsts kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<64>() / 4];
+    __shared__ uint32_t red[kWaves];
+    build_tables<64>(lds, kc);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = wave_id();
+    const LaneAddr la = lane_addr(lane);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    uint32_t acc = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < a.nchunks; t += nwaves) {
+        const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
+        const uint64_t n = t ? a.chunk : a.first;
+        uint32_t crc = buffer_crc<64, U>(lds, p, n, t ? 0u : a.seed, lane, la);
+        const uint64_t m = a.nchunks - 1 - t;  // wave-uniform
+        crc = mulmod(mulmod(crc, a.xp[m & 63u]), a.xq[(m >> 6) & 63u]);
+        acc ^= crc;
+    }
+    if (lane == 0) red[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v ^= red[w];
+        if (gridDim.x == 1) {
+            *a.out = v;
+        } else {
+            atomicXor(a.acc, v);
+            __threadfence();
+            if (atomicAdd(a.acc + 1, 1u) == gridDim.x - 1) {
+                __threadfence();
+                *a.out = atomicExch(a.acc, 0u);  // every workgroup's XOR has landed
+                atomicExch(a.acc + 1, 0u);
+            }
+        }
+    }
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {

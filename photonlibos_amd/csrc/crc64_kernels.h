@@ -314,6 +314,88 @@ __device__ __forceinline__ uint64_t finish64(uint2 q, uint32_t d, const uint32_t
     return x;
 }
 
+// The raw CRC-64 register after the bytes [p, p+n) from `init` (a group of
+// G lanes; valid on the group's first lane; crc64ecma_extend = ~reg with
+// init = ~crc, crc.cpp:119-122).
+template <int G>
+__device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint8_t* p, uint64_t n, uint64_t init,
+                                                 uint32_t gl, uint32_t lane, const LaneAddr64& la) {
+    constexpr int U = PCRC64_U;
+    uint64_t reg;
+    if (n < 64) {
+        reg = init;
+        if (gl == 0)
+            for (uint64_t k = 0; k < n; ++k) reg = bytestep64(lds, reg, load8(p + k), la);
+    } else {
+        const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
+        const uint8_t* e = p + n;
+        const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
+        const int s0 = (int)(p - a0);
+        const uint64_t nb = (uint64_t)(eb - a0) >> 4;
+        const uint64_t full = nb / G;
+        const uint64_t rows = (nb + G - 1) / G;
+        const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);
+        const uint8_t* lp = a0 + 16 * gl;
+        uint2 pc = make_uint2(0, 0);
+        // Row 0, the lead rows ((full-1) % U, so the U-row loop ends at the
+        // last full row), the first step's U rows and the partial last row
+        // are issued together: no row is loaded on its own and waited for.
+        const uint32_t lead = full >= 1 ? (uint32_t)((full - 1) % U) : 0u;
+        uint4 w0, wl[U - 1], cur[U], wp;
+        if (gl < nb) w0 = load16(lp);
+#pragma unroll
+        for (int u = 0; u < U - 1; ++u)
+            if ((uint32_t)u < lead) wl[u] = load16(lp + (1 + u) * (16 * G));
+        const bool steps = 1 + lead + U <= full;
+        if (steps) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = load16(lp + (1 + lead + u) * (16 * G));
+        }
+        const bool part = full >= 1 && full < rows && full * G + gl < nb;
+        if (part) wp = load16(lp + full * (16 * G));
+        // Row 0 (head: masked leading bytes + inverted init).
+        if (gl < nb) {
+            uint4 w = w0;
+            if (gl < 2) {
+                const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
+                const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
+                w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+            }
+            pc = lag16_64(lds, w, la);
+        }
+#pragma unroll
+        for (int u = 0; u < U - 1; ++u)
+            if ((uint32_t)u < lead) pc = sstep64(lds, pc, la, lag16_64(lds, wl[u], la));
+        uint64_t row = 1 + lead;
+        // U lagged blocks (independent) then U row shifts (the carried chain).
+        auto column_step = [&](const uint4(&w)[U]) {
+            uint2 c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) c[u] = lag16_64(lds, w[u], la);
+#pragma unroll
+            for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+        };
+        if (steps) {
+            for (; row + 2 * U <= full; row += U) {
+                uint4 nxt[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+                column_step(cur);
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            }
+            column_step(cur);
+        }
+        if (part) pc = sstep64(lds, pc, la, lag16_64(lds, wp, la));
+        // Q * x^(64 + 128 d) (Q -> P and the shift to the end of the blocks), XOR over the group.
+        const uint64_t f = finish64<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds, lane);
+        reg = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+        if (gl == 0)
+            for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
+    }
+    return reg;
+}
+
 // Any pointer / length / seed (iovec batches, ragged and unaligned buffers).
 template <int G>
 __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
@@ -323,7 +405,6 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp = lane / G;
     constexpr int GPW = 64 / G;
-    constexpr int U = PCRC64_U;
     const LaneAddr64 la = lane_addr64(lane);
 
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
@@ -342,79 +423,8 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
             }
             if (args.seeds) seed = args.seeds[bi];
         }
-        const uint64_t init = ~seed;  // crc.cpp:119-122: register starts at ~crc
-        uint64_t reg;
-        if (n < 64) {
-            reg = init;
-            if (gl == 0)
-                for (uint64_t k = 0; k < n; ++k) reg = bytestep64(lds, reg, load8(p + k), la);
-        } else {
-            const uint8_t* a0 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(15));
-            const uint8_t* e = p + n;
-            const uint8_t* eb = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(e) & ~uintptr_t(15));
-            const int s0 = (int)(p - a0);
-            const uint64_t nb = (uint64_t)(eb - a0) >> 4;
-            const uint64_t full = nb / G;
-            const uint64_t rows = (nb + G - 1) / G;
-            const uint32_t rlast = (uint32_t)(nb - (rows - 1) * G);
-            const uint8_t* lp = a0 + 16 * gl;
-            uint2 pc = make_uint2(0, 0);
-            // Row 0, the lead rows ((full-1) % U, so the U-row loop ends at the
-            // last full row), the first step's U rows and the partial last row
-            // are issued together: no row is loaded on its own and waited for.
-            const uint32_t lead = full >= 1 ? (uint32_t)((full - 1) % U) : 0u;
-            uint4 w0, wl[U - 1], cur[U], wp;
-            if (gl < nb) w0 = load16(lp);
-#pragma unroll
-            for (int u = 0; u < U - 1; ++u)
-                if ((uint32_t)u < lead) wl[u] = load16(lp + (1 + u) * (16 * G));
-            const bool steps = 1 + lead + U <= full;
-            if (steps) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = load16(lp + (1 + lead + u) * (16 * G));
-            }
-            const bool part = full >= 1 && full < rows && full * G + gl < nb;
-            if (part) wp = load16(lp + full * (16 * G));
-            // Row 0 (head: masked leading bytes + inverted init).
-            if (gl < nb) {
-                uint4 w = w0;
-                if (gl < 2) {
-                    const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
-                    const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
-                    w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-                }
-                pc = lag16_64(lds, w, la);
-            }
-#pragma unroll
-            for (int u = 0; u < U - 1; ++u)
-                if ((uint32_t)u < lead) pc = sstep64(lds, pc, la, lag16_64(lds, wl[u], la));
-            uint64_t row = 1 + lead;
-            // U lagged blocks (independent) then U row shifts (the carried chain).
-            auto column_step = [&](const uint4(&w)[U]) {
-                uint2 c[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) c[u] = lag16_64(lds, w[u], la);
-#pragma unroll
-                for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
-            };
-            if (steps) {
-                for (; row + 2 * U <= full; row += U) {
-                    uint4 nxt[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                    column_step(cur);
-#pragma unroll
-                    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-                }
-                column_step(cur);
-            }
-            if (part) pc = sstep64(lds, pc, la, lag16_64(lds, wp, la));
-            // Q * x^(64 + 128 d) (Q -> P and the shift to the end of the blocks), XOR over the group.
-            const uint64_t f = finish64<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds, lane);
-            reg = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
-            if (gl == 0)
-                for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
-        }
+        // crc.cpp:119-122: the register starts at ~crc and the result is inverted
+        const uint64_t reg = buffer_reg64<G>(lds, p, n, ~seed, gl, lane, la);
         if (active && gl == 0) args.out[bi] = ~reg;
     }
 }
@@ -640,38 +650,56 @@ __global__ void crc64_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_
     out[m] = acc;
 }
 
-// One long buffer split into k pieces of `piece` bytes (the last one
-// last_len): out = sum_i crc_i * x^(8 * bytes after piece i) ^ seed * x^(8n)
-// (the seed term only for seed != 0: combine's shortcut). One 1024-thread
-// block; thread t folds a contiguous run of pieces by Horner with
-// K = x^(8*piece), shifts it past the rest, then a block XOR reduction.
-__global__ __launch_bounds__(1024) void crc64_fold_pieces_kernel(const uint64_t* crcs, uint64_t k, uint64_t piece,
-                                                                 uint64_t last_len, uint64_t seed, uint64_t nbytes,
-                                                                 uint64_t kpiece, uint64_t* out, PowTable64 pt) {
-    __shared__ uint64_t red[1024];
-    const uint32_t t = threadIdx.x;
-    const uint64_t per = (k + 1023) / 1024;
-    const uint64_t lo = t * per, hi = lo + per < k ? lo + per : k;
-    uint64_t acc = 0;
-    if (lo < hi) {
-        // pieces lo..hi-1, all full-size except possibly piece k-1 (which is
-        // then the run's last): Horner over the full pieces, last one appended.
-        for (uint64_t i = lo; i < hi; ++i) {
-            const bool last = i == k - 1;
-            acc = last ? mulmod64(acc, xpow8_tab64(last_len, pt)) ^ crcs[i] : mulmod64(acc, kpiece) ^ crcs[i];
-        }
-        // acc = sum crc_i * x^(8 * bytes from the end of piece i to the end of
-        // the run); shift it past the bytes after the run.
-        if (hi < k) acc = mulmod64(acc, xpow8_tab64((k - 1 - hi) * piece + last_len, pt));
-    }
-    red[t] = acc;
-    __syncthreads();
-    for (uint32_t o = 512; o > 0; o >>= 1) {
-        if (t < o) red[t] ^= red[t + o];
-        __syncthreads();
-    }
-    if (t == 0) *out = red[0] ^ (seed ? mulmod64(seed, xpow8_tab64(nbytes, pt)) : 0ull);
-}
+// photon_crc64ecma_extend_device in one launch: crc32c_long_kernel's scheme
+// (chunks, one per wavefront, shifted to the end by X^(T-1-t), XOR-reduced by
+// workgroup atomics, the last workgroup writes) on the raw CRC-64 register:
+// chunk 0 starts from ~seed, the others from 0, the result is inverted
+// (crc.cpp:119-122).
+struct Long64Args {
+    const uint8_t* data;
+    uint64_t first, chunk, nchunks;
+    uint64_t seed;
+    uint64_t* out;
+    uint64_t* acc;      // {accumulator, ticket}: zero before the launch (grid > 1 only)
+    uint64_t xp[64];    // X^j, X = x^(8*chunk) mod P64
+    uint64_t xq[64];    // X^(64 j)
+};
 
+__global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneConsts64 kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+    __shared__ uint64_t red[kWaves];
+    build_tables64<64>(lds, kc);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = wave_id();
+    const LaneAddr64 la = lane_addr64(lane);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    uint64_t acc = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < a.nchunks; t += nwaves) {
+        const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
+        const uint64_t n = t ? a.chunk : a.first;
+        uint64_t reg = buffer_reg64<64>(lds, p, n, t ? 0ull : ~a.seed, lane, lane, la);
+        const uint64_t m = a.nchunks - 1 - t;  // wave-uniform
+        reg = mulmod64(mulmod64(reg, a.xp[m & 63u]), a.xq[(m >> 6) & 63u]);
+        acc ^= reg;
+    }
+    if (lane == 0) red[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) v ^= red[w];
+        if (gridDim.x == 1) {
+            *a.out = ~v;
+        } else {
+            atomicXor(reinterpret_cast<unsigned long long*>(a.acc), (unsigned long long)v);
+            __threadfence();
+            if (atomicAdd(reinterpret_cast<unsigned long long*>(a.acc + 1), 1ull) == gridDim.x - 1) {
+                __threadfence();
+                *a.out = ~(uint64_t)atomicExch(reinterpret_cast<unsigned long long*>(a.acc), 0ull);
+                atomicExch(reinterpret_cast<unsigned long long*>(a.acc + 1), 0ull);
+            }
+        }
+    }
+}
 
 }  // namespace pcrc

@@ -199,12 +199,13 @@ int read_span_parallel(int fd, uint8_t* dst, uint64_t want_min, uint64_t want_ma
     return 0;
 }
 
-}  // namespace
-
 // Ranges registered through photon_crc_host_register, so the message batch
-// can check that a segment [p, p+n) stays inside its registration.
+// can check that a segment [p, p+n) stays inside its registration (file-local:
+// no exported symbol a host application could collide with).
 std::mutex g_reg_mu;
 std::map<uintptr_t, uint64_t> g_reg;
+
+}  // namespace
 
 int pcrc::registered_range_check(const void* p, uint64_t n) {
     const uintptr_t q = reinterpret_cast<uintptr_t>(p);

@@ -13,7 +13,8 @@
 #                                        against the in-tree one, alternating, fresh process each
 #                                        (a run whose self-check fails -- ablation builds -- is
 #                                        recorded with "ok": false, not a failure); AB_NEW=LIB2 puts
-#                                        another build on the "new" side
+#                                        another build on the "new" side; AB_ARGS adds bench.py arguments
+#                                        (e.g. AB_ARGS="--steps 20 --warmup 5": the driver's conditions)
 # Several commands chain with "::", e.g.
 #   scripts/gpu.sh tests :: bench --steps 20 --warmup 5 :: prof c2
 set -o pipefail
@@ -61,10 +62,10 @@ run_one() {
           for side in new old; do
             local envv=""; [ $side = old ] && envv="PHOTON_CRC_LIB=$lib"
             [ $side = new ] && [ -n "$AB_NEW" ] && envv="PHOTON_CRC_LIB=$AB_NEW"
-            env $envv timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-live-pmc --no-shape64 \
+            env $envv timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-live-pmc --no-shape64 $AB_ARGS \
               > $O/ab_tmp.json 2>> $O/ab.err || [ "$(wc -l < $O/ab_tmp.json)" -gt 0 ] \
               || { echo "ab $c $side failed"; tail -5 $O/ab.err; return 1; }  # (self-check false still prints its line: ablation builds)
-            python -c "import json,sys; d=json.loads(open('$O/ab_tmp.json').read().splitlines()[-1]); r=d['roofline']; print(json.dumps({'round': $r, 'config': '$c', 'side': '$side', 'value': d['value'], 'frac_kernel': r['frac_kernel'], 'frac_steady': r['frac_steady_median_launch'], 'ok': d['self_check']}))" | tee -a $O/ab.jsonl
+            python -c "import json,sys; d=json.loads(open('$O/ab_tmp.json').read().splitlines()[-1]); r=d['roofline']; print(json.dumps({'round': $r, 'config': '$c', 'side': '$side', 'args': '$AB_ARGS', 'value': d['value'], 'frac_kernel': r['frac_kernel'], 'frac_steady': r['frac_steady_median_launch'], 'ok': d['self_check']}))" | tee -a $O/ab.jsonl
           done
         done
       done ;;

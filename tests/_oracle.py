@@ -98,6 +98,18 @@ def extend_chain(segments, seed=0):
     return c
 
 
+def checked_message_object(segments, struct_bytes):
+    """CheckedMessage<Crc32Hasher>::add_checksum / validate_checksum as the
+    reference runs them on a message OBJECT (rpc/serialize.h:244-275, 425,
+    462-463): extend_hash accumulates into m_checksum by reference, and
+    m_checksum is the struct's first 4 bytes, so the struct is hashed while
+    it holds the running CRC of the payload."""
+    acc = extend_chain(segments, 0)
+    b = bytearray(_b(struct_bytes))
+    b[:4] = acc.to_bytes(4, "little")
+    return crc32c(bytes(b), acc)
+
+
 # ---------------------------------------------------------------- batches
 # Full-size parity (tests/test_gpu_fullsize.py): the same oracle functions in
 # C loops, fanned out over a thread pool (ctypes releases the GIL). Host

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from photonlibos_amd import checksum as ck
-from photonlibos_amd.checked import MessageBatch, PinnedAlloc, TRUSTED
+from photonlibos_amd.checked import DETACHED_BODY, MessageBatch, PinnedAlloc, TRUSTED
 from photonlibos_amd.checksum import CrcError
 
 pytestmark = pytest.mark.gpu
@@ -52,7 +52,9 @@ def _expected(alloc, oracle, segs, body):
     return oracle.extend_chain(data, 0)
 
 
-@pytest.mark.parametrize("flags", [0, 2])  # zero-copy staging (default) / STAGED copies
+# These tests hash payload + a separate body buffer (DETACHED_BODY); the
+# default, the body as the message object itself, is tested below.
+@pytest.mark.parametrize("flags", [4, 6])  # zero-copy staging / STAGED copies
 def test_validate_batch_matches_oracle(torch_dev, oracle, flags):
     rng = random.Random(11)
     alloc = PinnedAlloc()
@@ -84,7 +86,7 @@ def test_validate_batch_matches_oracle(torch_dev, oracle, flags):
     assert alloc.release() == slab
 
 
-@pytest.mark.parametrize("flags", [0, 2])
+@pytest.mark.parametrize("flags", [4, 6])
 def test_payload_corruption_detected(torch_dev, oracle, flags):
     rng = random.Random(12)
     alloc = PinnedAlloc()
@@ -185,10 +187,11 @@ def _cm_fixture():
         return json.load(f)["messages"]
 
 
-@pytest.mark.parametrize("flags", [0, 2])
+@pytest.mark.parametrize("flags", [4, 6])
 def test_batch_matches_reference_checked_message(torch_dev, flags):
     """The device batch against the REFERENCE's own CheckedMessage template
-    (serialize.h:239-279 run by oracle/ref/checked_message_fixtures.cpp):
+    (serialize.h:239-279 run by oracle/ref/checked_message_fixtures.cpp, whose
+    body is a buffer separate from the CheckedMessage object: DETACHED_BODY):
     every checksum add_checksum stored, every validate_checksum verdict."""
     from photonlibos_amd import datagen
     msgs = _cm_fixture()
@@ -220,5 +223,181 @@ def test_batch_matches_reference_checked_message(torch_dev, flags):
             assert valid == (m["validate"] if claim == "right" else m["validate_bad_claim"]), (k, claim)
         assert nbad == (0 if claim == "right" else len(msgs))
         batch.close()
+    for a in blocks:
+        alloc.dealloc(a)
+
+
+def test_resubmit_while_done_callback_runs_is_busy(torch_dev, oracle):
+    """done_ev fires before the `done` host function runs. While a
+    slow callback is still running (and may read the verdicts), a resubmit or
+    reset from another thread is -EBUSY instead of overwriting them; result()
+    inside the callback sees the settled batch; once the callback has
+    returned, the batch resubmits."""
+    import threading
+    import time
+    torch = torch_dev
+    d = torch.randint(0, 256, (8192,), dtype=torch.uint8, device="cuda")
+    want = oracle.crc32c(d.cpu().numpy())
+    b = MessageBatch(1, 1)
+    b.add([(d.data_ptr(), 8192)], None, want)
+    entered, seen = threading.Event(), []
+
+    def slow_done():
+        seen.append(b.result(0))  # settled before the callback: no HIP call needed
+        entered.set()
+        time.sleep(0.5)
+
+    b.submit(done=slow_done)
+    assert entered.wait(30)
+    with pytest.raises(CrcError) as e:
+        b.submit()
+    assert e.value.code == -16  # EBUSY: the callback has not returned
+    with pytest.raises(CrcError) as e:
+        b.reset()
+    assert e.value.code == -16
+    assert seen == [(True, want)]
+    deadline = time.time() + 30
+    while True:  # the callback returns after its sleep
+        try:
+            b.submit()
+            break
+        except CrcError as err:
+            assert err.code == -16 and time.time() < deadline
+            time.sleep(0.05)
+    assert b.wait() == 0 and b.result(0) == (True, want)
+    b.close()
+
+
+def test_segment_past_its_pinned_block_is_refused(torch_dev):
+    """a segment in pinned-pool memory must stay inside its own
+    live IOAlloc block (not merely inside the 64 MiB slab)."""
+    alloc = PinnedAlloc()
+    a = alloc.alloc(4096)        # a 4 KiB-class block
+    nb = alloc.alloc(4096)       # a neighbour, possibly the next block
+    try:
+        b = MessageBatch(4, 4)
+        b.add([(a, 4096)])                  # the whole block: fine
+        b.add([(a + 100, 3996)])            # ends exactly at the block end: fine
+        with pytest.raises(CrcError) as e:
+            b.add([(a + 16, 4096)])         # 16 bytes past the end of its block
+        assert e.value.code == -14
+        freed, nb = nb, None
+        alloc.dealloc(freed)
+        with pytest.raises(CrcError) as e:  # a freed block is not the caller's memory any more
+            b.add([(freed, 64)])
+        assert e.value.code == -14
+        b.close()
+    finally:
+        alloc.dealloc(a)
+        if nb:
+            alloc.dealloc(nb)
+
+
+def test_ioalloc_binding_against_reference_headers(torch_dev):
+    """INTEGRATION.md §2.1 compiled verbatim against the
+    reference's io-alloc.h / iovector.h / serialize.h (oracle/ref/
+    ioalloc_binding.cpp, built in the build container into oracle/_ref/).
+    On this box it builds 200 received requests with reference
+    IOVector::push_back(size) allocating from photon_crc_pinned_allocate
+    (rpc/rpc.cpp:216-220, 279), runs the reference CheckedMessage
+    add_checksum / validate_checksum over the drop-in, then the §2.1 receive
+    path hands every message to the GPU batch. Checked: the reference's
+    checksums equal the committed fixture (tests/golden/ioalloc_binding.json,
+    made over Photon's own crc.cpp), the batch reproduces every checksum, its
+    verdicts flag exactly the corrupted claims, and every pinned block went
+    back to the pool."""
+    import json
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "oracle", "_ref", "ioalloc_dropin")
+    assert os.path.exists(exe), "oracle/_ref/ioalloc_dropin not built (make -C oracle/ref in the build container)"
+    r = subprocess.run([exe, "pinned", "200"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    with open(os.path.join(repo, "tests", "golden", "ioalloc_binding.json")) as f:
+        gold = json.load(f)["messages"]
+    assert got["pinned_in_use_bytes"] > 0 and got["pinned_in_use_after"] == 0
+    assert len(got["messages"]) == len(gold) == 200
+    for m, (g, w) in enumerate(zip(got["messages"], gold)):
+        assert (g["lens"], g["seeds"], g["checksum"], g["validate"]) == \
+            (w["lens"], w["seeds"], w["checksum"], w["validate"]), m
+        assert g["batch_crc"] == w["checksum"], m
+        assert g["batch_valid"] == (0 if m % 7 == 3 else 1), m
+
+
+
+def _object_messages(alloc, rng, nmsg):
+    """Photon's layout: payload segments, then the message struct whose first
+    4 bytes are m_checksum (the CheckedMessage<> base), 48 bytes."""
+    msgs, blocks = [], []
+    for _ in range(nmsg):
+        segs = []
+        for _ in range(rng.randrange(0, 6)):
+            ln = rng.randrange(1, 9000)
+            a = alloc.alloc(ln)
+            blocks.append(a)
+            alloc.view(a, ln)[:] = np.frombuffer(rng.randbytes(ln), np.uint8)
+            segs.append((a, ln))
+        t = alloc.alloc(48)
+        blocks.append(t)
+        alloc.view(t, 48)[:] = np.frombuffer(rng.randbytes(48), np.uint8)
+        msgs.append((segs, (t, 48)))
+    return msgs, blocks
+
+
+def _photon_checksum(alloc, oracle, segs, body):
+    """The reference's value for a message object (oracle.checked_message_object:
+    the in-place accumulation of serialize.h:244-275, 462-463)."""
+    return oracle.checked_message_object([bytes(alloc.view(a, n)) for a, n in segs], bytes(alloc.view(*body)))
+
+
+@pytest.mark.parametrize("flags", [0, 2])
+def test_message_object_body_matches_reference_semantics(torch_dev, oracle, flags):
+    """Default batches: the body is the message object (t->validate_checksum(
+    iov, t, sizeof(*t)), serialize.h:462-463). The batch equals the
+    reference's in-place accumulation computed step by step, which equals
+    crc32c of the struct with m_checksum zeroed: a corrupted payload is NOT
+    detected (as in Photon), a corrupted struct field is; DETACHED_BODY over
+    the same messages covers the payload."""
+    rng = random.Random(21)
+    alloc = PinnedAlloc()
+    msgs, blocks = _object_messages(alloc, rng, 120)
+    want = [_photon_checksum(alloc, oracle, s, body) for s, body in msgs]
+    for (s, (t, n)), w in zip(msgs, want):
+        z = bytearray(alloc.view(t, n))
+        z[:4] = b"\0\0\0\0"
+        assert w == oracle.crc32c(bytes(z))  # the identity the batch relies on
+    # corrupt one payload byte of every 3rd message that has a payload, one
+    # struct byte (past m_checksum) of every 5th
+    pay_bad, body_bad = set(), set()
+    for i, (segs, (t, n)) in enumerate(msgs):
+        if i % 3 == 0 and segs:
+            a, ln = segs[0]
+            alloc.view(a, ln)[rng.randrange(ln)] ^= 0x40
+            pay_bad.add(i)
+        if i % 5 == 0:
+            alloc.view(t, n)[4 + rng.randrange(44)] ^= 0x01
+            body_bad.add(i)
+    b = MessageBatch(len(msgs), 4096, flags)
+    for i, (segs, body) in enumerate(msgs):
+        alloc.view(body[0], 4)[:] = np.frombuffer(rng.randbytes(4), np.uint8)  # m_checksum holds the claim
+        assert b.add(segs, body, want[i]) == i
+        assert not alloc.view(body[0], 4).any()  # validate_checksum's m_checksum = 0
+    b.submit()
+    assert b.wait() == len(body_bad)
+    for i in range(len(msgs)):
+        assert b.result(i)[0] == (i not in body_bad), i
+    b.close()
+    # the same messages, payload hashed (DETACHED_BODY: payload then struct)
+    d = MessageBatch(len(msgs), 4096, flags | DETACHED_BODY)
+    for i, (segs, body) in enumerate(msgs):
+        d.add(segs, body, want[i])
+    d.submit()
+    d.wait()
+    for i, (segs, body) in enumerate(msgs):
+        data = [bytes(alloc.view(a, n)) for a, n in segs] + [bytes(alloc.view(*body))]
+        assert d.result(i)[1] == oracle.extend_chain(data, 0), i
+    d.close()
     for a in blocks:
         alloc.dealloc(a)

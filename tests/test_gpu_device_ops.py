@@ -270,3 +270,29 @@ def test_extend_device_over_4gib(torch_dev):
     assert int(u32(one)[0]) == int(u32(folded)[0])
     del dbuf
     torch.cuda.empty_cache()
+
+
+def test_scratch_release_frees_idle_buffers(torch_dev, oracle):
+    """the library's device scratch is not kept forever. A
+    two-kernel message batch without caller-provided segment CRCs leases
+    scratch; photon_crc_scratch_release() frees it once idle, and the next
+    call allocates afresh with the same results."""
+    torch = torch_dev
+    n, nmsg = 4096, 4
+    d = torch.empty(n * nmsg * 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, n, n, nmsg * 64, 0x5EED0A00)
+    iov = np.array([[d.data_ptr() + k * n, n] for k in range(nmsg * 64)], np.uint64)
+    start = np.arange(0, nmsg * 64 + 1, 64, dtype=np.uint64)
+    d_iov = torch.from_numpy(iov.view(np.int64).copy()).cuda()
+    d_start = torch.from_numpy(start.view(np.int64).copy()).cuda()
+    host = d.cpu().numpy()
+    want = [oracle.crc32c(host[m * 64 * n:(m + 1) * 64 * n]) for m in range(nmsg)]
+    for rep in range(2):
+        ck.set_msg_mode(2)
+        out = torch.zeros(nmsg, dtype=torch.int32, device="cuda")
+        ck.batch_msg_n(d_iov, d_start, nmsg, nmsg * 64, None, out)
+        torch.cuda.synchronize()
+        ck.set_msg_mode(0)
+        assert list(u32(out)) == want, rep
+        assert ck.scratch_release() > 0, rep
+    assert ck.scratch_release() == 0

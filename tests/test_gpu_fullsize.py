@@ -155,3 +155,84 @@ def test_full_c4_shard_every_crc(torch_dev, oracle):
         want = oracle.crc32c_strided(host, nbytes, nbytes, per)
         assert _first_mismatch(a[lo:lo + per], want) is None, (lo, _first_mismatch(a[lo:lo + per], want))
     del d
+
+
+# ------------------------------------------------- one long buffer (row f3)
+# photon_crc32c_extend_device / photon_crc64ecma_extend_device: one launch,
+# chunks of the buffer one per wavefront, XOR-combined by workgroup atomics.
+# The reference's own perf shape (test_checksum.cpp:125-168: one 128 KiB and
+# one 1 GiB buffer at buf+1) and every edge of the chunk plan.
+
+def _extend(torch, d, off, n, seed, crc64=False):
+    if crc64:
+        out = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ck.extend64_device(d.data_ptr() + off, n, out, seed=seed)
+        torch.cuda.synchronize()
+        return int(out.cpu().numpy().view(np.uint64)[0])
+    out = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.extend_device(d.data_ptr() + off, n, seed, out)
+    torch.cuda.synchronize()
+    return int(_u32(out)[0])
+
+
+@pytest.mark.parametrize("n", [128 << 10, 1 << 30])
+def test_extend_device_reference_perf_shape(torch_dev, oracle, n):
+    torch = torch_dev
+    d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, n + 64, n + 64, 1, 0x5EED0600)
+    host = d.cpu().numpy()[1:1 + n]
+    for seed in (0, 0xFFFFFFFF):
+        assert _extend(torch, d, 1, n, seed) == oracle.crc32c(host, seed), (n, seed)
+    if n <= (128 << 10):
+        assert _extend(torch, d, 1, n, 7, True) == oracle.crc64ecma(host, 7)
+    del d
+
+
+def test_extend_device_plan_edges(torch_dev, oracle):
+    # Chunk-plan edges: one chunk, the one-workgroup limit (256 KiB, 16
+    # chunks) and one byte past it, T at multiples of 16 waves +- 1, the
+    # 16-KiB-chunk limit of a full grid (64 MiB) +- a few bytes, odd sizes;
+    # offsets 0, 1, 15; seeds; CRC-32C and CRC-64. Each call also leaves its
+    # accumulator state zeroed for the next one (repeated calls agree).
+    torch = torch_dev
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    big = 16 * cus * (16 << 10)
+    sizes = [0, 1, 15, 64, 4095, 4096, 4097, 65536 + 3, (256 << 10) - 1, 256 << 10, (256 << 10) + 1,
+             (256 << 10) + 16385, 17 * (16 << 10), 33 * (16 << 10) + 5, big - 1, big, big + 7, 3 * big + 12345]
+    d = torch.empty(max(sizes) + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0700)
+    host = d.cpu().numpy()
+    for k, n in enumerate(sizes):
+        off = (0, 1, 15)[k % 3]
+        seed = (k * 0x9E3779B1) & 0xFFFFFFFF
+        want = oracle.crc32c(host[off:off + n], seed)
+        assert _extend(torch, d, off, n, seed) == want, (n, off)
+        assert _extend(torch, d, off, n, seed) == want, ("repeat", n, off)
+        if n <= (1 << 20):
+            s64 = seed * 0x100000001
+            assert _extend(torch, d, off, n, s64, True) == oracle.crc64ecma(host[off:off + n], s64), (n, off)
+    n = big + 7  # CRC-64 on a full grid of chunks
+    assert _extend(torch, d, 3, n, 5, True) == oracle.crc64ecma(host[3:3 + n], 5)
+    del d
+
+
+def test_extend_device_concurrent_streams(torch_dev, oracle):
+    # Eight streams each run long-buffer calls at once: every call leases its
+    # own accumulator (scratch_alloc(zeroed)), results stay exact.
+    torch = torch_dev
+    n = (40 << 20) + 11
+    d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, n + 64, n + 64, 1, 0x5EED0800)
+    host = d.cpu().numpy()
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    outs = [torch.zeros(4, dtype=torch.int32, device="cuda") for _ in streams]
+    torch.cuda.synchronize()
+    for r in range(4):
+        for k, (s, o) in enumerate(zip(streams, outs)):
+            ck.extend_device(d.data_ptr() + k, n - 8 * k, r + k, o[r:r + 1], stream=s)
+    torch.cuda.synchronize()
+    for k, o in enumerate(outs):
+        got = _u32(o)
+        for r in range(4):
+            assert int(got[r]) == oracle.crc32c(host[k:k + n - 8 * k], r + k), (k, r)
+    del d

@@ -177,3 +177,23 @@ def test_batch_drivers_match_single_calls(oracle):
     assert oracle.msg_chain(iov, start, None, 7).tolist() == [
         oracle.extend_chain([host[offs[k]:offs[k] + lens[k]] for k in range(int(start[m]), int(start[m + 1]))], 7)
         for m in range(6)]
+
+
+def test_ioalloc_binding_fixture(oracle):
+    # tests/golden/ioalloc_binding.json: the reference's CheckedMessage over
+    # IOAlloc-allocated IOVectors with the message struct hashed as itself
+    # (Photon's own crc.cpp). It equals the oracle's restatement of the
+    # in-place accumulation (m_checksum = running CRC while the struct is
+    # hashed), and that equals crc32c of the struct with m_checksum zeroed:
+    # the payload does not enter Photon's RPC checksum.
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ioalloc_binding.json")) as f:
+        msgs = json.load(f)["messages"]
+    for m, g in enumerate(msgs):
+        parts = [datagen.stream_bytes(s, n) for s, n in zip(g["seeds"], g["lens"])]
+        body = np.concatenate([np.zeros(4, np.uint8), datagen.stream_bytes(0x5EEDAB00 + m, 44)])
+        assert oracle.checked_message_object(parts, body) == g["checksum"], m
+        assert oracle.crc32c(body) == g["checksum"], m
+        if any(g["lens"]):  # the payload-covering chain is a different value
+            assert oracle.extend_chain(parts + [body], 0) != g["checksum"], m
