@@ -781,7 +781,8 @@ def main(argv=None):
             traffic, traffic_src = lt["bytes"], f"live rocprofv3 --pmc FETCH_SIZE x1024x2, {lt['launches']} launches"
     if traffic is None:
         traffic = load_traffic(args.traffic_json, args.config)
-        traffic_src = f"profiles/pmc_{args.config}.json (committed PMC pass)" if traffic else None
+        traffic_src = (f"committed, not this run: profiles/pmc_{args.config}.json (an earlier rocprofv3 --pmc "
+                       "FETCH_SIZE pass of this config on one GPU)") if traffic else None
 
     if rank == 0:
         steady = wl.bytes_per_step / (float(np.median([r["launch_ms"]["median"] for r in ranks])) * 1e-3) / 1e9

@@ -57,6 +57,11 @@ int photon_crc_set_msg_mode(int mode);
 /* Rows per step of the one-kernel message form (tuning): 2 (default) or 4. */
 int photon_crc_set_msg_rows(int rows_per_step);
 
+/* One long buffer (photon_crc32c_extend_device / photon_crc64ecma_extend_device,
+ * buffers over 256 KiB): lanes per chunk (0 = automatic = 64, or 32) and
+ * chunks per lane group of the full grid (0 = automatic = 1). */
+int photon_crc_set_long_shape(int lanes, int rounds);
+
 /* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
  * each lane reads two consecutive 16-byte blocks per row, one row shift per
  * 32 bytes (lanes per buffer <= 32; overrides the interleave). */

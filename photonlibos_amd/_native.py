@@ -66,6 +66,7 @@ def _declare(L):
     fn("photon_crc_set_stream_config", ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int)
     fn("photon_crc64_set_stream_config", ctypes.c_int, ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_generic_rows", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc_set_long_shape", ctypes.c_int, ctypes.c_int, ctypes.c_int)
     fn("photon_crc64_set_interleave", ctypes.c_int, ctypes.c_int)
     fn("photon_crc64_set_run_blocks", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_msg_mode", ctypes.c_int, ctypes.c_int)

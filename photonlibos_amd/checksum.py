@@ -486,6 +486,12 @@ def set_msg_mode(mode):
     _check(lib().photon_crc_set_msg_mode(mode))
 
 
+def set_long_shape(lanes=0, rounds=0):
+    """One long buffer (extend_device / extend64_device): lanes per chunk (0 =
+    automatic, 32, 64) and chunks per lane group of the grid (0 = automatic)."""
+    _check(lib().photon_crc_set_long_shape(lanes, rounds))
+
+
 def set_msg_rows(u):
     """Rows per step of the one-kernel message form (2 or 4; tuning)."""
     _check(lib().photon_crc_set_msg_rows(u))

@@ -116,19 +116,13 @@ const void* device_address(const void* p, uint64_t n, bool* host) {
         } else {
             (void)hipGetLastError();
         }
-    } else {
-        // Host memory: against its photon_crc_host_register registration, else
-        // against its hipHostMalloc allocation when HIP reports the range.
-        const int reg = registered_range_check(p, n);
-        if (reg == 0) return nullptr;
-        void* lo = nullptr;
-        size_t size = 0;
-        if (reg < 0 && hipMemGetAddressRange(&lo, &size, const_cast<void*>(p)) == hipSuccess && size) {
-            const uintptr_t q = reinterpret_cast<uintptr_t>(p), b0 = reinterpret_cast<uintptr_t>(lo);
-            if (q < b0 || n > size || q - b0 > size - n) return nullptr;
-        } else if (reg < 0) {
-            (void)hipGetLastError();
-        }
+    } else if (registered_range_check(p, n) == 0) {
+        // Host memory registered through photon_crc_host_register or a vDMA
+        // target's register_memory: against its registration. (hipHostMalloc
+        // memory from other code keeps the start-pointer check: HIP does not
+        // report the range of registered host memory reliably --
+        // hipMemGetAddressRange refused in-range vDMA registrations.)
+        return nullptr;
     }
     if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) {
         *host = false;

@@ -695,36 +695,45 @@ int pipe_init(HostPipe& p) {
 }
 
 // One long buffer (photon_crc32c_extend_device, photon_crc64ecma_extend_device):
-// T chunks (the first one shorter), one per wavefront of the long kernels.
-// Up to 256 KiB: at most 16 chunks of >= 4 KiB, one workgroup, the result
-// written directly (latency). Above: chunks of >= 16 KiB (4 KiB multiples),
-// as many as the grid has waves (16 per CU; VERDICT r2: the piece batch used
-// to fill half, or an eighth, of the chip), T <= 4096 (the two 64-entry power
-// tables of the kernels).
+// T chunks (the first one shorter), one per lane group of the long kernels.
+// Up to 256 KiB: at most 16 chunks of >= 4 KiB in one workgroup of 64-lane
+// groups, the result written directly (latency). Above: chunks of >= 16 KiB
+// (4 KiB multiples), `rounds` chunks per lane group of a full grid (16 waves
+// per CU; VERDICT r2: the piece batch used to fill half, or an eighth, of the
+// chip). Lane groups and rounds: tuning.h photon_crc_set_long_shape.
+std::atomic<uint32_t> g_long_shape{0};  // lanes | rounds << 8; 0 = automatic
+
 struct LongPlan {
     uint64_t chunk, first, nchunks, grid;
+    int lanes;
 };
 
 LongPlan long_plan(uint64_t n, int cus) {
+    const uint32_t shape = g_long_shape.load(std::memory_order_relaxed);
     const bool small = n <= (256u << 10);
-    uint64_t waves = small ? 16 : 16ull * (uint64_t)cus;
-    if (waves > 4096) waves = 4096;
-    uint64_t chunk = ((n + waves - 1) / waves + 4095) & ~4095ull;
+    const int lanes = small || !(shape & 0xff) ? 64 : (int)(shape & 0xff);
+    const uint64_t rounds = small || !(shape >> 8) ? 1 : shape >> 8;
+    const uint64_t slots = small ? 16 : 16ull * (uint64_t)cus * (64 / (uint64_t)lanes) * rounds;
+    uint64_t chunk = ((n + slots - 1) / slots + 4095) & ~4095ull;
     const uint64_t lo = small ? 4096 : 16384;
     if (chunk < lo) chunk = lo;
+    while ((n + chunk - 1) / chunk > (1u << 18)) chunk <<= 1;  // the kernels' three 64-entry power tables
     LongPlan p;
+    p.lanes = lanes;
     p.chunk = chunk;
     p.nchunks = n ? (n + chunk - 1) / chunk : 1;
     p.first = n - (p.nchunks - 1) * chunk;
-    p.grid = (p.nchunks + kWaves - 1) / kWaves;
+    const uint64_t waves = (p.nchunks * (uint64_t)lanes + 63) / 64;
+    p.grid = (waves + kWaves - 1) / kWaves;
+    if (p.grid > (uint64_t)cus) p.grid = cus;
     return p;
 }
 
-// X^j and X^(64 j), j < 64, X = x^(8 * chunk) (CRC-32C or CRC-64/ECMA),
+// X^j, X^(64 j), X^(4096 j), j < 64, X = x^(8 * chunk) (CRC-32C or CRC-64/ECMA),
 // computed on first use per chunk size and kept (callers repeat sizes).
 struct LongPowers {
-    uint32_t p32[64], q32[64];
-    uint64_t p64[64], q64[64];
+    uint32_t p32[3][64];
+    uint64_t p64[3][64];
 };
 
 const LongPowers& long_powers(uint64_t chunk, bool crc64) {
@@ -737,19 +746,16 @@ const LongPowers& long_powers(uint64_t chunk, bool crc64) {
             if (e.first == chunk) return *e.second;
     }
     LongPowers* t = new LongPowers();
-    if (crc64) {
-        const uint64_t y = xpow64(8 * chunk), y64 = xpow64(512 * chunk);
-        t->p64[0] = t->q64[0] = kOne64;
-        for (int j = 1; j < 64; ++j) {
-            t->p64[j] = mulmod64(t->p64[j - 1], y);
-            t->q64[j] = mulmod64(t->q64[j - 1], y64);
-        }
-    } else {
-        const uint32_t x = xpow(8 * chunk), x64 = xpow(512 * chunk);
-        t->p32[0] = t->q32[0] = kOne;
-        for (int j = 1; j < 64; ++j) {
-            t->p32[j] = mulmod(t->p32[j - 1], x);
-            t->q32[j] = mulmod(t->q32[j - 1], x64);
+    for (int lvl = 0; lvl < 3; ++lvl) {
+        const uint64_t bits = (8 * chunk) << (6 * lvl);  // X^(64^lvl)
+        if (crc64) {
+            const uint64_t y = xpow64(bits);
+            t->p64[lvl][0] = kOne64;
+            for (int j = 1; j < 64; ++j) t->p64[lvl][j] = mulmod64(t->p64[lvl][j - 1], y);
+        } else {
+            const uint32_t x = xpow(bits);
+            t->p32[lvl][0] = kOne;
+            for (int j = 1; j < 64; ++j) t->p32[lvl][j] = mulmod(t->p32[lvl][j - 1], x);
         }
     }
     std::lock_guard<std::mutex> lk(mu);
@@ -855,6 +861,13 @@ int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in
 int photon_crc_set_msg_mode(int mode) {
     if (mode < 0 || mode > 2) return fail(-EINVAL, "message mode must be 0 (auto), 1 (fused) or 2 (two kernels)");
     g_msg_mode.store(mode, std::memory_order_relaxed);
+    return 0;
+}
+
+int photon_crc_set_long_shape(int lanes, int rounds) {
+    if ((lanes != 0 && lanes != 32 && lanes != 64) || rounds < 0 || rounds > 64)
+        return fail(-EINVAL, "long-buffer lanes must be 0, 32 or 64 and rounds 0..64");
+    g_long_shape.store((uint32_t)lanes | (uint32_t)rounds << 8, std::memory_order_relaxed);
     return 0;
 }
 
@@ -1304,14 +1317,18 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     a.nchunks = lp.nchunks;
     a.seed = seed;
     a.out = d_out;
-    memcpy(a.xp, pw.p64, sizeof(a.xp));
-    memcpy(a.xq, pw.q64, sizeof(a.xq));
+    memcpy(a.xp, pw.p64[0], sizeof(a.xp));
+    memcpy(a.xq, pw.p64[1], sizeof(a.xq));
+    memcpy(a.xr, pw.p64[2], sizeof(a.xr));
     void* state = nullptr;  // {accumulator, ticket}, left zeroed by the kernel
     if (lp.grid > 1) {
         if (int rc = scratch_alloc(&state, 16, st, true)) return rc;
         a.acc = static_cast<uint64_t*>(state);
     }
-    hipLaunchKernelGGL(crc64_long_kernel, dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(64));
+    if (lp.lanes == 32)
+        hipLaunchKernelGGL((crc64_long_kernel<32>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(32));
+    else
+        hipLaunchKernelGGL((crc64_long_kernel<64>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(64));
     const hipError_t e = hipGetLastError();
     int rc = e == hipSuccess ? 0 : hip_fail(e, "crc64_long_kernel launch");
     if (state) {
@@ -1404,14 +1421,18 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     a.nchunks = lp.nchunks;
     a.seed = seed;
     a.out = d_out;
-    memcpy(a.xp, pw.p32, sizeof(a.xp));
-    memcpy(a.xq, pw.q32, sizeof(a.xq));
+    memcpy(a.xp, pw.p32[0], sizeof(a.xp));
+    memcpy(a.xq, pw.p32[1], sizeof(a.xq));
+    memcpy(a.xr, pw.p32[2], sizeof(a.xr));
     void* state = nullptr;  // {accumulator, ticket}, left zeroed by the kernel
     if (lp.grid > 1) {
         if (int rc = scratch_alloc(&state, 8, st, true)) return rc;
         a.acc = static_cast<uint32_t*>(state);
     }
-    hipLaunchKernelGGL((crc32c_long_kernel<4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(64));
+    if (lp.lanes == 32)
+        hipLaunchKernelGGL((crc32c_long_kernel<32, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(32));
+    else
+        hipLaunchKernelGGL((crc32c_long_kernel<64, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(64));
     const hipError_t e = hipGetLastError();
     int rc = e == hipSuccess ? 0 : hip_fail(e, "crc32c_long_kernel launch");
     if (state) {

@@ -1359,26 +1359,40 @@ struct LongArgs {
     uint32_t* acc;      // {accumulator, ticket}: zero before the launch (grid > 1 only)
     uint32_t xp[64];    // X^j
     uint32_t xq[64];    // X^(64 j)
+    uint32_t xr[64];    // X^(4096 j)
 };
 
-template <int U>
+// X^m for m < 2^18 from the three power tables (wave-uniform m: scalar reads).
+template <typename A>
+__device__ __forceinline__ uint32_t long_shift(uint32_t crc, uint64_t m, const A& a) {
+    crc = mulmod(crc, a.xp[m & 63u]);
+    if (m >= 64) crc = mulmod(crc, a.xq[(m >> 6) & 63u]);
+    if (m >= 4096) crc = mulmod(crc, a.xr[(m >> 12) & 63u]);
+    return crc;
+}
+
+// G lanes per chunk (64: one wavefront; 32: two chunks per wavefront).
+template <int G, int U>
 __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneConsts kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<64>() / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
     __shared__ uint32_t red[kWaves];
-    build_tables<64>(lds, kc);
+    build_tables<G>(lds, kc);
+    constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
+    const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr la = lane_addr(lane);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     uint32_t acc = 0;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < a.nchunks; t += nwaves) {
+    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
+        const uint64_t t = wv * GPW + grp;
+        const bool active = t < a.nchunks;
         const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
-        const uint64_t n = t ? a.chunk : a.first;
-        uint32_t crc = buffer_crc<64, U>(lds, p, n, t ? 0u : a.seed, lane, la);
-        const uint64_t m = a.nchunks - 1 - t;  // wave-uniform
-        crc = mulmod(mulmod(crc, a.xp[m & 63u]), a.xq[(m >> 6) & 63u]);
-        acc ^= crc;
+        const uint64_t n = !active ? 0 : t ? a.chunk : a.first;
+        uint32_t crc = buffer_crc<G, U>(lds, p, n, t ? 0u : a.seed, gl, la);
+        if (active) acc ^= long_shift(crc, a.nchunks - 1 - t, a);
     }
+    acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their chunks' values
     if (lane == 0) red[wave] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {

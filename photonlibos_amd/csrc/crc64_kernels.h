@@ -663,25 +663,34 @@ struct Long64Args {
     uint64_t* acc;      // {accumulator, ticket}: zero before the launch (grid > 1 only)
     uint64_t xp[64];    // X^j, X = x^(8*chunk) mod P64
     uint64_t xq[64];    // X^(64 j)
+    uint64_t xr[64];    // X^(4096 j)
 };
 
+template <int G>
 __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneConsts64 kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
     __shared__ uint64_t red[kWaves];
-    build_tables64<64>(lds, kc);
+    build_tables64<G>(lds, kc);
+    constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
+    const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr64 la = lane_addr64(lane);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     uint64_t acc = 0;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWaves + wave; t < a.nchunks; t += nwaves) {
+    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
+        const uint64_t t = wv * GPW + grp;
+        const bool active = t < a.nchunks;
         const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
-        const uint64_t n = t ? a.chunk : a.first;
-        uint64_t reg = buffer_reg64<64>(lds, p, n, t ? 0ull : ~a.seed, lane, lane, la);
-        const uint64_t m = a.nchunks - 1 - t;  // wave-uniform
-        reg = mulmod64(mulmod64(reg, a.xp[m & 63u]), a.xq[(m >> 6) & 63u]);
-        acc ^= reg;
+        const uint64_t n = !active ? 0 : t ? a.chunk : a.first;
+        uint64_t reg = buffer_reg64<G>(lds, p, n, t ? 0ull : ~a.seed, gl, lane, la);  // valid on gl == 0
+        const uint64_t m = a.nchunks - 1 - t;
+        reg = mulmod64(reg, a.xp[m & 63u]);
+        if (m >= 64) reg = mulmod64(reg, a.xq[(m >> 6) & 63u]);
+        if (m >= 4096) reg = mulmod64(reg, a.xr[(m >> 12) & 63u]);
+        if (active && gl == 0) acc ^= reg;
     }
+    acc = ((uint64_t)group_xor<64>((uint32_t)(acc >> 32)) << 32) | group_xor<64>((uint32_t)acc);
     if (lane == 0) red[wave] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -207,6 +207,16 @@ std::map<uintptr_t, uint64_t> g_reg;
 
 }  // namespace
 
+void pcrc::record_registration(const void* p, uint64_t n) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[reinterpret_cast<uintptr_t>(p)] = n;
+}
+
+void pcrc::forget_registration(const void* p) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg.erase(reinterpret_cast<uintptr_t>(p));
+}
+
 int pcrc::registered_range_check(const void* p, uint64_t n) {
     const uintptr_t q = reinterpret_cast<uintptr_t>(p);
     std::lock_guard<std::mutex> lk(g_reg_mu);

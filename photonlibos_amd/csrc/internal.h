@@ -21,4 +21,8 @@ int batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, 
 // 1 inside one registration, 0 p is registered but the range runs past it,
 // -1 p is in no registration made through this library.
 int registered_range_check(const void* p, uint64_t n);
+// Record / forget a host range registered with hipHostRegister by another part
+// of the library (the vDMA target's register_memory), for the check above.
+void record_registration(const void* p, uint64_t n);
+void forget_registration(const void* p);
 }  // namespace pcrc

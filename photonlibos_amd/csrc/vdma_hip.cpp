@@ -198,6 +198,7 @@ public:
                 errno = EIO;
                 return nullptr;
             }
+            pcrc::record_registration(buf, size);  // so batches check segments against it
         }
         std::lock_guard<std::mutex> lk(mu_);
         auto hb = std::unique_ptr<HipBuffer>(new HipBuffer(static_cast<char*>(buf), size, !device_mem, this));
@@ -215,6 +216,7 @@ public:
         }
         if (it->second->host_pinned()) {
             DeviceScope scope(dev_);
+            pcrc::forget_registration(it->second->address());
             (void)hipHostUnregister(it->second->address());
         }
         registered_.erase(it);

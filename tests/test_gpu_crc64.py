@@ -95,16 +95,19 @@ def test_strided(torch_dev, oracle, g):
             assert int(got[i]) == oracle.crc64ecma(datagen.stream_bytes(0x640 + nbytes + i, nbytes), 0x1234), i
 
 
-@pytest.mark.parametrize("v", [1, 2, 4, "b2"])
-@pytest.mark.parametrize("shape", [(4, 2), (4, 3), (2, 4), (8, 1), (4, 1), (2, 2), (2, 3), None])
+# (shape, v) cases: every streaming shape with every row interleave and with
+# runs of two blocks ("b2"); None = the generic kernel, which has neither.
+STREAM64_CASES = [(shape, v) for shape in [(4, 2), (4, 3), (2, 4), (8, 1), (4, 1), (2, 2), (2, 3)]
+                  for v in [1, 2, 4, "b2"]] + [(None, 1)]
+
+
+@pytest.mark.parametrize("shape,v", STREAM64_CASES)
 @pytest.mark.parametrize("g", [8, 32, 64])
 def test_streaming_shapes(torch_dev, oracle, shape, g, v):
     # The CRC-64 streaming kernel (uniform batches) in every shape and row
     # interleave, with seed0, per-buffer seeds and no seed; counts that do not
     # fill whole wave tuples. v = "b2": runs of two blocks per lane.
     if shape is None:
-        if v != 1:
-            pytest.skip("generic kernel has no interleave")
         ck.set_stream64_config(0, 0)  # generic kernel only
     else:
         ck.set_stream64_config(*shape)
