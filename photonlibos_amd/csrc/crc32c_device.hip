@@ -1320,9 +1320,9 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     memcpy(a.xp, pw.p64[0], sizeof(a.xp));
     memcpy(a.xq, pw.p64[1], sizeof(a.xq));
     memcpy(a.xr, pw.p64[2], sizeof(a.xr));
-    void* state = nullptr;  // {accumulator, ticket}, left zeroed by the kernel
+    void* state = nullptr;  // long_reduce's 18 words, left zeroed by the kernel
     if (lp.grid > 1) {
-        if (int rc = scratch_alloc(&state, 16, st, true)) return rc;
+        if (int rc = scratch_alloc(&state, 18 * 8, st, true)) return rc;
         a.acc = static_cast<uint64_t*>(state);
     }
     if (lp.lanes == 32)
@@ -1424,9 +1424,9 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     memcpy(a.xp, pw.p32[0], sizeof(a.xp));
     memcpy(a.xq, pw.p32[1], sizeof(a.xq));
     memcpy(a.xr, pw.p32[2], sizeof(a.xr));
-    void* state = nullptr;  // {accumulator, ticket}, left zeroed by the kernel
+    void* state = nullptr;  // long_reduce's 18 words, left zeroed by the kernel
     if (lp.grid > 1) {
-        if (int rc = scratch_alloc(&state, 8, st, true)) return rc;
+        if (int rc = scratch_alloc(&state, 18 * 4, st, true)) return rc;
         a.acc = static_cast<uint32_t*>(state);
     }
     if (lp.lanes == 32)

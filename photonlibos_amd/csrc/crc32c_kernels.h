@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/photon_crc/crc32c_gpu.h"
 #include "gf2.h"
 
@@ -1356,11 +1358,44 @@ struct LongArgs {
     uint64_t nchunks;   // T
     uint32_t seed;
     uint32_t* out;
-    uint32_t* acc;      // {accumulator, ticket}: zero before the launch (grid > 1 only)
+    uint32_t* acc;      // long_reduce state (18 words), zero before the launch (grid > 1 only)
     uint32_t xp[64];    // X^j
     uint32_t xq[64];    // X^(64 j)
     uint32_t xr[64];    // X^(4096 j)
 };
+
+// The long kernels' cross-workgroup XOR (thread 0 of each workgroup, value v):
+// workgroup b adds v into accumulator b % 8 with a device-scope atomic and
+// counts itself in; the last of its group (by the returned ticket) moves the
+// group's value into a top accumulator and counts the group in; the last
+// group writes fin(total) and every word it used is left zero again for the
+// next lease. Eight groups keep the end of the launch free of a 2-atomics-
+// per-workgroup queue on one address (grid up to 256 workgroups).
+// state: acc[8], cnt[8], top, topcnt (T words each, zeroed).
+template <typename T, typename F>
+__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
+    using A = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
+    A* st = reinterpret_cast<A*>(state);
+    const uint32_t grid = gridDim.x;
+    if (grid == 1) {
+        *out = fin(v);
+        return;
+    }
+    const uint32_t g = blockIdx.x & 7u;
+    const uint32_t members = (grid + 7u - g) / 8u, groups = grid < 8u ? grid : 8u;
+    atomicXor(st + g, (A)v);
+    __threadfence();
+    if (atomicAdd(st + 8 + g, (A)1) != members - 1) return;
+    __threadfence();
+    const A gv = atomicExch(st + g, (A)0);  // every member's XOR has landed
+    atomicExch(st + 8 + g, (A)0);
+    atomicXor(st + 16, gv);
+    __threadfence();
+    if (atomicAdd(st + 17, (A)1) != groups - 1) return;
+    __threadfence();
+    *out = fin((T)atomicExch(st + 16, (A)0));
+    atomicExch(st + 17, (A)0);
+}
 
 // X^m for m < 2^18 from the three power tables (wave-uniform m: scalar reads).
 template <typename A>
@@ -1399,17 +1434,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneCon
         uint32_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        if (gridDim.x == 1) {
-            *a.out = v;
-        } else {
-            atomicXor(a.acc, v);
-            __threadfence();
-            if (atomicAdd(a.acc + 1, 1u) == gridDim.x - 1) {
-                __threadfence();
-                *a.out = atomicExch(a.acc, 0u);  // every workgroup's XOR has landed
-                atomicExch(a.acc + 1, 0u);
-            }
-        }
+        long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
     }
 }
 

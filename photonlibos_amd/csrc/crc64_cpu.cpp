@@ -11,6 +11,7 @@
 #include <errno.h>
 #include <immintrin.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "gf2.h"
@@ -145,7 +146,81 @@ void build_fold() {
     g_have_pclmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
 }
 
+// AVX-512 VPCLMULQDQ (Zen 4/5 EPYC, Ice Lake and later Xeons): the same
+// folding, four 512-bit registers = 16 states, 256 bytes per step
+// (crc32c_cpu.cpp has the CRC-32C twin). Constants per move of D bytes:
+// {x^(8D+63), x^(8D-1)} mod P in every 128-bit lane.
+#define PCRC64_V512 __attribute__((target("avx512f,avx512bw,avx512vl,avx512dq,vpclmulqdq,pclmul,sse4.1")))
+
+struct alignas(64) V512Fold64 {
+    uint64_t k256[8], k192[8], k128[8], k64[8], kred[8];
+};
+V512Fold64 g_v64;
+bool g_have_v512 = false;
+
+void fold_pair(uint64_t* k, uint64_t bytes) {
+    k[0] = pcrc::xpow64(8 * bytes + 63);
+    k[1] = pcrc::xpow64(8 * bytes - 1);
+}
+
+void build_v512() {
+    for (int l = 0; l < 4; ++l) {
+        fold_pair(g_v64.k256 + 2 * l, 256);
+        fold_pair(g_v64.k192 + 2 * l, 192);
+        fold_pair(g_v64.k128 + 2 * l, 128);
+        fold_pair(g_v64.k64 + 2 * l, 64);
+    }
+    fold_pair(g_v64.kred + 0, 48);
+    fold_pair(g_v64.kred + 2, 32);
+    fold_pair(g_v64.kred + 4, 16);
+    g_v64.kred[6] = g_v64.kred[7] = 0;
+    g_have_v512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                  __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512dq") &&
+                  __builtin_cpu_supports("vpclmulqdq") && __builtin_cpu_supports("pclmul") &&
+                  __builtin_cpu_supports("sse4.1") && !getenv("PHOTON_CRC_NO_AVX512");
+}
+
+PCRC64_V512 inline __m512i fold512_64(__m512i a, __m512i k, __m512i d) {
+    return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(a, k, 0x00), _mm512_clmulepi64_epi128(a, k, 0x11), d,
+                                     0x96);
+}
+
+PCRC64_V512 uint64_t engine64_v512(const uint8_t* p, size_t n, uint64_t c) {
+    // n >= 256
+    const __m512i k256 = _mm512_load_si512(g_v64.k256);
+    __m512i a0 = _mm512_xor_si512(_mm512_loadu_si512(p), _mm512_zextsi128_si512(_mm_cvtsi64_si128((long long)c)));
+    __m512i a1 = _mm512_loadu_si512(p + 64);
+    __m512i a2 = _mm512_loadu_si512(p + 128);
+    __m512i a3 = _mm512_loadu_si512(p + 192);
+    p += 256;
+    n -= 256;
+    for (; n >= 256; p += 256, n -= 256) {
+        a0 = fold512_64(a0, k256, _mm512_loadu_si512(p));
+        a1 = fold512_64(a1, k256, _mm512_loadu_si512(p + 64));
+        a2 = fold512_64(a2, k256, _mm512_loadu_si512(p + 128));
+        a3 = fold512_64(a3, k256, _mm512_loadu_si512(p + 192));
+    }
+    const __m512i k64 = _mm512_load_si512(g_v64.k64);
+    __m512i r = fold512_64(a0, _mm512_load_si512(g_v64.k192), a3);
+    r = fold512_64(a1, _mm512_load_si512(g_v64.k128), r);
+    r = fold512_64(a2, k64, r);
+    for (; n >= 64; p += 64, n -= 64) r = fold512_64(r, k64, _mm512_loadu_si512(p));
+    const __m512i kr = _mm512_load_si512(g_v64.kred);
+    const __m512i t = _mm512_xor_si512(_mm512_clmulepi64_epi128(r, kr, 0x00), _mm512_clmulepi64_epi128(r, kr, 0x11));
+    __m128i x = _mm_ternarylogic_epi64(_mm512_castsi512_si128(t), _mm512_extracti64x2_epi64(t, 1),
+                                       _mm512_extracti64x2_epi64(t, 2), 0x96);
+    x = _mm_xor_si128(x, _mm512_extracti64x2_epi64(r, 3));
+    const __m128i k16 = _mm_set_epi64x((long long)g_fold.k1_hi, (long long)g_fold.k1_lo);
+    for (; n >= 16; p += 16, n -= 16)
+        x = _mm_ternarylogic_epi64(_mm_clmulepi64_si128(x, k16, 0x00), _mm_clmulepi64_si128(x, k16, 0x11),
+                                   _mm_loadu_si128(reinterpret_cast<const __m128i*>(p)), 0x96);
+    uint8_t tail[16];
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(tail), x);
+    return engine64(p, n, engine64(tail, 16, 0));
+}
+
 uint64_t engine64_hw(const uint8_t* p, size_t n, uint64_t c) {
+    if (g_have_v512 && n >= 256) return engine64_v512(p, n, c);
     return g_have_pclmul ? engine64_clmul(p, n, c) : engine64(p, n, c);
 }
 
@@ -186,6 +261,7 @@ uint64_t (*crc64ecma_trim_auto)(CRC64ECMA_Component, CRC64ECMA_Component, CRC64E
 __attribute__((constructor(101))) static void photon_crc64_cpu_init() {
     build64();
     build_fold();
+    build_v512();
     crc64ecma_auto = crc64ecma_hw;
     crc64ecma_series_auto = crc64ecma_series_hw;
     crc64ecma_combine_auto = crc64ecma_combine_hw;

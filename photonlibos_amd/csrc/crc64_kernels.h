@@ -660,7 +660,7 @@ struct Long64Args {
     uint64_t first, chunk, nchunks;
     uint64_t seed;
     uint64_t* out;
-    uint64_t* acc;      // {accumulator, ticket}: zero before the launch (grid > 1 only)
+    uint64_t* acc;      // long_reduce state (18 words), zero before the launch (grid > 1 only)
     uint64_t xp[64];    // X^j, X = x^(8*chunk) mod P64
     uint64_t xq[64];    // X^(64 j)
     uint64_t xr[64];    // X^(4096 j)
@@ -697,17 +697,7 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
         uint64_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        if (gridDim.x == 1) {
-            *a.out = ~v;
-        } else {
-            atomicXor(reinterpret_cast<unsigned long long*>(a.acc), (unsigned long long)v);
-            __threadfence();
-            if (atomicAdd(reinterpret_cast<unsigned long long*>(a.acc + 1), 1ull) == gridDim.x - 1) {
-                __threadfence();
-                *a.out = ~(uint64_t)atomicExch(reinterpret_cast<unsigned long long*>(a.acc), 0ull);
-                atomicExch(reinterpret_cast<unsigned long long*>(a.acc + 1), 0ull);
-            }
-        }
+        long_reduce(v, a.acc, a.out, [](uint64_t x) { return ~x; });  // crc.cpp:119-122: inverted out
     }
 }
 

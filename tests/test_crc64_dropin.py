@@ -2,6 +2,7 @@
 against the reference's golden data (checksum.crc64) and the reference's own
 outputs (ref_vectors.json: crc64ecma_sw, combine_sw/hw, trim_sw/hw). CPU only."""
 import ctypes
+import os
 
 import pytest
 
@@ -62,15 +63,38 @@ def test_trim_error_path():
 
 
 def test_hw_folding_matches_sw():
-    # crc64ecma_hw (PCLMUL folding, 4 interleaved 16-byte states) against the
-    # table engine: every length through the fold thresholds, odd offsets, seeds.
+    # crc64ecma_hw (AVX-512 VPCLMULQDQ folding, 16 states in 4 zmm, on CPUs
+    # that have it; PCLMUL folding, 4 interleaved 16-byte states, below 256 B
+    # and elsewhere) against the table engine: every length through the fold
+    # thresholds of both (64/256-B steps, 64- and 16-B tails), odd offsets, seeds.
     import random
     from photonlibos_amd import datagen
     rnd = random.Random(0xF0D)
     data = datagen.stream_bytes(0xF0D, (1 << 20) + 64).tobytes()
-    lengths = list(range(0, 600)) + [1023, 1024, 4096, 65535, 65536, 65537, 1 << 20]
+    lengths = list(range(0, 1100)) + [1023, 1024, 4096, 65535, 65536, 65537, 1 << 20]
     for n in lengths:
         for off in (0, 3, 8, 13):
             seed = rnd.getrandbits(64) if n % 2 else 0
             b = data[off:off + n]
             assert ck.crc64ecma_hw(b, seed) == ck.crc64ecma_sw(b, seed), (n, off)
+
+
+def test_hw_engines_without_avx512():
+    # PHOTON_CRC_NO_AVX512 (read once at load) pins the 128-bit PCLMUL engines
+    # on any CPU: the same parity for them, in a fresh interpreter.
+    import subprocess
+    import sys
+    code = ("import random\n"
+            "from photonlibos_amd import checksum as ck, datagen\n"
+            "from tests import _oracle as o\n"
+            "d = datagen.stream_bytes(0xA5, 70000).tobytes()\n"
+            "r = random.Random(4)\n"
+            "for n in list(range(0, 1100)) + [r.randrange(1100, 69000) for _ in range(60)]:\n"
+            "    for off in (0, 5):\n"
+            "        b = d[off:off + n]\n"
+            "        s32, s64 = r.getrandbits(32), r.getrandbits(64)\n"
+            "        assert ck.crc32c_hw(b, s32) == o.crc32c(b, s32), n\n"
+            "        assert ck.crc64ecma_hw(b, s64) == o.crc64ecma(b, s64), n\n")
+    env = dict(os.environ, PHOTON_CRC_NO_AVX512="1")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run([sys.executable, "-c", code], check=True, env=env, cwd=repo, timeout=300)
