@@ -726,6 +726,7 @@ LongPlan long_plan(uint64_t n, int cus) {
     const uint64_t waves = (p.nchunks * (uint64_t)lanes + 63) / 64;
     p.grid = (waves + kWaves - 1) / kWaves;
     if (p.grid > (uint64_t)cus) p.grid = cus;
+    if (p.grid > kLongMaxGrid) p.grid = kLongMaxGrid;  // long_reduce's slots
     return p;
 }
 
@@ -1320,9 +1321,9 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     memcpy(a.xp, pw.p64[0], sizeof(a.xp));
     memcpy(a.xq, pw.p64[1], sizeof(a.xq));
     memcpy(a.xr, pw.p64[2], sizeof(a.xr));
-    void* state = nullptr;  // long_reduce's 18 words, left zeroed by the kernel
+    void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
     if (lp.grid > 1) {
-        if (int rc = scratch_alloc(&state, 18 * 8, st, true)) return rc;
+        if (int rc = scratch_alloc(&state, 8 + 8 * kLongMaxGrid, st, true)) return rc;
         a.acc = static_cast<uint64_t*>(state);
     }
     if (lp.lanes == 32)
@@ -1424,9 +1425,9 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     memcpy(a.xp, pw.p32[0], sizeof(a.xp));
     memcpy(a.xq, pw.p32[1], sizeof(a.xq));
     memcpy(a.xr, pw.p32[2], sizeof(a.xr));
-    void* state = nullptr;  // long_reduce's 18 words, left zeroed by the kernel
+    void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
     if (lp.grid > 1) {
-        if (int rc = scratch_alloc(&state, 18 * 4, st, true)) return rc;
+        if (int rc = scratch_alloc(&state, 8 + 8 * kLongMaxGrid, st, true)) return rc;
         a.acc = static_cast<uint32_t*>(state);
     }
     if (lp.lanes == 32)

@@ -13,6 +13,12 @@
 #ifndef PCRC_LANE_SEL
 #define PCRC_LANE_SEL 1  // per-lane v_perm selectors instead of rotating the word (+0.3 % on C2)
 #endif
+#ifndef PCRC_LONG_LEAD
+#define PCRC_LONG_LEAD true  // long kernels: lead rows + partial row preloaded (A/B: false)
+#endif
+#ifndef PCRC_BATCH_LEAD
+#define PCRC_BATCH_LEAD false  // the same in the buffer batch (A/B: true)
+#endif
 // buf_body's row loop (A/B variants): 0 = one register set
 // copied cur <- nxt on the loop edge (the default); 1 = the compiler's unroll
 // by two (no copies; the next step's loads issued before this step's land:
@@ -320,9 +326,15 @@ __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc
     }
     const uint32_t dv = basis_entry(kBasisD32.w, t, b);  // (b << 8t) * x^32
     const uint32_t sv = basis_entry(kc.sbasis, t, b);    // (b << 8t) * x^(8*16*G)
+    // Row b holds slice t's 8 replicas in words t*8 .. t*8+7 (bank t*8 + r):
+    // lanes of a wavefront share t and differ in b (row stride 64 words, the
+    // same bank), so writing replica r in step r put all 64 lanes on ONE bank
+    // (≈5 µs of a launch, scripts/probe_long_times.py). Lane l writes replica
+    // (i + l) % 8 in step i: 8 banks per instruction.
     const uint32_t base = ((b << 8) + (t << 5)) >> 2;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t r = (i + tid) & 7u;
         lds[base + r] = dv;
         lds[base + kSOff / 4 + r] = sv;
     }
@@ -451,10 +463,12 @@ __device__ __forceinline__ BufGeo buf_geo(const uint8_t* p, uint64_t n, uint32_t
     return g;
 }
 
-template <int U>
+template <int U, bool LEAD = false>
 struct BufPre {
     uint4 w0;      // row 0 (the head)
-    uint4 cur[U];  // rows 1..U
+    uint4 cur[U];  // rows 1..U (LEAD: 1+lead..lead+U)
+    uint4 wl[LEAD ? U - 1 : 1];  // LEAD: rows 1..lead, lead = (full-1) % U
+    uint4 wp;                    // LEAD: the partial last row
 };
 
 // Issue row 0 and the first step's U rows (vmcnt counts in order: waiting
@@ -463,19 +477,35 @@ struct BufPre {
 // row 0, or a buffer too short for a first step, re-reads the aligned start
 // (in bounds; the values are discarded), so there is no divergent region
 // around the loads and every later wait counts exactly.
-template <int G, int U>
-__device__ __forceinline__ void buf_preload(const BufGeo& g, uint32_t gl, BufPre<U>& pre) {
+// LEAD (long chunks, one buffer per lane group): the lead rows and the
+// partial last row are issued here too, so the U-row loop ends exactly at
+// the last full row and no row is loaded on its own and waited for (without
+// it a 16 KiB chunk ended in three serial load-wait-reduce rows; the CRC-64
+// kernels do the same, crc64_kernels.h buffer_reg64).
+template <int G, int U, bool LEAD = false>
+__device__ __forceinline__ void buf_preload(const BufGeo& g, uint32_t gl, BufPre<U, LEAD>& pre) {
     if (g.tiny) return;
     const uint8_t* p0 = gl < g.nb ? g.lp : g.a0;
     pre.w0 = load16(p0);
-    const bool step = 1 + U <= g.full;
+    if constexpr (LEAD) {
+        const uint32_t lead = g.full >= 1 ? (uint32_t)((g.full - 1) % U) : 0u;
 #pragma unroll
-    for (int u = 0; u < U; ++u) pre.cur[u] = load16(step ? g.lp + (1 + u) * (16 * G) : p0);
+        for (int u = 0; u < U - 1; ++u) pre.wl[u] = load16((uint32_t)u < lead ? g.lp + (1 + u) * (16 * G) : p0);
+        const bool step = 1 + lead + U <= g.full;
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre.cur[u] = load16(step ? g.lp + (1 + lead + u) * (16 * G) : p0);
+        const bool part = g.full >= 1 && g.full < g.rows && g.full * G + gl < g.nb;
+        pre.wp = load16(part ? g.lp + g.full * (16 * G) : p0);
+    } else {
+        const bool step = 1 + U <= g.full;
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre.cur[u] = load16(step ? g.lp + (1 + u) * (16 * G) : p0);
+    }
 }
 
 // The lane's lagged column partial Q over every row (the preloaded ones first).
-template <int G, int U>
-__device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& g, const BufPre<U>& pre,
+template <int G, int U, bool LEAD = false>
+__device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& g, const BufPre<U, LEAD>& pre,
                                              uint32_t seed, uint32_t gl, const LaneAddr& la) {
     if (g.tiny) return 0;
     // Row 0 holds the head: masked leading bytes + seed (branch-free; lanes
@@ -490,6 +520,13 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
     uint32_t pc = lag16(lds, w, la);
     // Full rows 1..full-1: U rows per step, the next U in flight.
     uint64_t row = 1;
+    if constexpr (LEAD) {
+        const uint32_t lead = g.full >= 1 ? (uint32_t)((g.full - 1) % U) : 0u;
+#pragma unroll
+        for (int u = 0; u < U - 1; ++u)
+            if ((uint32_t)u < lead) pc = sstep(lds, pc, la, lag16(lds, pre.wl[u], la));
+        row += lead;
+    }
     const uint8_t* lp = g.lp;
     if (row + U <= g.full) {
 #if PCRC_BODY == 2
@@ -538,10 +575,14 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
         row += U;
 #endif
     }
-    for (; row < g.full; ++row) pc = sstep(lds, pc, la, lag16(lds, load16(lp + row * (16 * G)), la));
-    // Partial last row.
-    if (g.full >= 1 && g.full < g.rows && g.full * G + gl < g.nb)
-        pc = sstep(lds, pc, la, lag16(lds, load16(lp + g.full * (16 * G)), la));
+    const bool part = g.full >= 1 && g.full < g.rows && g.full * G + gl < g.nb;
+    if constexpr (LEAD) {
+        if (part) pc = sstep(lds, pc, la, lag16(lds, pre.wp, la));
+    } else {
+        for (; row < g.full; ++row) pc = sstep(lds, pc, la, lag16(lds, load16(lp + row * (16 * G)), la));
+        // Partial last row.
+        if (part) pc = sstep(lds, pc, la, lag16(lds, load16(lp + g.full * (16 * G)), la));
+    }
     return pc;
 }
 
@@ -592,13 +633,13 @@ __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo
 
 // CRC-32C of one buffer (seed applied) by a group of G lanes, unpipelined;
 // the result is valid on every lane of the group.
-template <int G, int U>
+template <int G, int U, bool LEAD = false>
 __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_t* p, uint64_t n, uint32_t seed,
                                                uint32_t gl, const LaneAddr& la) {
     const BufGeo g = buf_geo<G>(p, n, gl);
-    BufPre<U> pre;
-    buf_preload<G, U>(g, gl, pre);
-    const uint32_t pc = buf_body<G, U>(lds, g, pre, seed, gl, la);
+    BufPre<U, LEAD> pre;
+    buf_preload<G, U, LEAD>(g, gl, pre);
+    const uint32_t pc = buf_body<G, U, LEAD>(lds, g, pre, seed, gl, la);
     return buf_finish<G>(lds, g, pc, p, n, seed, gl, la);
 }
 
@@ -760,7 +801,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             }
             if (args.seeds) seed = args.seeds[bi];
         }
-        const uint32_t crc = buffer_crc<G, U>(lds, p, n, seed, gl, la);
+        const uint32_t crc = buffer_crc<G, U, PCRC_BATCH_LEAD>(lds, p, n, seed, gl, la);
         if (active && gl == 0) args.out[bi] = crc;
     }
 }
@@ -1358,43 +1399,53 @@ struct LongArgs {
     uint64_t nchunks;   // T
     uint32_t seed;
     uint32_t* out;
-    uint32_t* acc;      // long_reduce state (18 words), zero before the launch (grid > 1 only)
+    uint32_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes, ticket zero; grid > 1 only)
     uint32_t xp[64];    // X^j
     uint32_t xq[64];    // X^(64 j)
     uint32_t xr[64];    // X^(4096 j)
 };
 
-// The long kernels' cross-workgroup XOR (thread 0 of each workgroup, value v):
-// workgroup b adds v into accumulator b % 8 with a device-scope atomic and
-// counts itself in; the last of its group (by the returned ticket) moves the
-// group's value into a top accumulator and counts the group in; the last
-// group writes fin(total) and every word it used is left zero again for the
-// next lease. Eight groups keep the end of the launch free of a 2-atomics-
-// per-workgroup queue on one address (grid up to 256 workgroups).
-// state: acc[8], cnt[8], top, topcnt (T words each, zeroed).
+// The long kernels' cross-workgroup XOR, called by EVERY thread of wave 0
+// with its workgroup's value v (valid on lane 0): lane 0 stores v into the
+// workgroup's slot and takes a ticket (release: the slot is visible first);
+// the workgroup that takes the last ticket (acquire) loads all slots at
+// once, XORs them, writes fin(total) and puts the ticket back to 0 for the
+// next lease. Two dependent round trips at the end of the launch (slot
+// store + ticket, slot loads); the round-3 first form -- device-scope
+// atomicXor into one accumulator, or into eight with a second level -- was
+// a chain of 4-7 dependent atomics with fences, 8 µs after the last chunk
+// (scripts/probe_long_times.py). state: ticket, then kLongMaxGrid slots
+// (8 + 8 * kLongMaxGrid bytes).
+constexpr uint32_t kLongMaxGrid = 512;
 template <typename T, typename F>
 __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
-    using A = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
-    A* st = reinterpret_cast<A*>(state);
-    const uint32_t grid = gridDim.x;
+    const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
     if (grid == 1) {
-        *out = fin(v);
+        if (lane == 0) *out = fin(v);
         return;
     }
-    const uint32_t g = blockIdx.x & 7u;
-    const uint32_t members = (grid + 7u - g) / 8u, groups = grid < 8u ? grid : 8u;
-    atomicXor(st + g, (A)v);
-    __threadfence();
-    if (atomicAdd(st + 8 + g, (A)1) != members - 1) return;
-    __threadfence();
-    const A gv = atomicExch(st + g, (A)0);  // every member's XOR has landed
-    atomicExch(st + 8 + g, (A)0);
-    atomicXor(st + 16, gv);
-    __threadfence();
-    if (atomicAdd(st + 17, (A)1) != groups - 1) return;
-    __threadfence();
-    *out = fin((T)atomicExch(st + 16, (A)0));
-    atomicExch(st + 17, (A)0);
+    // The same layout for both widths (the zeroed scratch class is shared by
+    // the CRC32C and CRC-64 kernels): a 32-bit ticket in bytes 0-3 (4-7 stay
+    // zero), slots from byte 8.
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(state);
+    T* slot = reinterpret_cast<T*>(reinterpret_cast<char*>(state) + 8);
+    uint32_t last = 0;
+    if (lane == 0) {
+        slot[blockIdx.x] = v;
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+    }
+    if (!__shfl(last, 0)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    T x = 0;
+    for (uint32_t w = lane; w < grid; w += 64) x ^= __hip_atomic_load(slot + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (sizeof(T) == 8)
+        x = ((T)group_xor<64>((uint32_t)(x >> 32)) << 32) | group_xor<64>((uint32_t)x);
+    else
+        x = group_xor<64>(x);
+    if (lane == 0) {
+        *out = fin(x);
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // X^m for m < 2^18 from the three power tables (wave-uniform m: scalar reads).
@@ -1424,13 +1475,13 @@ __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneCon
         const bool active = t < a.nchunks;
         const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
         const uint64_t n = !active ? 0 : t ? a.chunk : a.first;
-        uint32_t crc = buffer_crc<G, U>(lds, p, n, t ? 0u : a.seed, gl, la);
+        uint32_t crc = buffer_crc<G, U, PCRC_LONG_LEAD>(lds, p, n, t ? 0u : a.seed, gl, la);
         if (active) acc ^= long_shift(crc, a.nchunks - 1 - t, a);
     }
     acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their chunks' values
     if (lane == 0) red[wave] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (wave == 0) {
         uint32_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];

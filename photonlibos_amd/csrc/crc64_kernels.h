@@ -240,8 +240,11 @@ __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64
         const uint2 dv = u2of(basis_entry64(kBasisD64.w, t, b));
         const uint2 sv = u2of(basis_entry64(kc.sbasis, t, b));
         const uint32_t base = (b << 8) + (t << 5);
+        // replica (i + e) % 4 in step i: the lanes (same t, rows 256 B apart)
+        // spread over 4 bank pairs instead of one (crc32c_kernels.h build_tables)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t r = (i + e) & 3u;
             *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + base + r * 8) = dv;
             *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + k64SBase + base + r * 8) = sv;
         }
@@ -660,7 +663,7 @@ struct Long64Args {
     uint64_t first, chunk, nchunks;
     uint64_t seed;
     uint64_t* out;
-    uint64_t* acc;      // long_reduce state (18 words), zero before the launch (grid > 1 only)
+    uint64_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes, ticket zero; grid > 1 only)
     uint64_t xp[64];    // X^j, X = x^(8*chunk) mod P64
     uint64_t xq[64];    // X^(64 j)
     uint64_t xr[64];    // X^(4096 j)
@@ -693,7 +696,7 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
     acc = ((uint64_t)group_xor<64>((uint32_t)(acc >> 32)) << 32) | group_xor<64>((uint32_t)acc);
     if (lane == 0) red[wave] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (wave == 0) {
         uint64_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
