@@ -51,6 +51,7 @@
 #include "../../include/photon_crc/tuning.h"
 #include "crc32c_kernels.h"
 #include "crc64_kernels.h"
+#include "long_plan.h"
 #include "gf2.h"
 #include "internal.h"
 
@@ -695,83 +696,20 @@ int pipe_init(HostPipe& p) {
 }
 
 // One long buffer (photon_crc32c_extend_device, photon_crc64ecma_extend_device):
-// T chunks (the first one shorter), one per lane group of the long kernels.
-// Up to 256 KiB: at most 16 chunks of >= 4 KiB in one workgroup of 64-lane
-// groups, the result written directly (latency). Above: chunks of >= 16 KiB
-// (4 KiB multiples), `rounds` chunks per lane group of a full grid (16 waves
-// per CU; VERDICT r2: the piece batch used to fill half, or an eighth, of the
-// chip). Lane groups and rounds: tuning.h photon_crc_set_long_shape.
+// chunk 0 = the unaligned head up to the first 4 KiB boundary, then T-1
+// aligned chunks of `chunk` bytes (a multiple of 1 KiB: whole rows),
+// the last one cut at the end (crc32c_kernels.h "one long buffer"). Up to
+// 256 KiB: at most 16 chunks of >= 4 KiB in one workgroup of 64-lane groups,
+// the result written directly (latency). Above: chunks of >= 16 KiB,
+// `rounds` chunks per lane group of a full grid (16 waves per CU; VERDICT r2:
+// the piece batch used to fill half, or an eighth, of the chip), T equal to
+// the grid's lane-group slots so every group gets the same number of chunks
+// (chunk sizes were 4 KiB multiples before: up to one round of imbalance).
+// Lane groups and rounds: tuning.h photon_crc_set_long_shape.
 std::atomic<uint32_t> g_long_shape{0};  // lanes | rounds << 8; 0 = automatic
 
-struct LongPlan {
-    uint64_t chunk, first, nchunks, grid;
-    int lanes;
-};
-
-LongPlan long_plan(uint64_t n, int cus) {
-    const uint32_t shape = g_long_shape.load(std::memory_order_relaxed);
-    const bool small = n <= (256u << 10);
-    const int lanes = small || !(shape & 0xff) ? 64 : (int)(shape & 0xff);
-    const uint64_t rounds = small || !(shape >> 8) ? 1 : shape >> 8;
-    const uint64_t slots = small ? 16 : 16ull * (uint64_t)cus * (64 / (uint64_t)lanes) * rounds;
-    uint64_t chunk = ((n + slots - 1) / slots + 4095) & ~4095ull;
-    const uint64_t lo = small ? 4096 : 16384;
-    if (chunk < lo) chunk = lo;
-    while ((n + chunk - 1) / chunk > (1u << 18)) chunk <<= 1;  // the kernels' three 64-entry power tables
-    LongPlan p;
-    p.lanes = lanes;
-    p.chunk = chunk;
-    p.nchunks = n ? (n + chunk - 1) / chunk : 1;
-    p.first = n - (p.nchunks - 1) * chunk;
-    const uint64_t waves = (p.nchunks * (uint64_t)lanes + 63) / 64;
-    p.grid = (waves + kWaves - 1) / kWaves;
-    if (p.grid > (uint64_t)cus) p.grid = cus;
-    if (p.grid > kLongMaxGrid) p.grid = kLongMaxGrid;  // long_reduce's slots
-    return p;
-}
-
-// X^j, X^(64 j), X^(4096 j), j < 64, X = x^(8 * chunk) (CRC-32C or CRC-64/ECMA),
-// computed on first use per chunk size and kept (callers repeat sizes).
-struct LongPowers {
-    uint32_t p32[3][64];
-    uint64_t p64[3][64];
-};
-
-const LongPowers& long_powers(uint64_t chunk, bool crc64) {
-    static std::mutex mu;
-    static std::vector<std::pair<uint64_t, LongPowers*>> cache[2];
-    thread_local LongPowers overflow;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        for (auto& e : cache[crc64])
-            if (e.first == chunk) return *e.second;
-    }
-    LongPowers* t = new LongPowers();
-    for (int lvl = 0; lvl < 3; ++lvl) {
-        const uint64_t bits = (8 * chunk) << (6 * lvl);  // X^(64^lvl)
-        if (crc64) {
-            const uint64_t y = xpow64(bits);
-            t->p64[lvl][0] = kOne64;
-            for (int j = 1; j < 64; ++j) t->p64[lvl][j] = mulmod64(t->p64[lvl][j - 1], y);
-        } else {
-            const uint32_t x = xpow(bits);
-            t->p32[lvl][0] = kOne;
-            for (int j = 1; j < 64; ++j) t->p32[lvl][j] = mulmod(t->p32[lvl][j - 1], x);
-        }
-    }
-    std::lock_guard<std::mutex> lk(mu);
-    for (auto& e : cache[crc64])
-        if (e.first == chunk) {
-            delete t;
-            return *e.second;
-        }
-    if (cache[crc64].size() >= 256) {  // many distinct sizes: compute per call
-        overflow = *t;
-        delete t;
-        return overflow;
-    }
-    cache[crc64].emplace_back(chunk, t);
-    return *t;
+LongPlan long_plan(const void* data, uint64_t n, int cus) {
+    return long_plan_for(data, n, cus, g_long_shape.load(std::memory_order_relaxed));
 }
 
 }  // namespace
@@ -1309,16 +1247,20 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const LongPlan lp = long_plan(nbytes, cus);
-    const LongPowers& pw = long_powers(lp.chunk, true);
+    const LongPlan lp = long_plan(d_data, nbytes, cus);
+    const LongPowers& pw = long_powers(lp, true);
     Long64Args a{};
     a.data = static_cast<const uint8_t*>(d_data);
-    a.first = lp.first;
+    a.nbytes = nbytes;
+    a.head = lp.head;
     a.chunk = lp.chunk;
     a.nchunks = lp.nchunks;
     a.seed = seed;
+    a.jinv = pw.jinv64;
+    a.xs = pw.xs64;
+    a.stride = lp.stride;
     a.out = d_out;
-    memcpy(a.xp, pw.p64[0], sizeof(a.xp));
+    memcpy(a.xp, pw.xpj64, sizeof(a.xp));
     memcpy(a.xq, pw.p64[1], sizeof(a.xq));
     memcpy(a.xr, pw.p64[2], sizeof(a.xr));
     void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
@@ -1413,16 +1355,20 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const LongPlan lp = long_plan(nbytes, cus);
-    const LongPowers& pw = long_powers(lp.chunk, false);
+    const LongPlan lp = long_plan(d_data, nbytes, cus);
+    const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
     a.data = static_cast<const uint8_t*>(d_data);
-    a.first = lp.first;
+    a.nbytes = nbytes;
+    a.head = lp.head;
     a.chunk = lp.chunk;
     a.nchunks = lp.nchunks;
     a.seed = seed;
+    a.jinv = pw.jinv32;
+    a.xs = pw.xs32;
+    a.stride = lp.stride;
     a.out = d_out;
-    memcpy(a.xp, pw.p32[0], sizeof(a.xp));
+    memcpy(a.xp, pw.xpj32, sizeof(a.xp));
     memcpy(a.xq, pw.p32[1], sizeof(a.xq));
     memcpy(a.xr, pw.p32[2], sizeof(a.xr));
     void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel

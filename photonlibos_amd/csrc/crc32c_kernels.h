@@ -283,6 +283,15 @@ __device__ __forceinline__ uint32_t basis_entry(const B& basis, uint32_t t, uint
     return r;
 }
 
+// Workgroup barrier after LDS writes: this wave's LDS stores complete
+// (lgkmcnt(0)), then s_barrier. Unlike __syncthreads it does not wait for
+// the wave's global loads (vmcnt), so rows issued before the table prologue
+// stay in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt, expcnt: no wait
+    __builtin_amdgcn_s_barrier();
+}
+
 // Build the D and S tables in LDS (every workgroup; 1024 threads = one entry of
 // each table per thread).
 // FG = 0: R_k lane-combine tables; FG = 4 or 8: F_d finish tables for G = FG;
@@ -338,7 +347,7 @@ __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc
         lds[base + r] = dv;
         lds[base + kSOff / 4 + r] = sv;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 __device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
@@ -1380,27 +1389,41 @@ __global__ void crc32c_trim_kernel(const photon_crc_component* all, const photon
 
 // ------------------------------------------------------- one long buffer
 // photon_crc32c_extend_device (crc32c_extend, crc32c.h:30-33, over ONE
-// device buffer) in ONE launch that fills the chip. The buffer is cut into
-// T chunks, one per wavefront: chunk 0 = [0, first), chunk t >= 1 = [first +
-// (t-1)*chunk, first + t*chunk), so every chunk after the first is full and
-// ends (T-1-t)*chunk bytes before the end. A wave computes its chunk's CRC
-// (the seed in chunk 0 only; buffer_crc with 64 lanes) and shifts it to the
-// end of the buffer: crc_t * X^(T-1-t), X = x^(8*chunk), as two GF(2)
-// products by host-computed powers X^(m%64) and X^(64*(m/64)) (T <= 4096).
-// By linearity (crc.cpp:393-405) the buffer's CRC is the XOR of the shifted
-// chunk CRCs: waves XOR-reduce in registers and LDS, each workgroup XORs its
-// value into an accumulator word with one device-scope atomic, and the last
-// workgroup (ticket counter) writes the result and zeroes accumulator and
-// ticket. One workgroup (T <= 16) writes the result directly.
+// device buffer) in ONE launch that fills the chip. The buffer is cut into T
+// chunks on a grid anchored at an ABSOLUTE 4 KiB boundary A (the first one at
+// or after the data start): chunk 0 = [data, A) (the unaligned head, 0..4095
+// bytes, with the seed), chunk t >= 1 = [A + (t-1) chunk, A + t chunk), the
+// last one cut at the end of the buffer (L_last bytes, 0 < L_last <= chunk).
+// Every chunk but the two ends is aligned and whole, so no chunk has a masked
+// head or a byte-serial tail (round 3's first form anchored the grid at the
+// END of the buffer: at the reference's base+1 every chunk paid both).
+// By linearity (crc.cpp:393-405) the CRC is the XOR of the chunks' CRCs each
+// shifted by the bytes after it: with X = x^(8 chunk) and c'_t = crc_t
+// (t < T-1), c'_(T-1) = crc_(T-1) * x^(8 (chunk - L_last)) (the last chunk as
+// if it were whole), CRC = J * XOR_t c'_t X^(T-1-t), J = x^-(8 (chunk -
+// L_last)). A lane group's chunks are t_k = t_0 + k S (S = lane groups in the
+// grid), so it accumulates them in Horner form, acc <- acc X^S ^ c'_t: ONE
+// multiply by the launch constant X^S per chunk, done lane-parallel (each of
+// 32 lanes holds one basis word of X^S, a select and a 32-lane XOR), and at
+// the end one multiply by the group's factor J X^(T-1-t_last), lane-parallel
+// too (its basis words computed after the group's first chunk, off the
+// launch's critical tail). Round 3's first form: three 32-step bit-serial
+// multiplies per chunk (~600 VALU on every lane) and J at the very end.
+// Waves XOR-reduce in registers and LDS; workgroups through long_reduce.
 struct LongArgs {
     const uint8_t* data;
-    uint64_t first;     // bytes of chunk 0 (1..chunk; the whole buffer when T == 1)
+    uint64_t nbytes;
+    uint64_t head;      // bytes of chunk 0 = A - data (the whole buffer when T == 1)
     uint64_t chunk;
     uint64_t nchunks;   // T
     uint32_t seed;
+    uint32_t jinv;      // x^(8 (chunk - L_last)), applied to the last chunk's CRC (kOne when T == 1)
+    uint32_t xs;        // X^S
+    uint64_t stride;    // S: lane groups in the grid
     uint32_t* out;
     uint32_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes, ticket zero; grid > 1 only)
-    uint32_t xp[64];    // X^j
+    uint32_t xp[64];    // J X^j, J = x^-(8 (chunk - L_last)) (kOne when T == 1): every group's
+                        // final factor carries J once, so the total needs no last multiply
     uint32_t xq[64];    // X^(64 j)
     uint32_t xr[64];    // X^(4096 j)
 };
@@ -1448,7 +1471,7 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
     }
 }
 
-// X^m for m < 2^18 from the three power tables (wave-uniform m: scalar reads).
+// crc * J X^m for m < 2^18 from the three power tables (xp holds J X^j).
 template <typename A>
 __device__ __forceinline__ uint32_t long_shift(uint32_t crc, uint64_t m, const A& a) {
     crc = mulmod(crc, a.xp[m & 63u]);
@@ -1457,36 +1480,134 @@ __device__ __forceinline__ uint32_t long_shift(uint32_t crc, uint64_t m, const A
     return crc;
 }
 
-// G lanes per chunk (64: one wavefront; 32: two chunks per wavefront).
-template <int G, int U>
-__global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneConsts kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
-    __shared__ uint32_t red[kWaves];
+// J X^m (no leading multiply by one).
+template <typename A>
+__device__ __forceinline__ uint32_t long_pow(uint64_t m, const A& a) {
+    uint32_t k = a.xp[m & 63u];
+    if (m >= 64) k = mulmod(k, a.xq[(m >> 6) & 63u]);
+    if (m >= 4096) k = mulmod(k, a.xr[(m >> 12) & 63u]);
+    return k;
+}
+
+// v * x mod P (reflected: bit j = coefficient of x^(31-j)).
+__device__ __forceinline__ uint32_t mulx(uint32_t v) { return (v >> 1) ^ ((0u - (v & 1u)) & kPoly); }
+
+// Basis word i of a multiplication by c: (1 << i) * c = c * x^(31-i), by
+// 31 select steps (wave-uniform trip count; once per kernel).
+__device__ __forceinline__ uint32_t basis_word(uint32_t c, uint32_t i) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 31; ++k) c = k < 31 - i ? mulx(c) : c;
+    return c;
+}
+
+// v * c for a v held by every lane of a 32-lane half (lane l of the half
+// holds bw = basis word l of c): one select per lane and a 32-lane XOR.
+__device__ __forceinline__ uint32_t mul_lanes(uint32_t v, uint32_t bw, uint32_t l32) {
+    return group_xor<32>(((v >> l32) & 1u) ? bw : 0u);
+}
+
+// The chunk of a long buffer: [*p, *p + *n).
+template <typename A>
+__device__ __forceinline__ void long_chunk(const A& a, uint64_t t, const uint8_t** p, uint64_t* n) {
+    if (t == 0) {
+        *p = a.data;
+        *n = a.head;
+        return;
+    }
+    const uint64_t off = a.head + (t - 1) * a.chunk;
+    *p = a.data + off;
+    *n = t >= a.nchunks ? 0 : (a.nbytes - off < a.chunk ? a.nbytes - off : a.chunk);
+}
+
+// G lanes per chunk (64: one wavefront; 32: two chunks per wavefront), U rows
+// per step. STAMP and ABL are for the bench-only probe (probes.hip): STAMP =
+// per-wave s_memrealtime stamps into t (8 words per wave); ABL bits = cost
+// attribution, results NOT the CRC unless noted: 1 = chunks without the
+// lead-row preload (correct), 2 = every chunk shifted on its own, no Horner
+// (correct), 4 = no final shift and no cross-workgroup reduce.
+template <int G, int U, bool STAMP = false, int ABL = 0>
+__device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc, uint32_t* lds, uint32_t* red,
+                                         uint64_t* t) {
+    uint64_t t0 = 0, c0 = 0, t_tab = 0;
+    if constexpr (STAMP) {
+        t0 = __builtin_amdgcn_s_memrealtime();
+        c0 = __builtin_amdgcn_s_memtime();
+    }
     build_tables<G>(lds, kc);
+    if constexpr (STAMP) t_tab = __builtin_amdgcn_s_memrealtime();
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
     const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr la = lane_addr(lane);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    const uint32_t l32 = lane & 31u;
+    // The group's chunks: tf, tf + S, ..., tl (none when tf >= T).
+    const uint64_t tf = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
+    const uint64_t tl = tf < a.nchunks ? tf + (a.nchunks - 1 - tf) / a.stride * a.stride : 0;
+    uint32_t bw = 0, bwk = 0;  // basis words of X^S and of the group's final factor J X^(T-1-tl)
     uint32_t acc = 0;
+    bool first = true;
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
-        const uint64_t t = wv * GPW + grp;
-        const bool active = t < a.nchunks;
-        const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
-        const uint64_t n = !active ? 0 : t ? a.chunk : a.first;
-        uint32_t crc = buffer_crc<G, U, PCRC_LONG_LEAD>(lds, p, n, t ? 0u : a.seed, gl, la);
-        if (active) acc ^= long_shift(crc, a.nchunks - 1 - t, a);
+        const uint64_t tc = wv * GPW + grp;
+        const bool active = tc < a.nchunks;
+        const uint8_t* p;
+        uint64_t n;
+        long_chunk(a, tc, &p, &n);
+        uint32_t crc = buffer_crc<G, U, (ABL & 1) ? false : PCRC_LONG_LEAD>(lds, p, n, tc ? 0u : a.seed, gl, la);
+        if (tc == a.nchunks - 1) crc = mulmod(crc, a.jinv);
+        if constexpr (ABL & 2) {
+            if (active) acc ^= long_shift(crc, a.nchunks - 1 - tc, a);
+        } else {
+            if (first) {
+                // Once, after the first chunk (not in front of the first
+                // loads): 62 select steps and up to two multiplies per lane.
+                bw = basis_word(a.xs, l32);
+                bwk = basis_word(long_pow(tf < a.nchunks ? a.nchunks - 1 - tl : 0, a), l32);
+                first = false;
+            }
+            const uint32_t m = mul_lanes(acc, bw, l32);  // every lane: the halves stay convergent
+            if (active) acc = m ^ crc;
+        }
     }
-    acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their chunks' values
+    if constexpr (!(ABL & 6)) acc = mul_lanes(acc, bwk, l32);  // acc = 0 for a group without chunks
+    uint64_t t_body = 0;
+    if constexpr (STAMP) t_body = __builtin_amdgcn_s_memrealtime();
+    acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their values
     if (lane == 0) red[wave] = acc;
     __syncthreads();
     if (wave == 0) {
         uint32_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
+        if constexpr (ABL & 4) {
+            if (lane == 0) *a.out = v;
+        } else {
+            long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
+        }
     }
+    if constexpr (STAMP) {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime();
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            uint64_t* o = t + 8 * ((uint64_t)blockIdx.x * kWaves + wave);
+            o[0] = t0;
+            o[1] = t_tab;
+            o[2] = t_body;
+            o[3] = t1;
+            o[4] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+            o[5] = __builtin_amdgcn_s_getreg(20 | (3 << 11));
+            o[6] = c0;
+            o[7] = c1;
+        }
+    }
+}
+
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneConsts kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
+    __shared__ uint32_t red[kWaves];
+    long_run<G, U>(a, kc, lds, red, nullptr);
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {

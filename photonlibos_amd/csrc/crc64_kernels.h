@@ -654,20 +654,38 @@ __global__ void crc64_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_
 }
 
 // photon_crc64ecma_extend_device in one launch: crc32c_long_kernel's scheme
-// (chunks, one per wavefront, shifted to the end by X^(T-1-t), XOR-reduced by
-// workgroup atomics, the last workgroup writes) on the raw CRC-64 register:
-// chunk 0 starts from ~seed, the others from 0, the result is inverted
-// (crc.cpp:119-122).
+// (crc32c_kernels.h "one long buffer": chunk grid anchored at a 4 KiB
+// boundary, Horner accumulation per lane group with a lane-parallel multiply
+// by X^S, one general shift per group, workgroups XOR-reduced by
+// long_reduce) on the raw CRC-64 register: chunk 0 starts from ~seed, the
+// others from 0, the result is inverted (crc.cpp:119-122).
 struct Long64Args {
     const uint8_t* data;
-    uint64_t first, chunk, nchunks;
+    uint64_t nbytes, head, chunk, nchunks;
     uint64_t seed;
+    uint64_t jinv, xs;  // as LongArgs, mod P64
+    uint64_t stride;
     uint64_t* out;
     uint64_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes, ticket zero; grid > 1 only)
-    uint64_t xp[64];    // X^j, X = x^(8*chunk) mod P64
+    uint64_t xp[64];    // J X^j, X = x^(8*chunk) mod P64
     uint64_t xq[64];    // X^(64 j)
     uint64_t xr[64];    // X^(4096 j)
 };
+
+__device__ __forceinline__ uint64_t mulx64(uint64_t v) { return (v >> 1) ^ ((0ull - (v & 1ull)) & kPoly64); }
+
+// (1 << i) * c = c * x^(63-i) (63 select steps, once per kernel).
+__device__ __forceinline__ uint64_t basis_word64(uint64_t c, uint32_t i) {
+#pragma unroll 1
+    for (uint32_t k = 0; k < 63; ++k) c = k < 63 - i ? mulx64(c) : c;
+    return c;
+}
+
+__device__ __forceinline__ uint64_t xor_lanes64(uint64_t v, int width) {
+    const uint32_t lo = width == 64 ? group_xor<64>((uint32_t)v) : group_xor<32>((uint32_t)v);
+    const uint32_t hi = width == 64 ? group_xor<64>((uint32_t)(v >> 32)) : group_xor<32>((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 
 template <int G>
 __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneConsts64 kc) {
@@ -680,20 +698,47 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
     const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr64 la = lane_addr64(lane);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    // Basis words of X^S and of the group's final factor J X^(T-1-tl): 64
+    // lanes one each (G = 64), or two per lane of a 32-lane half (bits l and
+    // l + 32); computed after the group's first chunk.
+    const uint32_t l = G == 64 ? lane : (lane & 31u);
+    const uint64_t t0 = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
+    const uint64_t tl = t0 < a.nchunks ? t0 + (a.nchunks - 1 - t0) / a.stride * a.stride : 0;
+    uint64_t bw0 = 0, bw1 = 0, bk0 = 0, bk1 = 0;
+    bool first = true;
+    auto mul_basis_lanes = [&](uint64_t v, uint64_t b0, uint64_t b1) {
+        uint64_t term = ((v >> l) & 1ull) ? b0 : 0ull;
+        if (G != 64) term ^= ((v >> (l + 32)) & 1ull) ? b1 : 0ull;
+        return xor_lanes64(term, G == 64 ? 64 : 32);
+    };
     uint64_t acc = 0;
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
         const uint64_t t = wv * GPW + grp;
         const bool active = t < a.nchunks;
-        const uint8_t* p = t ? a.data + a.first + (t - 1) * a.chunk : a.data;
-        const uint64_t n = !active ? 0 : t ? a.chunk : a.first;
+        const uint8_t* p;
+        uint64_t n;
+        long_chunk(a, t, &p, &n);
         uint64_t reg = buffer_reg64<G>(lds, p, n, t ? 0ull : ~a.seed, gl, lane, la);  // valid on gl == 0
-        const uint64_t m = a.nchunks - 1 - t;
-        reg = mulmod64(reg, a.xp[m & 63u]);
-        if (m >= 64) reg = mulmod64(reg, a.xq[(m >> 6) & 63u]);
-        if (m >= 4096) reg = mulmod64(reg, a.xr[(m >> 12) & 63u]);
-        if (active && gl == 0) acc ^= reg;
+        reg = __shfl(reg, lane & ~(uint32_t)(G - 1), 64);                        // the whole group
+        if (t == a.nchunks - 1) reg = mulmod64(reg, a.jinv);
+        if (first) {
+            const uint64_t m = t0 < a.nchunks ? a.nchunks - 1 - tl : 0;
+            uint64_t k = a.xp[m & 63u];
+            if (m >= 64) k = mulmod64(k, a.xq[(m >> 6) & 63u]);
+            if (m >= 4096) k = mulmod64(k, a.xr[(m >> 12) & 63u]);
+            bw0 = basis_word64(a.xs, l);
+            bk0 = basis_word64(k, l);
+            if (G != 64) {
+                bw1 = basis_word64(a.xs, l + 32);
+                bk1 = basis_word64(k, l + 32);
+            }
+            first = false;
+        }
+        const uint64_t m = mul_basis_lanes(acc, bw0, bw1);
+        if (active) acc = m ^ reg;
     }
-    acc = ((uint64_t)group_xor<64>((uint32_t)(acc >> 32)) << 32) | group_xor<64>((uint32_t)acc);
+    acc = mul_basis_lanes(acc, bk0, bk1);
+    acc = xor_lanes64(gl == 0 ? acc : 0ull, 64);
     if (lane == 0) red[wave] = acc;
     __syncthreads();
     if (wave == 0) {

@@ -10,6 +10,7 @@
 
 #include "crc32c_kernels.h"
 #include "crc64_kernels.h"
+#include "long_plan.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
@@ -269,55 +270,18 @@ __global__ __launch_bounds__(1024) void group_rows_stamped_kernel(const uint8_t*
     ws.store(t, blockIdx.x * 16ull + wave);
 }
 
-// The product's crc32c_long_kernel<64, 4> (one long buffer, one chunk per
-// wavefront) with 8 stamps per wave: s_memrealtime at the start, after the
-// table prologue, after the wave's chunks, after the cross-workgroup reduce;
-// HW_ID, XCC_ID, s_memtime at the start and end. Attributes a launch's fixed
-// cost (scripts/probe_long_times.py).
+// The product's crc32c_long_kernel<G, 4> (one long buffer, chunks per lane
+// group: the same long_run) with 8 stamps per wave: s_memrealtime at the
+// start, after the LDS table prologue, after the wave's chunks and after the
+// cross-workgroup reduce; HW_ID, XCC_ID, s_memtime at the start and end.
+// Attributes a launch's fixed cost (scripts/probe_long_times.py).
+// ABL: long_run's cost-attribution bits (crc32c_kernels.h).
+template <int G, int ABL>
 __global__ __launch_bounds__(pcrc::kBlock) void long_stamped_kernel(pcrc::LongArgs a, pcrc::LaneConsts kc, uint64_t* t) {
     using namespace pcrc;
-    constexpr int G = 64, U = 4;
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
     __shared__ uint32_t red[kWaves];
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t c0 = __builtin_amdgcn_s_memtime();
-    build_tables<G>(lds, kc);
-    const uint64_t t_tab = __builtin_amdgcn_s_memrealtime();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = wave_id();
-    const LaneAddr la = lane_addr(lane);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-    uint32_t acc = 0;
-    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv < a.nchunks; wv += nwaves) {
-        const uint64_t c = wv;
-        const uint8_t* p = c ? a.data + a.first + (c - 1) * a.chunk : a.data;
-        const uint64_t n = c ? a.chunk : a.first;
-        const uint32_t crc = buffer_crc<G, U, PCRC_LONG_LEAD>(lds, p, n, c ? 0u : a.seed, lane, la);
-        acc ^= long_shift(crc, a.nchunks - 1 - c, a);
-    }
-    const uint64_t t_body = __builtin_amdgcn_s_memrealtime();
-    acc = group_xor<64>(lane == 0 ? acc : 0u);
-    if (lane == 0) red[wave] = acc;
-    __syncthreads();
-    if (wave == 0) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
-    }
-    const uint64_t c1 = __builtin_amdgcn_s_memtime();
-    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) {
-        const uint64_t gw = (uint64_t)blockIdx.x * kWaves + wave;
-        t[8 * gw] = t0;
-        t[8 * gw + 1] = t_tab;
-        t[8 * gw + 2] = t_body;
-        t[8 * gw + 3] = t1;
-        t[8 * gw + 4] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
-        t[8 * gw + 5] = __builtin_amdgcn_s_getreg(20 | (3 << 11));
-        t[8 * gw + 6] = c0;
-        t[8 * gw + 7] = c1;
-    }
+    long_run<G, 4, true, ABL>(a, kc, lds, red, t);
 }
 
 extern "C" {
@@ -480,35 +444,53 @@ int probe_read_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t c
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// long_stamped_kernel over [data, data + n): `chunk` bytes per wavefront (a
-// 4 KiB multiple; chunk 0 takes the remainder), grid = min(cus, waves / 16);
-// `state` = 8 + 8 * kLongMaxGrid bytes, the first 8 zero (left zero), t = 8 words per wave.
-int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint64_t chunk, uint32_t* out, uint32_t* state,
-                       uint64_t* t, int cus, void* stream) {
+// long_stamped_kernel<lanes> over [data, data + n), cut as the product cuts it
+// for photon_crc_set_long_shape(lanes, rounds) (long_plan.h); `state` = 8 + 8
+// * kLongMaxGrid bytes, the first 8 zero (left zero); t = 8 words per wave of
+// grid * 16 waves; *grid_out = the grid. force_chunk: a chunk size (a 1 KiB
+// multiple) instead of the plan's (0 = the plan's). rounds | ablation << 8
+// (long_run's ABL bits, 0..5).
+int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* out, uint32_t* state, uint64_t* t,
+                       int cus, int lanes, int rounds, uint64_t force_chunk, int* grid_out, void* stream) {
     using namespace pcrc;
-    if (!chunk || (chunk & 4095) || !n) return -22;
+    if ((lanes != 64 && lanes != 32) || (rounds & 255) < 1 || (rounds & 255) > 64) return -22;
+    if (force_chunk & 1023) return -22;
+    const LongPlan lp = long_plan_for(data, n, cus, (uint32_t)lanes | (uint32_t)(rounds & 255) << 8, force_chunk);
+    if (lp.nchunks > (1u << 18)) return -22;
+    const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
     a.data = static_cast<const uint8_t*>(data);
-    a.chunk = chunk;
-    a.nchunks = (n + chunk - 1) / chunk;
-    if (a.nchunks > (1u << 18)) return -22;
-    a.first = n - (a.nchunks - 1) * chunk;
+    a.nbytes = n;
+    a.head = lp.head;
+    a.chunk = lp.chunk;
+    a.nchunks = lp.nchunks;
     a.seed = seed;
+    a.jinv = pw.jinv32;
+    a.xs = pw.xs32;
+    a.stride = lp.stride;
     a.out = out;
     a.acc = state;
-    for (int lvl = 0; lvl < 3; ++lvl) {
-        const uint32_t x = xpow((8 * chunk) << (6 * lvl));
-        uint32_t* dst = lvl == 0 ? a.xp : lvl == 1 ? a.xq : a.xr;
-        dst[0] = kOne;
-        for (int j = 1; j < 64; ++j) dst[j] = mulmod(dst[j - 1], x);
-    }
+    memcpy(a.xp, pw.xpj32, sizeof(a.xp));
+    memcpy(a.xq, pw.p32[1], sizeof(a.xq));
+    memcpy(a.xr, pw.p32[2], sizeof(a.xr));
     LaneConsts kc{};
-    kc.kshift = xpow(8ull * 16ull * 64ull);
+    kc.kshift = xpow(8ull * 16ull * (uint64_t)lp.lanes);
     mul_basis(kc.kshift, kc.sbasis);
-    uint64_t grid = (a.nchunks + kWaves - 1) / kWaves;
-    if (grid > (uint64_t)cus) grid = cus;
-    if (grid > kLongMaxGrid) grid = kLongMaxGrid;
-    hipLaunchKernelGGL(long_stamped_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a, kc, t);
+    *grid_out = (int)lp.grid;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int abl = rounds >> 8;  // rounds | ablation bits << 8
+#define LSK(G, B) hipLaunchKernelGGL((long_stamped_kernel<G, B>), dim3(lp.grid), dim3(kBlock), 0, s, a, kc, t)
+#define LSG(B) if (lp.lanes == 64) LSK(64, B); else LSK(32, B)
+    switch (abl) {
+        case 1: LSG(1); break;
+        case 2: LSG(2); break;
+        case 3: LSG(3); break;
+        case 4: LSG(4); break;
+        case 5: LSG(5); break;
+        default: LSG(0); break;
+    }
+#undef LSG
+#undef LSK
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""A/B of one long buffer (photon_crc32c_extend_device) across library builds
+and long-kernel shapes in ONE process, interleaved rounds with alternating
+order (DVFS moves the clock between processes and with launch history, so
+only interleaved runs compare; cdna_hip_programming.md §5.4 rule 24).
+Bench-only.
+
+  LIBS      name=path,... of libphoton_checksum.so builds (default: new = in-tree)
+  VARIANTS  name:lanes/rounds,... (0/0 = automatic); probe:lanes/rounds/chunk_kib[/abl]
+            (the stamped probe build of the same long_run, libphoton_probes.so,
+            with that chunk size forced; 0 = the plan's); plus "batch64k" (the
+            strided batch kernel over the same bytes as 64 KiB pieces from an
+            aligned base) and "read" (the read-only grid-stride stream)
+  SIZES_MIB buffer sizes (at base+1, test_checksum.cpp:125-168)
+  LAUNCHES  back-to-back launches per variant per round, ROUNDS rounds
+Prints one JSON line per (size, variant): mean / median ms over all launches,
+frac of 8 TB/s; every variant's CRC must equal the first's."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from photonlibos_amd import checksum as ck  # noqa: E402
+
+vp, u64, u32, ci = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+libs = {}
+for item in os.environ.get("LIBS", "new=" + os.path.join(REPO, "photonlibos_amd/lib/libphoton_checksum.so")).split(","):
+    name, path = item.split("=", 1)
+    lib = ctypes.CDLL(path if os.path.isabs(path) else os.path.join(REPO, path), mode=ctypes.RTLD_LOCAL)
+    lib.photon_crc32c_extend_device.argtypes = [vp, u64, u32, vp, vp]
+    lib.photon_crc32c_extend_device.restype = ci
+    lib.photon_crc_set_long_shape.argtypes = [ci, ci]
+    lib.photon_crc_set_long_shape.restype = ci
+    libs[name] = lib
+VARIANTS = os.environ.get("VARIANTS", "new:0/0,batch64k,read").split(",")
+OFF = int(os.environ.get("OFF", "1"))  # buffer start offset from a 2 MiB-aligned allocation
+P = ctypes.CDLL(os.path.join(REPO, "photonlibos_amd", "lib", "libphoton_probes.so"))
+P.probe_long_stamped.argtypes = [vp, u64, u32, vp, vp, vp, ci, ci, ci, u64, vp, vp]
+P.probe_long_stamped.restype = ci
+cus = torch.cuda.get_device_properties(0).multi_processor_count
+SIZES = [int(x) << 20 for x in os.environ.get("SIZES_MIB", "1024").split(",")]
+N = int(os.environ.get("LAUNCHES", "10"))
+ROUNDS = int(os.environ.get("ROUNDS", "6"))
+
+st = torch.cuda.current_stream()
+big = max(SIZES)
+d = torch.empty(big + 4096, dtype=torch.uint8, device="cuda")
+ck.fill_splitmix(d, big + 4096, big + 4096, 1, 0x5EED0B00, stream=st)
+out = torch.zeros(N, dtype=torch.int32, device="cuda")
+pstate = torch.zeros(1024, dtype=torch.int32, device="cuda")
+pstamps = torch.zeros(8 * 16 * cus, dtype=torch.int64, device="cuda")
+pgrid = ctypes.c_int(0)
+sink = torch.zeros(1 << 22, dtype=torch.int32, device="cuda")
+
+
+def make(v, n):
+    # "variant@OFFSET": that buffer start offset for this variant (default OFF;
+    # batch64k: its pieces start at the offset, default 0)
+    off = OFF
+    if "@" in v:
+        v, o = v.split("@")
+        off = int(o)
+    elif v == "batch64k":
+        off = 0
+    if v == "read":
+        return lambda k: ck.read_stream(d.data_ptr(), n, sink, sink.numel(), stream=st)
+    if v == "batch64k":
+        pieces = torch.zeros(n >> 16, dtype=torch.int32, device="cuda")
+        cnt = (n - off) >> 16
+        return lambda k: ck.batch_strided(d.data_ptr() + off, 65536, 65536, cnt, pieces, stream=st)
+    name, shape = v.split(":")
+    if name == "probe":
+        parts = [int(x) for x in shape.split("/")]
+        lanes, rounds, ckib = parts[:3]
+        rounds |= (parts[3] if len(parts) > 3 else 0) << 8  # long_run ablation bits
+
+        def fp(k):
+            rc = P.probe_long_stamped(d.data_ptr() + off, n, 7, out.data_ptr() + 4 * k, pstate.data_ptr(),
+                                      pstamps.data_ptr(), cus, lanes, rounds, ckib * 1024, ctypes.byref(pgrid),
+                                      ctypes.c_void_p(st.cuda_stream))
+            assert rc == 0, (v, rc)
+        return fp
+    lanes, rounds = (int(x) for x in shape.split("/"))
+    lib = libs[name]
+
+    def f(k):
+        lib.photon_crc_set_long_shape(lanes, rounds)
+        rc = lib.photon_crc32c_extend_device(d.data_ptr() + off, n, 7, out.data_ptr() + 4 * k,
+                                             ctypes.c_void_p(st.cuda_stream))
+        assert rc == 0, (v, rc)
+    return f
+
+
+for n in SIZES:
+    fns = {v: make(v, n) for v in VARIANTS}
+    times = {v: [] for v in VARIANTS}
+    crcs = {}
+    for r in range(ROUNDS):
+        for v in (VARIANTS if r % 2 == 0 else VARIANTS[::-1]):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(N)]
+            for k in range(N):
+                ev[k][0].record(st)
+                fns[v](k)
+                ev[k][1].record(st)
+            torch.cuda.synchronize()
+            times[v] += [a.elapsed_time(b) for a, b in ev]
+            if ":" in v and "@" not in v:
+                crcs.setdefault(v, set()).update(int(x) & 0xFFFFFFFF for x in out.cpu().numpy())
+    for lib in libs.values():
+        lib.photon_crc_set_long_shape(0, 0)
+    ref = None
+    for v in VARIANTS:
+        t = np.array(times[v])
+        row = {"n": n, "variant": v, "ms_mean": round(float(t.mean()), 4), "ms_median": round(float(np.median(t)), 4),
+               "frac": round(n / float(t.mean()) / 8e9, 4), "launches": len(t)}
+        if v in crcs:
+            ref = crcs[v] if ref is None else ref
+            row["same_crc"] = len(crcs[v]) == 1 and crcs[v] == ref
+        print(json.dumps(row), flush=True)

@@ -39,7 +39,10 @@ def timed(fn, reps=20):
 
 
 SHAPES = {"c3": (4096, 1 << 20, (8, 16, 32)), "c2": (65536, 65536, (8, 16, 32, 64)), "c5": (8192, 1 << 19, (8, 16)),
-          "c4": (1 << 20, 4096, (16, 32, 64))}
+          "c4": (1 << 20, 4096, (16, 32, 64)),
+          # one 1 GiB buffer's worth (the reference's perf shape) as the long
+          # kernel cuts it: 16 Ki x 64 KiB and 4 Ki x 256 KiB pieces
+          "g1_64k": (65536, 16384, (32, 64)), "g1_256k": (1 << 18, 4096, (32, 64))}
 wanted = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c3", "c2"]
 
 

@@ -236,3 +236,40 @@ def test_extend_device_concurrent_streams(torch_dev, oracle):
         for r in range(4):
             assert int(got[r]) == oracle.crc32c(host[k:k + n - 8 * k], r + k), (k, r)
     del d
+
+
+@pytest.mark.parametrize("shape", [(0, 0), (64, 1), (64, 2), (32, 1), (32, 2), (32, 3)])
+def test_extend_device_aligned_grid_edges(torch_dev, oracle, shape):
+    # The chunk grid is anchored at the first 4 KiB boundary at or after the
+    # data start (long_plan.h): chunk 0 = the head (0 bytes when the data is
+    # 4 KiB-aligned, < 64 bytes on the byte-serial path, up to 4095), the last
+    # chunk cut at the end (1 byte up to a whole chunk), the whole buffer in
+    # chunk 0 when it ends before the boundary. Every lane/round shape
+    # (photon_crc_set_long_shape; (0, 0) = automatic), CRC-32C and CRC-64.
+    torch = torch_dev
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    lanes, rounds = shape
+    ck.set_long_shape(lanes, rounds)
+    try:
+        full = 16 * cus * (64 // (lanes or 64)) * (rounds or 1)  # lane-group slots of a full grid
+        n_full = 16384 * full  # the 16 KiB chunk floor of a full grid (64 MiB at 64 x 1)
+        d = torch.empty(n_full + 4 * 4096, dtype=torch.uint8, device="cuda")
+        ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0900 + lanes + rounds)
+        host = d.cpu().numpy()
+        al = (-d.data_ptr()) % 4096  # offset of the first 4 KiB boundary
+        cases = [(al, n_full), (al + 1, n_full), (al + 4095, n_full + 1),
+                 (al + 4096 - 10, 300 << 10), (al + 4096 - 100, (300 << 10) + 1),
+                 (al + 4096 - 5, 4), (al + 4096 - 5, 5), (al + 4096 - 5, 6), (al + 7, 4096 - 7),
+                 (al + 3, (256 << 10) + 4093), (al + 2, n_full - (16 << 10) + 1), (al + 5, 40 << 20)]
+        assert max(off + n for off, n in cases) <= d.numel()
+        for k, (off, n) in enumerate(cases):
+            seed = (k * 0x9E3779B1 + 1) & 0xFFFFFFFF
+            want = oracle.crc32c(host[off:off + n], seed)
+            assert _extend(torch, d, off, n, seed) == want, (shape, off - al, n)
+            if k == 0 or n < (1 << 20):
+                s64 = seed * 0x100000001
+                assert _extend(torch, d, off, n, s64, True) == oracle.crc64ecma(host[off:off + n], s64), \
+                    (shape, off - al, n)
+        del d
+    finally:
+        ck.set_long_shape(0, 0)
