@@ -575,7 +575,33 @@ def run_extend(args, stream):
         res[label] = {"bytes": nbytes, "kernel_ms_mean": round(float(np.mean(t)), 4),
                       "kernel_ms_median": round(float(np.median(t)), 4), "GiB_per_s": round(gbps * 1e9 / GIB, 1),
                       "frac_of_8TBps": round(gbps / HBM_PEAK_GBPS, 4),
+                      "frac_of_8TBps_median_launch": round(nbytes / (float(np.median(t)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                       "call_wait_us_median": round(float(np.median(lat)) * 1e6, 1)}
+    # What the same bytes can do as independent pieces, interleaved with the
+    # long kernel in rounds (the clock moves with launch history): the strided
+    # batch over 16 Ki x 64 KiB from an aligned base (no cross-chunk combine,
+    # no cross-workgroup reduce) and the read-only grid-stride stream.
+    pieces = torch.zeros(n >> 16, dtype=torch.int32, device="cuda")
+    sink = torch.zeros(1 << 22, dtype=torch.int32, device="cuda")
+    cmp_fns = {"long_kernel": lambda k: ck.extend_device(d.data_ptr() + 1, n, 0, out[k:k + 1], stream=stream),
+               "batch_64KiB_pieces": lambda k: ck.batch_strided(d.data_ptr(), 65536, 65536, n >> 16, pieces,
+                                                                stream=stream),
+               "read_stream": lambda k: ck.read_stream(d.data_ptr(), n, sink, sink.numel(), stream=stream)}
+    cmp_t = {k: [] for k in cmp_fns}
+    for r in range(6):
+        for name in (list(cmp_fns) if r % 2 == 0 else list(cmp_fns)[::-1]):
+            evs = []
+            for k in range(8):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                cmp_fns[name](k)
+                b.record(stream)
+                evs.append((a, b))
+            torch.cuda.synchronize()
+            cmp_t[name] += [a.elapsed_time(b) for a, b in evs]
+    res["1GiB_interleaved"] = {name: {"ms_median": round(float(np.median(v)), 4),
+                                      "frac_median_launch": round(n / (float(np.median(v)) * 1e-3) / 1e9 /
+                                                                  HBM_PEAK_GBPS, 4)} for name, v in cmp_t.items()}
     want = ck.crc32c_hw(d[1:1 + (128 << 10)].cpu().numpy().tobytes())
     ck.extend_device(d.data_ptr() + 1, 128 << 10, 0, out[:1], stream=stream)
     torch.cuda.synchronize()

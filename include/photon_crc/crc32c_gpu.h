@@ -147,8 +147,10 @@ int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, 
  *                    gives 0 (the reference's EINVAL result) and, when d_nerr
  *                    is non-null, increments *d_nerr (zero it beforehand);
  *   extend_device:   *d_out = crc32c_extend(d_data, nbytes, seed) for ONE
- *                    long buffer: split into up to 4096 pieces that run in
- *                    parallel, then combined on the device.
+ *                    long buffer in ONE launch over the whole device: chunks
+ *                    on a grid anchored at a 4 KiB boundary, each lane group's
+ *                    chunks folded in registers, the workgroups' values
+ *                    XOR-combined by the last workgroup to finish.
  * Asynchronous on `stream` like the batches. */
 int photon_crc32c_series_device(const void* d_buffer, uint32_t part_size, uint32_t n_parts, uint32_t* d_crc_parts,
                                 void* stream);
@@ -158,6 +160,21 @@ int photon_crc32c_trim_batch(const photon_crc_component* d_all, const photon_crc
                              const photon_crc_component* d_suffix, uint64_t count, uint32_t* d_out,
                              uint32_t* d_nerr, void* stream);
 int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, void* stream);
+
+/* (many GPUs) ONE logical buffer whose bytes lie on several devices of this
+ * process: span i = [d_data, d_data + nbytes) on `device`, the spans in
+ * buffer order. Every span runs photon_crc32c_extend_device (from seed 0) on
+ * its own device, all devices at once; the host folds the span CRCs with
+ * crc32c_combine's identity (crc.cpp:393-405): acc = seed, then acc =
+ * acc * x^(8 len_i) ^ crc_i. 4 bytes per device cross the host link; no
+ * collective. Synchronous: *h_result = crc32c_extend(buffer, total, seed).
+ * The caller's current device is restored. */
+typedef struct photon_crc_span {
+    int device;
+    const void* d_data;
+    uint64_t nbytes;
+} photon_crc_span;
+int photon_crc32c_extend_spans(const photon_crc_span* spans, int nspans, uint32_t seed, uint32_t* h_result);
 
 /* Route the drop-in entry points to the device when handed device memory:
  * with on != 0, crc32c_auto / crc32c_series_auto / crc32c_combine_series_auto
@@ -194,7 +211,7 @@ int photon_crc64ecma_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, ui
  *                  ecosystem/oss.h:217 expected_crc64); d_seg_out[s] = each
  *                  segment's crc64ecma(seg, 0); nseg == d_msg_start[nmsg];
  *   extend_device: *d_out = crc64ecma_extend(d_data, nbytes, seed) for ONE
- *                  long device buffer (split, run in parallel, folded). */
+ *                  long device buffer (one launch, as the CRC32C call). */
 /* Same layout as CRC64ECMA_Component {uint64_t crc; uint64_t size;}
  * (common/checksum/crc64ecma.h:68-71). */
 typedef struct photon_crc64_component {
@@ -222,6 +239,9 @@ int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* 
                                  uint64_t* d_out, void* stream);
 int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,
                                    void* stream);
+/* photon_crc32c_extend_spans for CRC-64/ECMA (crc64ecma_combine's identity:
+ * the inverted CRC folds the same way). */
+int photon_crc64ecma_extend_spans(const photon_crc_span* spans, int nspans, uint64_t seed, uint64_t* h_result);
 
 /* Synchronous convenience: photon_crc32c_batch_strided + stream sync. */
 int photon_crc32c_batch_strided_sync(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,

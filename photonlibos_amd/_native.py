@@ -88,6 +88,8 @@ def _declare(L):
     fn("photon_crc32c_combine_series_device", ctypes.c_int, vp, u32, u32, vp, vp)
     fn("photon_crc32c_trim_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp, vp)
     fn("photon_crc32c_extend_device", ctypes.c_int, vp, u64, u32, vp, vp)
+    fn("photon_crc32c_extend_spans", ctypes.c_int, vp, ctypes.c_int, u32, vp)
+    fn("photon_crc64ecma_extend_spans", ctypes.c_int, vp, ctypes.c_int, u64, vp)
     fn("photon_crc_set_device_dispatch", ctypes.c_int, ctypes.c_int)
     fn("photon_crc32c_batch_msg_n", ctypes.c_int, vp, vp, u64, u64, u32, vp, vp, vp, vp)
     # include/photon_crc/checked_batch.h

@@ -28,7 +28,7 @@ __all__ = [
     "Shard", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
     "crc64ecma_combine_series", "crc64ecma_trim",
-    "batch64_strided", "batch64_iov", "combine64_batch", "trim64_batch", "batch64_msg_n", "host_batch64_strided", "extend64_device", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
+    "batch64_strided", "batch64_iov", "combine64_batch", "trim64_batch", "batch64_msg_n", "host_batch64_strided", "extend64_device", "extend_spans", "extend64_spans", "Span", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
 ]
 
 _CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
@@ -398,6 +398,34 @@ def trim_batch(all_, prefix, suffix, count, out, nerr=None, stream=None):
 def extend_device(data, nbytes, seed, out, stream=None):
     """*out = crc32c_extend(data, nbytes, seed) for one long device buffer. Async."""
     _check(lib().photon_crc32c_extend_device(_ptr(data), nbytes, seed & 0xFFFFFFFF, _ptr(out), _stream(stream)))
+
+
+class Span(ctypes.Structure):
+    """photon_crc_span (include/photon_crc/crc32c_gpu.h)."""
+    _fields_ = [("device", ctypes.c_int), ("d_data", ctypes.c_void_p), ("nbytes", ctypes.c_uint64)]
+
+
+def _spans(spans):
+    arr = (Span * max(1, len(spans)))()
+    for a, (dev, ptr, n) in zip(arr, spans):
+        a.device, a.d_data, a.nbytes = dev, _ptr(ptr), n
+    return arr
+
+
+def extend_spans(spans, seed=0):
+    """crc32c_extend over ONE buffer whose bytes lie on several devices:
+    spans = [(device, device_pointer, nbytes), ...] in buffer order. Synchronous."""
+    res = ctypes.c_uint32(0)
+    _check(lib().photon_crc32c_extend_spans(_spans(spans), len(spans), seed & 0xFFFFFFFF, ctypes.byref(res)))
+    return res.value
+
+
+def extend64_spans(spans, seed=0):
+    """crc64ecma_extend over ONE buffer spanning devices (see extend_spans). Synchronous."""
+    res = ctypes.c_uint64(0)
+    _check(lib().photon_crc64ecma_extend_spans(_spans(spans), len(spans), seed & 0xFFFFFFFFFFFFFFFF,
+                                               ctypes.byref(res)))
+    return res.value
 
 
 def set_device_dispatch(on):

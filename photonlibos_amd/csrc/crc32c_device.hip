@@ -1389,6 +1389,76 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     return rc;
 }
 
+}  // extern "C"
+
+namespace pcrc {
+namespace {
+
+// photon_crc32c_extend_spans / photon_crc64ecma_extend_spans: every span's
+// CRC (seed 0) on its own device, the kernels of all devices enqueued before
+// any wait, then the host fold acc = acc * x^(8 len) ^ crc (crc.cpp:393-405).
+template <typename T, typename Launch, typename Shift>
+int extend_spans(const photon_crc_span* spans, int nspans, T seed, T* h_result, Launch launch, Shift shift) {
+    if (nspans < 0 || (nspans && !spans) || !h_result) return fail(-EINVAL, "bad span list or result");
+    int prev = -1;
+    hipError_t e = hipGetDevice(&prev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    std::vector<void*> outs(nspans, nullptr);
+    std::vector<T> crcs(nspans, 0);
+    int rc = 0;
+    int issued = 0;
+    for (int i = 0; i < nspans && !rc; ++i, ++issued) {
+        const photon_crc_span& sp = spans[i];
+        if (!sp.d_data && sp.nbytes) {
+            rc = fail(-EINVAL, "null span with bytes");
+            break;
+        }
+        if ((e = hipSetDevice(sp.device)) != hipSuccess) {
+            rc = hip_fail(e, "hipSetDevice");
+            break;
+        }
+        if ((rc = scratch_alloc(&outs[i], sizeof(T), nullptr))) break;
+        rc = launch(sp.d_data, sp.nbytes, static_cast<T*>(outs[i]));
+    }
+    // Collect (and return every lease) even after a failure, each on its device.
+    for (int i = 0; i < issued; ++i) {
+        if (!outs[i]) continue;
+        if ((e = hipSetDevice(spans[i].device)) == hipSuccess) {
+            if (!rc && (e = hipMemcpy(&crcs[i], outs[i], sizeof(T), hipMemcpyDeviceToHost)) != hipSuccess)
+                rc = hip_fail(e, "hipMemcpy(span CRC)");
+            const int frc = scratch_free(outs[i], nullptr);
+            if (!rc) rc = frc;
+        } else if (!rc) {
+            rc = hip_fail(e, "hipSetDevice");
+        }
+    }
+    (void)hipSetDevice(prev);
+    if (rc) return rc;
+    T acc = seed;
+    for (int i = 0; i < nspans; ++i) acc = shift(acc, spans[i].nbytes) ^ crcs[i];
+    *h_result = acc;
+    return 0;
+}
+
+}  // namespace
+}  // namespace pcrc
+
+extern "C" {
+
+int photon_crc32c_extend_spans(const photon_crc_span* spans, int nspans, uint32_t seed, uint32_t* h_result) {
+    return extend_spans<uint32_t>(
+        spans, nspans, seed, h_result,
+        [](const void* p, uint64_t n, uint32_t* o) { return photon_crc32c_extend_device(p, n, 0, o, nullptr); },
+        [](uint32_t acc, uint64_t n) { return acc ? shift_bytes(acc, n) : 0u; });
+}
+
+int photon_crc64ecma_extend_spans(const photon_crc_span* spans, int nspans, uint64_t seed, uint64_t* h_result) {
+    return extend_spans<uint64_t>(
+        spans, nspans, seed, h_result,
+        [](const void* p, uint64_t n, uint64_t* o) { return photon_crc64ecma_extend_device(p, n, 0, o, nullptr); },
+        [](uint64_t acc, uint64_t n) { return acc ? mulmod64(acc, xpow64(8 * n)) : 0ull; });
+}
+
 int64_t photon_crc_scratch_release(void) {
     std::lock_guard<std::mutex> lk(g_scr_mu);
     return scratch_trim_locked(true);

@@ -1471,6 +1471,31 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
     }
 }
 
+// long_reduce without fences (bench-only probe, ABL 8: prices the agent-scope
+// release/acquire, buffer_wbl2 sc1 / buffer_inv sc1): the slot store and the
+// slot loads are device-scope (sc1) atomics, the store completes (vmcnt(0))
+// before the ticket is taken.
+template <typename T>
+__device__ __forceinline__ void long_reduce_nofence(T v, T* state, T* out) {
+    const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(state);
+    T* slot = reinterpret_cast<T*>(reinterpret_cast<char*>(state) + 8);
+    uint32_t last = 0;
+    if (lane == 0) {
+        __hip_atomic_store(slot + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the slot store has completed
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+    }
+    if (!__shfl(last, 0)) return;
+    T x = 0;
+    for (uint32_t w = lane; w < grid; w += 64) x ^= __hip_atomic_load(slot + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = group_xor<64>(x);
+    if (lane == 0) {
+        *out = x;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // crc * J X^m for m < 2^18 from the three power tables (xp holds J X^j).
 template <typename A>
 __device__ __forceinline__ uint32_t long_shift(uint32_t crc, uint64_t m, const A& a) {
@@ -1524,7 +1549,8 @@ __device__ __forceinline__ void long_chunk(const A& a, uint64_t t, const uint8_t
 // per-wave s_memrealtime stamps into t (8 words per wave); ABL bits = cost
 // attribution, results NOT the CRC unless noted: 1 = chunks without the
 // lead-row preload (correct), 2 = every chunk shifted on its own, no Horner
-// (correct), 4 = no final shift and no cross-workgroup reduce.
+// (correct), 4 = no final shift and no cross-workgroup reduce, 8 = the
+// reduce without release/acquire fences, 16 = no basis words (constants).
 template <int G, int U, bool STAMP = false, int ABL = 0>
 __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc, uint32_t* lds, uint32_t* red,
                                          uint64_t* t) {
@@ -1562,8 +1588,13 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
             if (first) {
                 // Once, after the first chunk (not in front of the first
                 // loads): 62 select steps and up to two multiplies per lane.
-                bw = basis_word(a.xs, l32);
-                bwk = basis_word(long_pow(tf < a.nchunks ? a.nchunks - 1 - tl : 0, a), l32);
+                if constexpr (ABL & 16) {  // probe: price of this step (results wrong)
+                    bw = a.xs ^ l32;
+                    bwk = a.xp[l32];
+                } else {
+                    bw = basis_word(a.xs, l32);
+                    bwk = basis_word(long_pow(tf < a.nchunks ? a.nchunks - 1 - tl : 0, a), l32);
+                }
                 first = false;
             }
             const uint32_t m = mul_lanes(acc, bw, l32);  // every lane: the halves stay convergent
@@ -1582,6 +1613,12 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
         if constexpr (ABL & 4) {
             if (lane == 0) *a.out = v;
+        } else if constexpr (ABL & 8) {
+            if (gridDim.x == 1) {
+                if (lane == 0) *a.out = v;
+            } else {
+                long_reduce_nofence(v, a.acc, a.out);
+            }
         } else {
             long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
         }

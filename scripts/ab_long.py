@@ -65,14 +65,20 @@ def make(v, n):
     if "@" in v:
         v, o = v.split("@")
         off = int(o)
-    elif v == "batch64k":
+    elif v in ("batch64k", "batchfold"):
         off = 0
     if v == "read":
         return lambda k: ck.read_stream(d.data_ptr(), n, sink, sink.numel(), stream=st)
-    if v == "batch64k":
+    if v in ("batch64k", "batchfold"):
         pieces = torch.zeros(n >> 16, dtype=torch.int32, device="cuda")
         cnt = (n - off) >> 16
-        return lambda k: ck.batch_strided(d.data_ptr() + off, 65536, 65536, cnt, pieces, stream=st)
+        if v == "batch64k":
+            return lambda k: ck.batch_strided(d.data_ptr() + off, 65536, 65536, cnt, pieces, stream=st)
+
+        def bf(k):  # the pieces' CRCs folded by a second launch (combine_series)
+            ck.batch_strided(d.data_ptr() + off, 65536, 65536, cnt, pieces, stream=st)
+            ck.combine_series_device(pieces, 65536, cnt, out[k:k + 1], stream=st)
+        return bf
     name, shape = v.split(":")
     if name == "probe":
         parts = [int(x) for x in shape.split("/")]

@@ -273,3 +273,31 @@ def test_extend_device_aligned_grid_edges(torch_dev, oracle, shape):
         del d
     finally:
         ck.set_long_shape(0, 0)
+
+
+def test_extend_spans_one_buffer_over_devices(torch_dev, oracle):
+    # photon_crc32c_extend_spans / photon_crc64ecma_extend_spans: ONE logical
+    # buffer cut into spans, each span on a device (round-robin over the
+    # visible devices; all on device 0 on a one-GPU box), the span CRCs folded
+    # on the host (crc.cpp:393-405). Spans: empty, 1 byte, unaligned, one over
+    # the one-workgroup limit, a full-grid one; seeds 0 and all-ones.
+    torch = torch_dev
+    ndev = torch.cuda.device_count()
+    lens = [0, 1, 4095, 12345, (256 << 10) + 3, 0, 7, 9 << 20, 64]
+    host = np.random.default_rng(0x5EED0A00).integers(0, 256, sum(lens) + 64, dtype=np.uint8)
+    keep, spans, pos = [], [], 0
+    for k, n in enumerate(lens):
+        dev = k % ndev
+        t = torch.from_numpy(host[pos:pos + n + 16].copy()).to(f"cuda:{dev}")
+        keep.append(t)
+        spans.append((dev, t.data_ptr() + (k % 3), n))  # unaligned span starts
+        host[pos:pos + n] = host[pos + (k % 3):pos + (k % 3) + n].copy()
+        pos += n
+    data = host[:pos]
+    for seed in (0, 0xFFFFFFFF, 0x1234567):
+        assert ck.extend_spans(spans, seed) == oracle.crc32c(data, seed), seed
+        s64 = seed * 0x100000001
+        assert ck.extend64_spans(spans, s64) == oracle.crc64ecma(data, s64), seed
+    assert ck.extend_spans([], 5) == 5  # no bytes: the seed
+    with pytest.raises(ck.CrcError):
+        ck.extend_spans([(0, 0, 16)], 0)  # null span with bytes
