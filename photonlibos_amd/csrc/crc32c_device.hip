@@ -1400,6 +1400,10 @@ namespace {
 template <typename T, typename Launch, typename Shift>
 int extend_spans(const photon_crc_span* spans, int nspans, T seed, T* h_result, Launch launch, Shift shift) {
     if (nspans < 0 || (nspans && !spans) || !h_result) return fail(-EINVAL, "bad span list or result");
+    if (nspans == 0) {  // the empty buffer: its CRC is the seed
+        *h_result = seed;
+        return 0;
+    }
     int prev = -1;
     hipError_t e = hipGetDevice(&prev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");

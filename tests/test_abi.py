@@ -87,6 +87,13 @@ def test_device_calls_fail_loudly_without_gpu():
     assert lib().photon_crc_stream_create(ctypes.byref(p)) < 0
     with pytest.raises(ck.CrcError):
         ck.batch_strided_shards([dict(device=0, d_base=0x1000, stride=4096, nbytes=4096, count=1, d_out=0x2000)])
+    with pytest.raises(ck.CrcError):
+        ck.extend_spans([(0, 0x1000, 4096)], 0)
+    with pytest.raises(ck.CrcError):
+        ck.extend64_spans([(0, 0x1000, 4096)], 0)
+    # no spans: nothing to read, the CRC of the empty buffer is the seed (no device needed)
+    assert ck.extend_spans([], 0x1234) == 0x1234
+    assert ck.extend64_spans([], 7) == 7
 
 
 def test_argument_validation():
