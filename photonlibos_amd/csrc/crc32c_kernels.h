@@ -1505,15 +1505,6 @@ __device__ __forceinline__ uint32_t long_shift(uint32_t crc, uint64_t m, const A
     return crc;
 }
 
-// J X^m (no leading multiply by one).
-template <typename A>
-__device__ __forceinline__ uint32_t long_pow(uint64_t m, const A& a) {
-    uint32_t k = a.xp[m & 63u];
-    if (m >= 64) k = mulmod(k, a.xq[(m >> 6) & 63u]);
-    if (m >= 4096) k = mulmod(k, a.xr[(m >> 12) & 63u]);
-    return k;
-}
-
 // v * x mod P (reflected: bit j = coefficient of x^(31-j)).
 __device__ __forceinline__ uint32_t mulx(uint32_t v) { return (v >> 1) ^ ((0u - (v & 1u)) & kPoly); }
 
@@ -1550,7 +1541,7 @@ __device__ __forceinline__ void long_chunk(const A& a, uint64_t t, const uint8_t
 // attribution, results NOT the CRC unless noted: 1 = chunks without the
 // lead-row preload (correct), 2 = every chunk shifted on its own, no Horner
 // (correct), 4 = no final shift and no cross-workgroup reduce, 8 = the
-// reduce without release/acquire fences, 16 = no basis words (constants).
+// reduce without release/acquire fences.
 template <int G, int U, bool STAMP = false, int ABL = 0>
 __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc, uint32_t* lds, uint32_t* red,
                                          uint64_t* t) {
@@ -1570,38 +1561,36 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
     const uint32_t l32 = lane & 31u;
     // The group's chunks: tf, tf + S, ..., tl (none when tf >= T).
     const uint64_t tf = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
-    const uint64_t tl = tf < a.nchunks ? tf + (a.nchunks - 1 - tf) / a.stride * a.stride : 0;
-    uint32_t bw = 0, bwk = 0;  // basis words of X^S and of the group's final factor J X^(T-1-tl)
-    uint32_t acc = 0;
-    bool first = true;
+    const uint32_t bw = (ABL & 2) ? 0u : basis_word(a.xs, l32);  // basis word of X^S
+    uint32_t acc = 0, lastc = 0;
+    uint64_t tl = 0;
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
         const uint64_t tc = wv * GPW + grp;
         const bool active = tc < a.nchunks;
         const uint8_t* p;
         uint64_t n;
         long_chunk(a, tc, &p, &n);
-        uint32_t crc = buffer_crc<G, U, (ABL & 1) ? false : PCRC_LONG_LEAD>(lds, p, n, tc ? 0u : a.seed, gl, la);
-        if (tc == a.nchunks - 1) crc = mulmod(crc, a.jinv);
+        const uint32_t crc = buffer_crc<G, U, (ABL & 1) ? false : PCRC_LONG_LEAD>(lds, p, n, tc ? 0u : a.seed, gl, la);
         if constexpr (ABL & 2) {
-            if (active) acc ^= long_shift(crc, a.nchunks - 1 - tc, a);
+            if (active) acc ^= long_shift(tc == a.nchunks - 1 ? mulmod(crc, a.jinv) : crc, a.nchunks - 1 - tc, a);
         } else {
-            if (first) {
-                // Once, after the first chunk (not in front of the first
-                // loads): 62 select steps and up to two multiplies per lane.
-                if constexpr (ABL & 16) {  // probe: price of this step (results wrong)
-                    bw = a.xs ^ l32;
-                    bwk = a.xp[l32];
-                } else {
-                    bw = basis_word(a.xs, l32);
-                    bwk = basis_word(long_pow(tf < a.nchunks ? a.nchunks - 1 - tl : 0, a), l32);
-                }
-                first = false;
-            }
+            // The last chunk (always its group's last) is kept out of the
+            // fold: (acc X^S ^ crc jinv) J = acc X^S J ^ crc, so it needs no
+            // multiply (a general GF(2) multiply here, 32 unrolled steps,
+            // made the compiler reduce the row loop's blocks one at a time:
+            // 32 waits per 4 rows instead of 22).
+            const bool last = tc == a.nchunks - 1;
             const uint32_t m = mul_lanes(acc, bw, l32);  // every lane: the halves stay convergent
-            if (active) acc = m ^ crc;
+            if (active) {
+                acc = last ? m : m ^ crc;
+                lastc = last ? crc : lastc;
+                tl = tc;
+            }
         }
     }
-    if constexpr (!(ABL & 6)) acc = mul_lanes(acc, bwk, l32);  // acc = 0 for a group without chunks
+    (void)tf;
+    // acc * J X^(T-1-tl) (three table multiplies, once per group), then the last chunk.
+    if constexpr (!(ABL & 6)) acc = long_shift(acc, a.nchunks - 1 - tl, a) ^ lastc;
     uint64_t t_body = 0;
     if constexpr (STAMP) t_body = __builtin_amdgcn_s_memrealtime();
     acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their values

@@ -704,7 +704,7 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
     const uint32_t l = G == 64 ? lane : (lane & 31u);
     const uint64_t t0 = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
     const uint64_t tl = t0 < a.nchunks ? t0 + (a.nchunks - 1 - t0) / a.stride * a.stride : 0;
-    uint64_t bw0 = 0, bw1 = 0, bk0 = 0, bk1 = 0;
+    uint64_t bw0 = 0, bw1 = 0, bk0 = 0, bk1 = 0, lastc = 0;
     bool first = true;
     auto mul_basis_lanes = [&](uint64_t v, uint64_t b0, uint64_t b1) {
         uint64_t term = ((v >> l) & 1ull) ? b0 : 0ull;
@@ -720,7 +720,6 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
         long_chunk(a, t, &p, &n);
         uint64_t reg = buffer_reg64<G>(lds, p, n, t ? 0ull : ~a.seed, gl, lane, la);  // valid on gl == 0
         reg = __shfl(reg, lane & ~(uint32_t)(G - 1), 64);                        // the whole group
-        if (t == a.nchunks - 1) reg = mulmod64(reg, a.jinv);
         if (first) {
             const uint64_t m = t0 < a.nchunks ? a.nchunks - 1 - tl : 0;
             uint64_t k = a.xp[m & 63u];
@@ -734,10 +733,15 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
             }
             first = false;
         }
+        // the last chunk after the group's factor (J x^(8(chunk-L)) = 1; long_run)
+        const bool last = t == a.nchunks - 1;
         const uint64_t m = mul_basis_lanes(acc, bw0, bw1);
-        if (active) acc = m ^ reg;
+        if (active) {
+            acc = last ? m : m ^ reg;
+            lastc = last ? reg : lastc;
+        }
     }
-    acc = mul_basis_lanes(acc, bk0, bk1);
+    acc = mul_basis_lanes(acc, bk0, bk1) ^ lastc;
     acc = xor_lanes64(gl == 0 ? acc : 0ull, 64);
     if (lane == 0) red[wave] = acc;
     __syncthreads();
