@@ -1541,7 +1541,8 @@ __device__ __forceinline__ void long_chunk(const A& a, uint64_t t, const uint8_t
 // attribution, results NOT the CRC unless noted: 1 = chunks without the
 // lead-row preload (correct), 2 = every chunk shifted on its own, no Horner
 // (correct), 4 = no final shift and no cross-workgroup reduce, 8 = the
-// reduce without release/acquire fences.
+// reduce without release/acquire fences, 16 = no cross-workgroup reduce
+// (the final shift kept), 32 = no final shift (the reduce kept).
 template <int G, int U, bool STAMP = false, int ABL = 0>
 __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc, uint32_t* lds, uint32_t* red,
                                          uint64_t* t) {
@@ -1590,7 +1591,7 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
     }
     (void)tf;
     // acc * J X^(T-1-tl) (three table multiplies, once per group), then the last chunk.
-    if constexpr (!(ABL & 6)) acc = long_shift(acc, a.nchunks - 1 - tl, a) ^ lastc;
+    if constexpr (!(ABL & 6) && !(ABL & 32)) acc = long_shift(acc, a.nchunks - 1 - tl, a) ^ lastc;
     uint64_t t_body = 0;
     if constexpr (STAMP) t_body = __builtin_amdgcn_s_memrealtime();
     acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their values
@@ -1600,7 +1601,7 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
         uint32_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        if constexpr (ABL & 4) {
+        if constexpr (ABL & 20) {
             if (lane == 0) *a.out = v;
         } else if constexpr (ABL & 8) {
             if (gridDim.x == 1) {

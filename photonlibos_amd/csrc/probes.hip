@@ -449,7 +449,7 @@ int probe_read_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t c
 // * kLongMaxGrid bytes, the first 8 zero (left zero); t = 8 words per wave of
 // grid * 16 waves; *grid_out = the grid. force_chunk: a chunk size (a 1 KiB
 // multiple) instead of the plan's (0 = the plan's). rounds | ablation << 8
-// (long_run's ABL bits: 0..5, 8).
+// (long_run's ABL bits: 0..5, 8, 16, 32).
 int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* out, uint32_t* state, uint64_t* t,
                        int cus, int lanes, int rounds, uint64_t force_chunk, int* grid_out, void* stream) {
     using namespace pcrc;
@@ -488,6 +488,8 @@ int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* ou
         case 4: LSG(4); break;
         case 5: LSG(5); break;
         case 8: LSG(8); break;
+        case 16: LSG(16); break;
+        case 32: LSG(32); break;
         default: LSG(0); break;
     }
 #undef LSG
