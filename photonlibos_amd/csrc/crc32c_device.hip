@@ -39,6 +39,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -712,6 +714,50 @@ LongPlan long_plan(const void* data, uint64_t n, int cus) {
     return long_plan_for(data, n, cus, g_long_shape.load(std::memory_order_relaxed));
 }
 
+// long_reduce's state (ticket + slots) for a long-buffer launch on `st`: ONE
+// zeroed buffer per (device, stream) -- per thread for hipStreamPerThread --
+// kept for the life of the process. Launches on one stream run in order and
+// each leaves the ticket at 0, so the buffer needs no lease and no event: the
+// scratch lease's hipEventRecord after every launch put a marker packet
+// between back-to-back launches and cost 6 µs per 1 GiB call
+// (scripts/ab_long.py probe+ev). A stream handle is reused only after the
+// stream's work has completed. *lease = true: a leased scratch buffer
+// instead (more than 4096 streams seen), to be returned with scratch_free.
+std::mutex g_ls_mu;
+std::map<std::tuple<int, uintptr_t, std::thread::id>, void*> g_long_state;
+
+int long_state(hipStream_t st, void** p, bool* lease) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    const auto key = std::make_tuple(dev, reinterpret_cast<uintptr_t>(st),
+                                     st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id());
+    *lease = false;
+    {
+        std::lock_guard<std::mutex> lk(g_ls_mu);
+        auto it = g_long_state.find(key);
+        if (it != g_long_state.end()) {
+            *p = it->second;
+            return 0;
+        }
+        if (g_long_state.size() >= 4096) {
+            *lease = true;
+            return scratch_alloc(p, 8 + 8 * kLongMaxGrid, st, true);
+        }
+    }
+    void* b = nullptr;
+    if ((e = hipMalloc(&b, 8 + 8 * kLongMaxGrid)) != hipSuccess) return hip_fail(e, "hipMalloc(long state)");
+    if ((e = hipMemset(b, 0, 8 + 8 * kLongMaxGrid)) != hipSuccess) {
+        (void)hipFree(b);
+        return hip_fail(e, "hipMemset(long state)");
+    }
+    std::lock_guard<std::mutex> lk(g_ls_mu);
+    auto ins = g_long_state.emplace(key, b);
+    if (!ins.second) (void)hipFree(b);  // another thread registered this stream first
+    *p = ins.first->second;
+    return 0;
+}
+
 }  // namespace
 
 // For the other translation units of the library (internal.h).
@@ -1264,8 +1310,9 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     memcpy(a.xq, pw.p64[1], sizeof(a.xq));
     memcpy(a.xr, pw.p64[2], sizeof(a.xr));
     void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
+    bool leased = false;
     if (lp.grid > 1) {
-        if (int rc = scratch_alloc(&state, 8 + 8 * kLongMaxGrid, st, true)) return rc;
+        if (int rc = long_state(st, &state, &leased)) return rc;
         a.acc = static_cast<uint64_t*>(state);
     }
     if (lp.lanes == 32)
@@ -1274,7 +1321,7 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
         hipLaunchKernelGGL((crc64_long_kernel<64>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(64));
     const hipError_t e = hipGetLastError();
     int rc = e == hipSuccess ? 0 : hip_fail(e, "crc64_long_kernel launch");
-    if (state) {
+    if (leased) {
         const int frc = scratch_free(state, st);
         if (!rc) rc = frc;
     }
@@ -1372,8 +1419,9 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     memcpy(a.xq, pw.p32[1], sizeof(a.xq));
     memcpy(a.xr, pw.p32[2], sizeof(a.xr));
     void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
+    bool leased = false;
     if (lp.grid > 1) {
-        if (int rc = scratch_alloc(&state, 8 + 8 * kLongMaxGrid, st, true)) return rc;
+        if (int rc = long_state(st, &state, &leased)) return rc;
         a.acc = static_cast<uint32_t*>(state);
     }
     if (lp.lanes == 32)
@@ -1382,7 +1430,7 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
         hipLaunchKernelGGL((crc32c_long_kernel<64, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(64));
     const hipError_t e = hipGetLastError();
     int rc = e == hipSuccess ? 0 : hip_fail(e, "crc32c_long_kernel launch");
-    if (state) {
+    if (leased) {
         const int frc = scratch_free(state, st);
         if (!rc) rc = frc;
     }

@@ -1430,17 +1430,26 @@ struct LongArgs {
 
 // The long kernels' cross-workgroup XOR, called by EVERY thread of wave 0
 // with its workgroup's value v (valid on lane 0): lane 0 stores v into the
-// workgroup's slot and takes a ticket (release: the slot is visible first);
-// the workgroup that takes the last ticket (acquire) loads all slots at
-// once, XORs them, writes fin(total) and puts the ticket back to 0 for the
-// next lease. Two dependent round trips at the end of the launch (slot
-// store + ticket, slot loads); the round-3 first form -- device-scope
-// atomicXor into one accumulator, or into eight with a second level -- was
-// a chain of 4-7 dependent atomics with fences, 8 µs after the last chunk
-// (scripts/probe_long_times.py). state: ticket, then kLongMaxGrid slots
-// (8 + 8 * kLongMaxGrid bytes).
+// workgroup's slot and takes a ticket; the workgroup that takes the last
+// ticket loads all slots at once, XORs them, writes fin(total) and puts the
+// ticket back to 0 for the next lease. state: ticket, then kLongMaxGrid
+// slots (8 + 8 * kLongMaxGrid bytes).
+//
+// Ordering without fences: every access to the state is a device-scope
+// (agent) atomic -- the slot store and the slot loads are `sc1` accesses,
+// coherent across the XCDs' separate L2s by themselves -- and the slot store
+// has completed (s_waitcnt vmcnt(0)) before the ticket is taken; the last
+// workgroup issues its slot loads only after its ticket returned. This is
+// the LLVM AMDGPU memory model's mapping of monotonic agent-scope atomics on
+// gfx942/gfx950; an acquire/release pair is only needed to order plain
+// (non-atomic) accesses, and at agent scope it costs a `buffer_wbl2 sc1`
+// (write back the XCD's L2) plus `buffer_inv sc1`. FENCED (bench probe,
+// ABL 8) keeps that pair: 5.7 µs more per 1 GiB launch
+// (repo:profiles/r03b_ab_long_tail_ablations.jsonl). Round 3's first form,
+// device-scope atomicXor into one accumulator or eight with a second level,
+// was a chain of 4-7 dependent atomics with fences (8 µs after the last chunk).
 constexpr uint32_t kLongMaxGrid = 512;
-template <typename T, typename F>
+template <typename T, typename F, bool FENCED = false>
 __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
     const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
     if (grid == 1) {
@@ -1454,11 +1463,19 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
     T* slot = reinterpret_cast<T*>(reinterpret_cast<char*>(state) + 8);
     uint32_t last = 0;
     if (lane == 0) {
-        slot[blockIdx.x] = v;
-        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+        if constexpr (FENCED) {
+            slot[blockIdx.x] = v;
+            last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+        } else {
+            __hip_atomic_store(slot + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler order only
+            __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): the slot store has completed
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+        }
     }
     if (!__shfl(last, 0)) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if constexpr (FENCED) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     T x = 0;
     for (uint32_t w = lane; w < grid; w += 64) x ^= __hip_atomic_load(slot + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (sizeof(T) == 8)
@@ -1467,31 +1484,6 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
         x = group_xor<64>(x);
     if (lane == 0) {
         *out = fin(x);
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// long_reduce without fences (bench-only probe, ABL 8: prices the agent-scope
-// release/acquire, buffer_wbl2 sc1 / buffer_inv sc1): the slot store and the
-// slot loads are device-scope (sc1) atomics, the store completes (vmcnt(0))
-// before the ticket is taken.
-template <typename T>
-__device__ __forceinline__ void long_reduce_nofence(T v, T* state, T* out) {
-    const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(state);
-    T* slot = reinterpret_cast<T*>(reinterpret_cast<char*>(state) + 8);
-    uint32_t last = 0;
-    if (lane == 0) {
-        __hip_atomic_store(slot + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the slot store has completed
-        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
-    }
-    if (!__shfl(last, 0)) return;
-    T x = 0;
-    for (uint32_t w = lane; w < grid; w += 64) x ^= __hip_atomic_load(slot + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    x = group_xor<64>(x);
-    if (lane == 0) {
-        *out = x;
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -1541,8 +1533,9 @@ __device__ __forceinline__ void long_chunk(const A& a, uint64_t t, const uint8_t
 // attribution, results NOT the CRC unless noted: 1 = chunks without the
 // lead-row preload (correct), 2 = every chunk shifted on its own, no Horner
 // (correct), 4 = no final shift and no cross-workgroup reduce, 8 = the
-// reduce without release/acquire fences, 16 = no cross-workgroup reduce
-// (the final shift kept), 32 = no final shift (the reduce kept).
+// reduce WITH the agent-scope release/acquire (correct), 16 = no
+// cross-workgroup reduce (the final shift kept), 32 = no final shift (the
+// reduce kept).
 template <int G, int U, bool STAMP = false, int ABL = 0>
 __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc, uint32_t* lds, uint32_t* red,
                                          uint64_t* t) {
@@ -1604,11 +1597,7 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
         if constexpr (ABL & 20) {
             if (lane == 0) *a.out = v;
         } else if constexpr (ABL & 8) {
-            if (gridDim.x == 1) {
-                if (lane == 0) *a.out = v;
-            } else {
-                long_reduce_nofence(v, a.acc, a.out);
-            }
+            long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(v, a.acc, a.out, [](uint32_t x) { return x; });
         } else {
             long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
         }

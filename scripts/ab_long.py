@@ -80,7 +80,10 @@ def make(v, n):
             ck.combine_series_device(pieces, 65536, cnt, out[k:k + 1], stream=st)
         return bf
     name, shape = v.split(":")
-    if name == "probe":
+    if name in ("probe", "probe+ev"):
+        # probe+ev: the same launch followed by a (timing-disabled) event
+        # record on the stream, as the product's scratch lease does per call
+        xev = torch.cuda.Event(enable_timing=False) if name == "probe+ev" else None
         parts = [int(x) for x in shape.split("/")]
         lanes, rounds, ckib = parts[:3]
         rounds |= (parts[3] if len(parts) > 3 else 0) << 8  # long_run ablation bits
@@ -90,6 +93,8 @@ def make(v, n):
                                       pstamps.data_ptr(), cus, lanes, rounds, ckib * 1024, ctypes.byref(pgrid),
                                       ctypes.c_void_p(st.cuda_stream))
             assert rc == 0, (v, rc)
+            if xev is not None:
+                xev.record(st)
         return fp
     lanes, rounds = (int(x) for x in shape.split("/"))
     lib = libs[name]
