@@ -1417,7 +1417,8 @@ struct LongArgs {
     uint64_t chunk;
     uint64_t nchunks;   // T
     uint32_t seed;
-    uint32_t jinv;      // x^(8 (chunk - L_last)), applied to the last chunk's CRC (kOne when T == 1)
+    uint32_t jinv;      // x^(8 (chunk - L_last)) (kOne when T == 1); J jinv = 1, so the kernel folds the
+                        // last chunk in after its group's factor instead (probe ablation 2 multiplies)
     uint32_t xs;        // X^S
     uint64_t stride;    // S: lane groups in the grid
     uint32_t* out;
