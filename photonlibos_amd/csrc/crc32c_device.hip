@@ -1309,6 +1309,7 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     memcpy(a.xp, pw.xpj64, sizeof(a.xp));
     memcpy(a.xq, pw.p64[1], sizeof(a.xq));
     memcpy(a.xr, pw.p64[2], sizeof(a.xr));
+    memcpy(a.xsb, pw.xsb64, sizeof(a.xsb));
     void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
     bool leased = false;
     if (lp.grid > 1) {

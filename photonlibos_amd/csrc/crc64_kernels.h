@@ -670,6 +670,7 @@ struct Long64Args {
     uint64_t xp[64];    // J X^j, X = x^(8*chunk) mod P64
     uint64_t xq[64];    // X^(64 j)
     uint64_t xr[64];    // X^(4096 j)
+    uint64_t xsb[64];   // basis words of X^S: (1 << i) * X^S (host-computed, long_powers)
 };
 
 __device__ __forceinline__ uint64_t mulx64(uint64_t v) { return (v >> 1) ^ ((0ull - (v & 1ull)) & kPoly64); }
@@ -698,20 +699,18 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
     const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr64 la = lane_addr64(lane);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-    // Basis words of X^S and of the group's final factor J X^(T-1-tl): 64
-    // lanes one each (G = 64), or two per lane of a 32-lane half (bits l and
-    // l + 32); computed after the group's first chunk.
+    // Basis words of X^S from the host: 64 lanes one each (G = 64), or two
+    // per lane of a 32-lane half (bits l and l + 32). Nothing but the chunk
+    // loop's own work sits in the loop (crc32c_kernels.h long_run: any
+    // general multiply there serialises the row loop's lookups).
     const uint32_t l = G == 64 ? lane : (lane & 31u);
-    const uint64_t t0 = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
-    const uint64_t tl = t0 < a.nchunks ? t0 + (a.nchunks - 1 - t0) / a.stride * a.stride : 0;
-    uint64_t bw0 = 0, bw1 = 0, bk0 = 0, bk1 = 0, lastc = 0;
-    bool first = true;
-    auto mul_basis_lanes = [&](uint64_t v, uint64_t b0, uint64_t b1) {
-        uint64_t term = ((v >> l) & 1ull) ? b0 : 0ull;
-        if (G != 64) term ^= ((v >> (l + 32)) & 1ull) ? b1 : 0ull;
+    const uint64_t bw0 = a.xsb[l], bw1 = G == 64 ? 0ull : a.xsb[l + 32];
+    auto mul_basis_lanes = [&](uint64_t v) {
+        uint64_t term = ((v >> l) & 1ull) ? bw0 : 0ull;
+        if (G != 64) term ^= ((v >> (l + 32)) & 1ull) ? bw1 : 0ull;
         return xor_lanes64(term, G == 64 ? 64 : 32);
     };
-    uint64_t acc = 0;
+    uint64_t acc = 0, lastc = 0;  // uniform across the group (reg and the lane XOR are)
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
         const uint64_t t = wv * GPW + grp;
         const bool active = t < a.nchunks;
@@ -720,28 +719,24 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
         long_chunk(a, t, &p, &n);
         uint64_t reg = buffer_reg64<G>(lds, p, n, t ? 0ull : ~a.seed, gl, lane, la);  // valid on gl == 0
         reg = __shfl(reg, lane & ~(uint32_t)(G - 1), 64);                        // the whole group
-        if (first) {
-            const uint64_t m = t0 < a.nchunks ? a.nchunks - 1 - tl : 0;
-            uint64_t k = a.xp[m & 63u];
-            if (m >= 64) k = mulmod64(k, a.xq[(m >> 6) & 63u]);
-            if (m >= 4096) k = mulmod64(k, a.xr[(m >> 12) & 63u]);
-            bw0 = basis_word64(a.xs, l);
-            bk0 = basis_word64(k, l);
-            if (G != 64) {
-                bw1 = basis_word64(a.xs, l + 32);
-                bk1 = basis_word64(k, l + 32);
-            }
-            first = false;
-        }
         // the last chunk after the group's factor (J x^(8(chunk-L)) = 1; long_run)
         const bool last = t == a.nchunks - 1;
-        const uint64_t m = mul_basis_lanes(acc, bw0, bw1);
+        const uint64_t m = mul_basis_lanes(acc);
         if (active) {
             acc = last ? m : m ^ reg;
             lastc = last ? reg : lastc;
         }
     }
-    acc = mul_basis_lanes(acc, bk0, bk1) ^ lastc;
+    // The group's final factor J X^(T-1-tl) (tl its last chunk), applied to the
+    // group-uniform accumulator with bit-serial multiplies after the loop.
+    const uint64_t t0 = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
+    if (t0 < a.nchunks) {
+        const uint64_t m = (a.nchunks - 1 - t0) % a.stride;  // T-1-tl
+        uint64_t k = a.xp[m & 63u];
+        if (m >= 64) k = mulmod64(k, a.xq[(m >> 6) & 63u]);
+        if (m >= 4096) k = mulmod64(k, a.xr[(m >> 12) & 63u]);
+        acc = mulmod64(acc, k) ^ lastc;
+    }
     acc = xor_lanes64(gl == 0 ? acc : 0ull, 64);
     if (lane == 0) red[wave] = acc;
     __syncthreads();

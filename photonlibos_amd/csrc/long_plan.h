@@ -73,6 +73,7 @@ struct LongPowers {
     uint64_t xpj64[64];
     uint32_t xs32, j32, jinv32;
     uint64_t xs64, j64, jinv64;
+    uint64_t xsb64[64];  // (1 << i) * X^S mod P64: crc64_long_kernel's lane basis words
 };
 
 inline const LongPowers& long_powers(const LongPlan& lp, bool crc64) {
@@ -106,6 +107,7 @@ inline const LongPowers& long_powers(const LongPlan& lp, bool crc64) {
         t->jinv64 = xpow64(pad);
         t->j64 = xpow64_inv(pad);
         for (int j = 0; j < 64; ++j) t->xpj64[j] = mulmod64(t->p64[0][j], t->j64);
+        for (int i = 0; i < 64; ++i) t->xsb64[i] = mulmod64(1ull << i, t->xs64);
     } else {
         t->xs32 = mulmod(mulmod(t->p32[0][s & 63], t->p32[1][(s >> 6) & 63]), t->p32[2][(s >> 12) & 63]);
         t->jinv32 = xpow(pad);

@@ -8,7 +8,9 @@ Bench-only.
   LIBS      name=path,... of libphoton_checksum.so builds (default: new = in-tree)
   VARIANTS  name:lanes/rounds,... (0/0 = automatic); probe:lanes/rounds/chunk_kib[/abl]
             (the stamped probe build of the same long_run, libphoton_probes.so,
-            with that chunk size forced; 0 = the plan's); plus "batch64k" (the
+            with that chunk size forced; 0 = the plan's); "c64" (CRC-64/ECMA,
+            photon_crc64ecma_extend_device, automatic shape) and "b64k64" (the
+            CRC-64 batch kernel over the same bytes as 64 KiB pieces); "batch64k" (the
             strided batch kernel over the same bytes as 64 KiB pieces from an
             aligned base) and "read" (the read-only grid-stride stream)
   SIZES_MIB buffer sizes (at base+1, test_checksum.cpp:125-168)
@@ -52,6 +54,7 @@ big = max(SIZES)
 d = torch.empty(big + 4096, dtype=torch.uint8, device="cuda")
 ck.fill_splitmix(d, big + 4096, big + 4096, 1, 0x5EED0B00, stream=st)
 out = torch.zeros(N, dtype=torch.int32, device="cuda")
+out64 = torch.zeros(N, dtype=torch.int64, device="cuda")
 pstate = torch.zeros(1024, dtype=torch.int32, device="cuda")
 pstamps = torch.zeros(8 * 16 * cus, dtype=torch.int64, device="cuda")
 pgrid = ctypes.c_int(0)
@@ -65,8 +68,32 @@ def make(v, n):
     if "@" in v:
         v, o = v.split("@")
         off = int(o)
-    elif v in ("batch64k", "batchfold"):
+    elif v in ("batch64k", "batchfold", "b64k64"):
         off = 0
+    if v == "c64" or v.startswith("c64:"):  # c64[:lanes/rounds]
+        lanes, rounds = (int(x) for x in v.split(":")[1].split("/")) if ":" in v else (0, 0)
+        lib = next(iter(libs.values()))
+
+        def fc64(k):
+            lib.photon_crc_set_long_shape(lanes, rounds)
+            ck.extend64_device(d.data_ptr() + off, n, out64[k:k + 1], seed=7, stream=st)
+        return fc64
+    if v.startswith("c64="):  # c64=<library path>: another build's CRC-64 extend_device
+        # (same kernel names in two loaded builds: only builds with the same
+        # kernel argument layout compare reliably)
+        path = v.split("=", 1)[1]
+        l64 = ctypes.CDLL(path if os.path.isabs(path) else os.path.join(REPO, path), mode=ctypes.RTLD_LOCAL)
+        l64.photon_crc64ecma_extend_device.argtypes = [vp, u64, ctypes.c_uint64, vp, vp]
+        l64.photon_crc64ecma_extend_device.restype = ci
+
+        def f64(k):
+            rc = l64.photon_crc64ecma_extend_device(d.data_ptr() + off, n, 7, out64.data_ptr() + 8 * k,
+                                                    ctypes.c_void_p(st.cuda_stream))
+            assert rc == 0, (v, rc)
+        return f64
+    if v == "b64k64":
+        pieces64 = torch.zeros(n >> 16, dtype=torch.int64, device="cuda")
+        return lambda k: ck.batch64_strided(d.data_ptr() + off, 65536, 65536, (n - off) >> 16, pieces64, stream=st)
     if v == "read":
         return lambda k: ck.read_stream(d.data_ptr(), n, sink, sink.numel(), stream=st)
     if v in ("batch64k", "batchfold"):
@@ -111,6 +138,7 @@ for n in SIZES:
     fns = {v: make(v, n) for v in VARIANTS}
     times = {v: [] for v in VARIANTS}
     crcs = {}
+    c64 = {}
     for r in range(ROUNDS):
         for v in (VARIANTS if r % 2 == 0 else VARIANTS[::-1]):
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(N)]
@@ -120,8 +148,10 @@ for n in SIZES:
                 ev[k][1].record(st)
             torch.cuda.synchronize()
             times[v] += [a.elapsed_time(b) for a, b in ev]
-            if ":" in v and "@" not in v:
+            if ":" in v and "@" not in v and not v.startswith("c64"):
                 crcs.setdefault(v, set()).update(int(x) & 0xFFFFFFFF for x in out.cpu().numpy())
+            if v.startswith("c64"):
+                c64.setdefault(v, set()).update(int(x) & 0xFFFFFFFFFFFFFFFF for x in out64.cpu().numpy())
     for lib in libs.values():
         lib.photon_crc_set_long_shape(0, 0)
     ref = None
@@ -129,6 +159,8 @@ for n in SIZES:
         t = np.array(times[v])
         row = {"n": n, "variant": v, "ms_mean": round(float(t.mean()), 4), "ms_median": round(float(np.median(t)), 4),
                "frac": round(n / float(t.mean()) / 8e9, 4), "launches": len(t)}
+        if v in c64:
+            row["same_crc"] = len(c64[v]) == 1 and c64[v] == next(iter(c64.values()))
         if v in crcs:
             ref = crcs[v] if ref is None else ref
             row["same_crc"] = len(crcs[v]) == 1 and crcs[v] == ref
