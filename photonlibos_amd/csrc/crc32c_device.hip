@@ -710,8 +710,8 @@ int pipe_init(HostPipe& p) {
 // Lane groups and rounds: tuning.h photon_crc_set_long_shape.
 std::atomic<uint32_t> g_long_shape{0};  // lanes | rounds << 8; 0 = automatic
 
-LongPlan long_plan(const void* data, uint64_t n, int cus) {
-    return long_plan_for(data, n, cus, g_long_shape.load(std::memory_order_relaxed));
+LongPlan long_plan(const void* data, uint64_t n, int cus, bool crc64) {
+    return long_plan_for(data, n, cus, g_long_shape.load(std::memory_order_relaxed), 0, crc64);
 }
 
 // long_reduce's state (ticket + slots) for a long-buffer launch on `st`: ONE
@@ -1293,7 +1293,7 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const LongPlan lp = long_plan(d_data, nbytes, cus);
+    const LongPlan lp = long_plan(d_data, nbytes, cus, true);
     const LongPowers& pw = long_powers(lp, true);
     Long64Args a{};
     a.data = static_cast<const uint8_t*>(d_data);
@@ -1403,7 +1403,7 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const LongPlan lp = long_plan(d_data, nbytes, cus);
+    const LongPlan lp = long_plan(d_data, nbytes, cus, false);
     const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
     a.data = static_cast<const uint8_t*>(d_data);

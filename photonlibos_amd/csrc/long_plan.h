@@ -21,14 +21,18 @@ struct LongPlan {
 };
 
 // force_chunk (bench-only probes): that chunk size instead of the computed one.
-inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t shape, uint64_t force_chunk = 0) {
+inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t shape, uint64_t force_chunk = 0,
+                              bool crc64 = false) {
     const bool small = n <= (256u << 10);
-    // automatic: 2 rounds; 64 lanes, 32 from 512 MiB (r03 interleaved A/B,
-    // scripts/ab_long.py: 1 GiB 32x2 0.177 ms vs 64x1 0.184 / 64x2 0.196;
-    // 256 MiB 64x2 0.060 vs 32x2 0.060 / 64x1 0.065)
+    // automatic (r03 interleaved A/B, scripts/ab_long.py):
+    //  CRC-32C: 2 rounds; 64 lanes, 32 from 512 MiB (1 GiB 32x2 0.177 ms vs
+    //    64x1 0.184 / 64x2 0.196; 256 MiB 64x2 0.060 vs 32x2 0.060 / 64x1 0.065)
+    //  CRC-64: 64 lanes; 1 round from 1 GiB, else 2 (1 GiB 64x1 0.176 vs 32x2
+    //    0.180 / 64x2 0.188; 2 GiB 0.331 / 0.372 / 0.336; 512 MiB 64x2 0.100
+    //    vs 0.109 / 0.111; profiles/r03e_ab_long_crc64_*.jsonl)
     const bool huge = n >= (512ull << 20);
-    const int lanes = small ? 64 : (shape & 0xff) ? (int)(shape & 0xff) : huge ? 32 : 64;
-    const uint64_t rounds = small ? 1 : (shape >> 8) ? shape >> 8 : 2;
+    const int lanes = small ? 64 : (shape & 0xff) ? (int)(shape & 0xff) : (huge && !crc64) ? 32 : 64;
+    const uint64_t rounds = small ? 1 : (shape >> 8) ? shape >> 8 : (crc64 && n >= (1ull << 30)) ? 1 : 2;
     const uint64_t gpw = 64 / (uint64_t)lanes;
     const uint64_t slots = small ? 16 : 16ull * (uint64_t)cus * gpw * rounds;
     LongPlan p{};
