@@ -25,14 +25,17 @@ inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t sh
                               bool crc64 = false) {
     const bool small = n <= (256u << 10);
     // automatic (r03 interleaved A/B, scripts/ab_long.py):
-    //  CRC-32C: 2 rounds; 64 lanes, 32 from 512 MiB (1 GiB 32x2 0.177 ms vs
-    //    64x1 0.184 / 64x2 0.196; 256 MiB 64x2 0.060 vs 32x2 0.060 / 64x1 0.065)
+    //  CRC-32C: 64 lanes x 2 rounds; 32 x 2 from 512 MiB (1 GiB 32x2 0.177 ms
+    //    vs 64x1 0.184 / 64x2 0.196; 256 MiB 64x2 0.060 vs 32x2 0.060 / 64x1
+    //    0.065); 64 x 1 from 1.5 GiB (2 GiB 0.326 vs 32x2 0.367, 4 GiB 0.633
+    //    vs 0.650; chunks near 128 KiB read slowly, profiles/r03e_ab_long_crc32c_big.jsonl)
     //  CRC-64: 64 lanes; 1 round from 1 GiB, else 2 (1 GiB 64x1 0.176 vs 32x2
     //    0.180 / 64x2 0.188; 2 GiB 0.331 / 0.372 / 0.336; 512 MiB 64x2 0.100
     //    vs 0.109 / 0.111; profiles/r03e_ab_long_crc64_*.jsonl)
-    const bool huge = n >= (512ull << 20);
-    const int lanes = small ? 64 : (shape & 0xff) ? (int)(shape & 0xff) : (huge && !crc64) ? 32 : 64;
-    const uint64_t rounds = small ? 1 : (shape >> 8) ? shape >> 8 : (crc64 && n >= (1ull << 30)) ? 1 : 2;
+    const bool huge = n >= (512ull << 20), giant = n >= (3ull << 29);
+    const int lanes = small ? 64 : (shape & 0xff) ? (int)(shape & 0xff) : (huge && !giant && !crc64) ? 32 : 64;
+    const uint64_t one = crc64 ? n >= (1ull << 30) : giant;
+    const uint64_t rounds = small ? 1 : (shape >> 8) ? shape >> 8 : one ? 1 : 2;
     const uint64_t gpw = 64 / (uint64_t)lanes;
     const uint64_t slots = small ? 16 : 16ull * (uint64_t)cus * gpw * rounds;
     LongPlan p{};
