@@ -5,9 +5,11 @@ MI355X through the C-ABI engine (libphoton_checksum.so).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|...]
 
 One "step" = one pass of the hot path over one batch (BASELINE.json configs):
-  c2 (default at N=1, configs[1]): 65,536 x 64 KiB random buffers, device-resident
-  c4 (default at N>1, configs[3]): 32,768 x 1 MiB per GPU = the 256 Ki x 1 MiB
-      batch sharded over 8 GPUs (weak scaling: the per-GPU shard is fixed)
+  c2 (the default at EVERY N, configs[1]): 65,536 x 64 KiB random buffers,
+      device-resident, per GPU (weak scaling: N GPUs checksum N such batches,
+      so the driver's 1/2/4/8-GPU lines compare like with like)
+  c4 (configs[3]): 32,768 x 1 MiB per GPU = the 256 Ki x 1 MiB batch sharded
+      over 8 GPUs (`--config c4 --gpus 8`)
   c3: 1,048,576 x 4 KiB        c5: 65,536 messages x 8 non-contiguous 8 KiB
       segments, per-segment CRC + crc32c_combine fold (BASELINE.json configs[4])
   c5_chain: the C5 shape, one CRC per message chained through the seed
@@ -77,8 +79,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=25)
-    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                    help="default: c2 at --gpus 1, c4 (the 8-GPU config's shard) at --gpus > 1")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="default c2 per GPU at every --gpus N (one workload for the whole scaling sweep)")
     ap.add_argument("--share-gpus", action="store_true",
                     help="rehearsal: allow more ranks than visible GPUs (round-robin); marked in the output")
     ap.add_argument("--cpu-rehearsal", action="store_true",
@@ -100,10 +102,7 @@ def parse(argv=None):
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (profiles/*.json) giving HBM bytes per launch (fallback when no live pass)")
-    args = ap.parse_args(argv)
-    if args.config is None:
-        args.config = "c4" if args.gpus > 1 else "c2"
-    return args
+    return ap.parse_args(argv)
 
 
 # ------------------------------------------------------------------ launcher
@@ -689,7 +688,10 @@ def run_file_records(args):
 def run_cpu_rehearsal(args, rank, world, dist):
     """The N-rank launcher, timed region and report with no GPU: every rank
     checksums its own shard of 64 x 64 KiB host buffers through this library's
-    crc32c() drop-in (the C-ABI library's host engine). For the CPU tests."""
+    crc32c() drop-in (the C-ABI library's host engine). For the CPU tests.
+    `config` names the GPU workload this --gpus N / --config would run (the
+    same at every N, so a scaling sweep compares like with like); the host
+    step itself is `rehearsal_step`."""
     from photonlibos_amd import datagen
     n, cnt = 65536, 64
     bufs = [datagen.stream_bytes(shard_seed_base(rank, cnt) + i, n).tobytes() for i in range(cnt)]
@@ -713,8 +715,9 @@ def run_cpu_rehearsal(args, rank, world, dist):
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "scaling": "weak",
                           "rehearsal": "cpu", "per_rank": ranks,
-                          "config": {"workload": f"{cnt} x {n} B host buffers per rank, crc32c() drop-in",
-                                     "parallelism": f"shard-per-rank x{world}"}}), flush=True)
+                          "rehearsal_step": f"{cnt} x {n} B host buffers per rank, crc32c() drop-in",
+                          "config": {"workload": CONFIGS[args.config]["workload"], "config": args.config,
+                                     "parallelism": f"shard-per-gpu x{world}"}}), flush=True)
 
 
 # ----------------------------------------------------------------------- main
@@ -825,7 +828,8 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 random bytes generated on device)",
-            "config": {"workload": cfg["workload"], "buffers": cfg["count"], "buffer_bytes": cfg["nbytes"],
+            "config": {"workload": cfg["workload"], "config": args.config, "buffers": cfg["count"],
+                       "buffer_bytes": cfg["nbytes"],
                        "bytes_per_gpu_per_step": wl.bytes_per_step, "parallelism": f"shard-per-gpu x{world}",
                        "lanes_per_buffer": args.lanes or "auto"},
             "roofline": {"bound": "hbm", "achieved": round(per_launch_gbps, 1), "peak": HBM_PEAK_GBPS,

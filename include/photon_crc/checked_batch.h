@@ -34,8 +34,11 @@
  *      reference's checksum is crc32c(body with m_checksum = 0): the payload
  *      does NOT enter it (tests/golden/ioalloc_binding.json: the reference's
  *      own template over reference IOVectors). The batch reproduces that: it
- *      zeroes m_checksum (validate_checksum's second line) and checksums the
- *      body; payload segments are not read.
+ *      checksums the body with its first 4 bytes read as zero
+ *      (validate_checksum's second line) and does not read the payload
+ *      segments. It never writes the caller's message: m_checksum keeps the
+ *      received claim (the reference leaves the recomputed value there,
+ *      which equals the claim whenever the message is valid).
  *    - PHOTON_CRC_BATCH_DETACHED_BODY: `body` is a separate buffer (not the
  *      object holding m_checksum) or absent: Crc32Hasher::extend_hash over
  *      the payload segments, then the body, seed 0 (serialize.h:244-252;
@@ -96,17 +99,20 @@ typedef struct photon_crc_msg_batch photon_crc_msg_batch;
 #define PHOTON_CRC_BATCH_DETACHED_BODY 4u /* bodies are separate buffers: hash payload, then body */
 
 /* A batch on the current device with room for max_messages messages and
- * max_segments segments in total (bodies count as segments). NULL on error. */
+ * max_segments segments in total (a DETACHED_BODY body counts as one
+ * segment, a message-object body as two: the zero word standing for
+ * m_checksum and the rest of the object). NULL on error. */
 photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_t max_segments, uint32_t flags);
 void photon_crc_msg_batch_destroy(photon_crc_msg_batch* b);
 
 /* Append one message: its payload iovector (iov[iovcnt], struct iovec layout)
  * followed by `body` (skipped when NULL or body_length == 0, as
  * validate_checksum does) and the checksum it must match. Unless the batch
- * is DETACHED_BODY, a body is the message object: its first 4 bytes
- * (m_checksum) are set to 0 here, as validate_checksum does, and only the
- * body is checksummed (see 2. above). Returns the message's index (>= 0) or
- * -ENOSPC / -EFAULT / -EBUSY (submitted, not yet reset) / -EINVAL. */
+ * is DETACHED_BODY, a body is the message object: it is checksummed with its
+ * first 4 bytes (m_checksum) read as 0, as validate_checksum zeroes them,
+ * at every submit, without writing the object (see 2. above). Returns the
+ * message's index (>= 0) or -ENOSPC / -EFAULT / -EBUSY (submitted, not yet
+ * reset) / -EINVAL. */
 int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec* iov, uint32_t iovcnt,
                                  const void* body, uint64_t body_length, uint32_t expected);
 

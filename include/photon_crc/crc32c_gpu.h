@@ -150,7 +150,15 @@ int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, 
  *                    long buffer in ONE launch over the whole device: chunks
  *                    on a grid anchored at a 4 KiB boundary, each lane group's
  *                    chunks folded in registers, the workgroups' values
- *                    XOR-combined by the last workgroup to finish.
+ *                    XOR-combined by the last workgroup to finish; up to a
+ *                    256 KiB block span, one workgroup with no table
+ *                    prologue (the latency path). Above that the launches of
+ *                    one stream share the reduce's state (a ticket counting
+ *                    every workgroup of the stream's launches, a slot per
+ *                    workgroup): the calls are safe from any number of
+ *                    streams and threads, but such a call cannot be captured
+ *                    into a HIP graph (-ENOTSUP while `stream` is capturing;
+ *                    the latency path may be captured).
  * Asynchronous on `stream` like the batches. */
 int photon_crc32c_series_device(const void* d_buffer, uint32_t part_size, uint32_t n_parts, uint32_t* d_crc_parts,
                                 void* stream);
@@ -180,8 +188,11 @@ int photon_crc32c_extend_spans(const photon_crc_span* spans, int nspans, uint32_
  * with on != 0, crc32c_auto / crc32c_series_auto / crc32c_combine_series_auto
  * (crc.cpp:126-134) and crc64ecma_auto point to wrappers that ask HIP whether the data pointer
  * is device memory (hipMemoryTypeDevice) and, if so, run the calls above
- * synchronously on that pointer's device (legacy default stream), else call
- * the host engine. Off (the default, also at load time) restores the host
+ * synchronously on that pointer's device, else call the host engine. A
+ * routed call runs on a non-blocking stream leased from a per-device pool
+ * (never the legacy default stream, so it does not serialise against the
+ * process's other streams; concurrent routed calls get streams of their
+ * own) and its result is written by the kernel into pinned host memory. Off (the default, also at load time) restores the host
  * engines. The reference signatures have no error channel and the reference
  * always computes (crc.cpp:114-117), so a routed call whose device work
  * fails NEVER returns a made-up value: it is reported on stderr, counted,

@@ -58,8 +58,11 @@ int photon_crc_set_msg_mode(int mode);
 int photon_crc_set_msg_rows(int rows_per_step);
 
 /* One long buffer (photon_crc32c_extend_device / photon_crc64ecma_extend_device,
- * buffers over 256 KiB): lanes per chunk (0 = automatic = 64, or 32) and
- * chunks per lane group of the full grid (0 = automatic = 1). */
+ * buffers over 256 KiB): lanes per chunk (32 or 64) and chunks per lane
+ * group of the full grid (rounds, 1..64); 0 = automatic, by buffer size and
+ * CRC width (photonlibos_amd/csrc/long_plan.h long_plan_for, which lists the
+ * measurements behind each step): CRC-32C 64 lanes x 2 rounds, 32 x 2 from
+ * 512 MiB, 64 x 1 from 1.5 GiB; CRC-64 64 lanes, 2 rounds, 1 from 1 GiB. */
 int photon_crc_set_long_shape(int lanes, int rounds);
 
 /* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =

@@ -85,9 +85,14 @@ class MessageBatch:
         arguments) runs on a HIP runtime thread once the verdicts are on the
         host; it must not call HIP, submit, reset or close this batch."""
         cb = self._DONE(lambda _arg: done()) if done is not None else None
-        self._cb = cb  # keep the ctypes trampoline alive while HIP may call it
+        # `cb` (a local) keeps the new trampoline alive through the call. It
+        # replaces the one held for the previous submit only once this submit
+        # succeeded: the C side refuses (-EBUSY) while the previous callback
+        # is queued or running, so after a refusal HIP may still call the old
+        # trampoline, and after a success it never will again (ADVICE r3).
         _check(lib().photon_crc_msg_batch_submit(self._b, stream, ctypes.cast(cb, ctypes.c_void_p) if cb else None,
                                                  None))
+        self._cb = cb
 
     def wait(self):
         rc = lib().photon_crc_msg_batch_wait(self._b)

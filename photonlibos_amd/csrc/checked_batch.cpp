@@ -169,6 +169,11 @@ struct photon_crc_msg_batch {
     uint64_t* d_start = nullptr;
     uint32_t* d_out = nullptr;
     uint32_t* d_seg = nullptr;  // segment CRCs of the two-kernel form (device memory)
+    // 16 zero bytes of device memory: an object body's m_checksum is hashed
+    // as this zero word instead of being zeroed in the caller's message
+    // (no host memset on a TRUSTED batch's device body, refilled
+    // bodies re-masked on every submit, the caller's object left unmodified).
+    uint32_t* d_zero = nullptr;
     hipEvent_t done_ev = nullptr;
     uint64_t nmsg = 0, nseg = 0;
     uint64_t host_bytes = 0, total_bytes = 0;  // payload in host memory / all (lane choice)
@@ -195,6 +200,7 @@ void free_batch(photon_crc_msg_batch* b) {
         for (void* p : {(void*)b->d_iov, (void*)b->d_start, (void*)b->d_out})
             if (p) (void)hipFree(p);
     if (b->d_seg) (void)hipFree(b->d_seg);
+    if (b->d_zero) (void)hipFree(b->d_zero);
     delete b;
 }
 
@@ -347,6 +353,8 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
     dm((void**)&b->d_start, b->h_start, (M + 1) * 8);
     dm((void**)&b->d_out, b->h_out, M * 4);
     if (e == hipSuccess) e = hipMalloc((void**)&b->d_seg, S * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&b->d_zero, 16);
+    if (e == hipSuccess) e = hipMemset(b->d_zero, 0, 16);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         report_hip_error(e, "photon_crc_msg_batch_create");
@@ -377,39 +385,45 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
     // word is the CRC (init 0) of the data with that word zeroed, so the
     // reference's value is crc32c(body with m_checksum = 0) and the payload
     // does not enter it (tests/golden/ioalloc_binding.json).
+    // The batch hashes the body as two segments, the batch's own device zero
+    // word in place of m_checksum and then body[4, len): the same CRC, with
+    // the caller's object never written (device or host, TRUSTED or not) and
+    // the word masked again on every resubmit of refilled bodies.
     const bool object_body = has_body && !(b->flags & PHOTON_CRC_BATCH_DETACHED_BODY);
     if (object_body && body_length < 4) return report_error(-EINVAL, "message body shorter than its m_checksum");
-    const uint32_t nput = object_body ? 1 : iovcnt + (has_body ? 1 : 0);
+    const uint32_t nput = object_body ? (body_length > 4 ? 2u : 1u) : iovcnt + (has_body ? 1 : 0);
     if (b->nmsg >= b->max_msg || b->nseg + nput > b->max_seg) return report_error(-ENOSPC, "batch is full");
     const bool trusted = b->flags & PHOTON_CRC_BATCH_TRUSTED;
     uint64_t s = b->nseg;
     uint64_t host = 0, total = 0;
-    auto put = [&](const void* p, uint64_t n, bool zero_field) -> int {
-        if (!n) return 0;  // crc32c_extend over 0 bytes is the identity
-        bool in_host = true;  // trusted batches: assume RPC payloads in pinned host memory
-        const void* d = trusted ? p : device_address(p, n, &in_host);
-        if (!d) return report_error(-EFAULT, "segment is not device-accessible (pin it: photon_crc_pinned_allocate)");
-        if (zero_field) {  // validate_checksum's `m_checksum = Hasher::init_value()` (serialize.h:268)
-            if (in_host) {
-                memset(const_cast<void*>(p), 0, 4);
-            } else {
-                static const uint32_t zero = 0;
-                hipError_t e = hipMemcpy(const_cast<void*>(d), &zero, 4, hipMemcpyHostToDevice);
-                if (e != hipSuccess) return report_hip_error(e, "hipMemcpy(m_checksum = 0)");
-            }
-        }
+    // The device address of [p, p + n) (checked unless TRUSTED); null if not device-accessible.
+    auto resolve = [&](const void* p, uint64_t n, bool* in_host) -> const void* {
+        *in_host = true;  // trusted batches: assume RPC payloads in pinned host memory
+        return trusted ? p : device_address(p, n, in_host);
+    };
+    auto put = [&](const void* d, uint64_t n, bool in_host) {
+        if (!n) return;  // crc32c_extend over 0 bytes is the identity
         b->h_iov[s++] = photon_crc_iovec{d, n};
         total += n;
         if (in_host) host += n;
-        return 0;
     };
     if (object_body) {
-        if (int rc = put(body, body_length, true)) return rc;
+        bool in_host = true;
+        const void* d = resolve(body, body_length, &in_host);
+        if (!d) return report_error(-EFAULT, "body is not device-accessible (pin it: photon_crc_pinned_allocate)");
+        put(b->d_zero, 4, false);  // validate_checksum's `m_checksum = Hasher::init_value()` (serialize.h:268)
+        put(static_cast<const uint8_t*>(d) + 4, body_length - 4, in_host);
     } else {
-        for (uint32_t k = 0; k < iovcnt; ++k)
-            if (int rc = put(iov[k].base, iov[k].len, false)) return rc;
-        if (has_body)
-            if (int rc = put(body, body_length, false)) return rc;
+        for (uint32_t k = 0; k <= iovcnt; ++k) {
+            const void* p = k < iovcnt ? iov[k].base : body;
+            const uint64_t n = k < iovcnt ? iov[k].len : (has_body ? body_length : 0);
+            if (!n) continue;
+            bool in_host = true;
+            const void* d = resolve(p, n, &in_host);
+            if (!d)
+                return report_error(-EFAULT, "segment is not device-accessible (pin it: photon_crc_pinned_allocate)");
+            put(d, n, in_host);
+        }
     }
     b->nseg = s;
     b->host_bytes += host;

@@ -714,48 +714,164 @@ LongPlan long_plan(const void* data, uint64_t n, int cus, bool crc64) {
     return long_plan_for(data, n, cus, g_long_shape.load(std::memory_order_relaxed), 0, crc64);
 }
 
-// long_reduce's state (ticket + slots) for a long-buffer launch on `st`: ONE
-// zeroed buffer per (device, stream) -- per thread for hipStreamPerThread --
-// kept for the life of the process. Launches on one stream run in order and
-// each leaves the ticket at 0, so the buffer needs no lease and no event: the
-// scratch lease's hipEventRecord after every launch put a marker packet
-// between back-to-back launches and cost 6 µs per 1 GiB call
-// (scripts/ab_long.py probe+ev). A stream handle is reused only after the
-// stream's work has completed. *lease = true: a leased scratch buffer
-// instead (more than 4096 streams seen), to be returned with scratch_free.
-std::mutex g_ls_mu;
-std::map<std::tuple<int, uintptr_t, std::thread::id>, void*> g_long_state;
+// A multi-workgroup long launch may not be captured into a graph (see
+// long_state); one-workgroup launches (<= 256 KiB) hold no state and may.
+int refuse_if_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(st, &cs);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(-ENOTSUP, "a long-buffer call over 256 KiB cannot be captured into a HIP graph "
+                              "(its cross-workgroup reduce state is per stream)");
+    return 0;
+}
 
-int long_state(hipStream_t st, void** p, bool* lease) {
+// long_reduce's state (ticket + slots) for a long-buffer launch on `st`: ONE
+// buffer per (device, stream) -- per thread for hipStreamPerThread -- kept
+// for the life of the process. Launches on one stream run in order, so the
+// buffer needs no lease and no event: the scratch lease's hipEventRecord
+// after every launch put a marker packet between back-to-back launches and
+// cost 6 µs per 1 GiB call (scripts/ab_long.py probe+ev). Its 64-bit ticket
+// is never reset (long_reduce): `base` counts the workgroups of every launch
+// enqueued on the state so far, advanced under the state's lock in the same
+// order as the launches are enqueued. If a destroyed stream's handle (or a
+// recycled thread id's per-thread stream) comes back while the old stream's
+// last launch still runs, the two launches may spoil each other's result,
+// but the count stays exact for every later launch. A stream
+// being captured into a HIP graph is refused by the caller (the graph would
+// embed one `base` and replay it). lease != nullptr: a leased scratch buffer
+// instead (more than 4096 streams seen), ticket 0 and put back to 0 by the
+// kernel, to be returned with scratch_free.
+struct LongState {
+    void* p = nullptr;
+    uint64_t base = 0;
+    std::mutex mu;
+};
+std::mutex g_ls_mu;
+std::map<std::tuple<int, uintptr_t, std::thread::id>, LongState*> g_long_state;
+
+int long_state(hipStream_t st, LongState** out, void** lease) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     const auto key = std::make_tuple(dev, reinterpret_cast<uintptr_t>(st),
                                      st == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id());
-    *lease = false;
+    *out = nullptr;
+    *lease = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_ls_mu);
         auto it = g_long_state.find(key);
         if (it != g_long_state.end()) {
-            *p = it->second;
+            *out = it->second;
             return 0;
         }
-        if (g_long_state.size() >= 4096) {
-            *lease = true;
-            return scratch_alloc(p, 8 + 8 * kLongMaxGrid, st, true);
-        }
+        if (g_long_state.size() >= 4096) return scratch_alloc(lease, 8 + 8 * kLongMaxGrid, st, true);
     }
-    void* b = nullptr;
-    if ((e = hipMalloc(&b, 8 + 8 * kLongMaxGrid)) != hipSuccess) return hip_fail(e, "hipMalloc(long state)");
-    if ((e = hipMemset(b, 0, 8 + 8 * kLongMaxGrid)) != hipSuccess) {
-        (void)hipFree(b);
+    auto* ls = new LongState;
+    if ((e = hipMalloc(&ls->p, 8 + 8 * kLongMaxGrid)) != hipSuccess) {
+        delete ls;
+        return hip_fail(e, "hipMalloc(long state)");
+    }
+    if ((e = hipMemset(ls->p, 0, 8 + 8 * kLongMaxGrid)) != hipSuccess) {
+        (void)hipFree(ls->p);
+        delete ls;
         return hip_fail(e, "hipMemset(long state)");
     }
     std::lock_guard<std::mutex> lk(g_ls_mu);
-    auto ins = g_long_state.emplace(key, b);
-    if (!ins.second) (void)hipFree(b);  // another thread registered this stream first
-    *p = ins.first->second;
+    auto ins = g_long_state.emplace(key, ls);
+    if (!ins.second) {  // another thread registered this stream first
+        (void)hipFree(ls->p);
+        delete ls;
+    }
+    *out = ins.first->second;
     return 0;
+}
+
+// Enqueue a long launch on its state: `launch(state, base, reset)` returns
+// the hipError_t of the enqueue; a persistent state's base advances by the
+// grid only when the launch was enqueued, under its lock (launch order).
+template <typename L>
+int long_launch(hipStream_t st, uint64_t grid, const char* what, L launch) {
+    if (grid <= 1) {
+        const hipError_t e = launch(nullptr, 0ull, 0u);
+        return e == hipSuccess ? 0 : hip_fail(e, what);
+    }
+    if (int rc = refuse_if_capturing(st)) return rc;
+    LongState* ls = nullptr;
+    void* lease = nullptr;
+    if (int rc = long_state(st, &ls, &lease)) return rc;
+    if (lease) {
+        const hipError_t e = launch(lease, 0ull, 1u);
+        const int frc = scratch_free(lease, st);
+        return e != hipSuccess ? hip_fail(e, what) : frc;
+    }
+    std::lock_guard<std::mutex> lk(ls->mu);
+    const hipError_t e = launch(ls->p, ls->base, 0u);
+    if (e != hipSuccess) return hip_fail(e, what);
+    ls->base += grid;
+    return 0;
+}
+
+
+// The small-buffer kernel's device image (crc32c_kernels.h "one small
+// buffer"): its LDS tables and basis words, computed on the host with gf2.h
+// and copied to each device once, on that device's first small call (a
+// private non-blocking stream, so no other stream is synchronised).
+std::mutex g_img_mu;
+std::vector<uint32_t*> g_img;
+
+std::vector<uint32_t> small_image_host() {
+    std::vector<uint32_t> img(kSmImage / 4, 0u);
+    auto slices = [&](uint32_t off, uint32_t k) {  // (b << 8t) * k, t < 4, b < 256, at byte offset off
+        for (uint32_t t = 0; t < 4; ++t)
+            for (uint32_t b = 0; b < 256; ++b) img[off / 4 + t * 256 + b] = mulmod(b << (8 * t), k);
+    };
+    slices(kSmD, kPoly);                                    // x^32: the word step
+    slices(kSmS, xpow(8ull * 16ull * kSmallBlocks / 16));  // one row of 1024 blocks: x^(8 * 16384)
+    for (uint32_t dl = 0; dl < 8; ++dl) slices(kSmA + dl * 4096u, xpow(32ull + 128ull * dl));
+    for (uint32_t dh = 1; dh < 8; ++dh) slices(kSmB + (dh - 1) * 4096u, xpow(1024ull * dh));
+    for (uint32_t w = 0; w < 16; ++w) mul_basis(xpow(8192ull * (15 - w)), &img[kSmWave / 4 + w * 32]);
+    for (uint32_t k = 0; k < 32; ++k) mul_basis(xpow_inv(8ull * k), &img[kSmTail / 4 + k * 32]);
+    return img;
+}
+
+int small_image(int dev, const uint32_t** out) {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    if ((int)g_img.size() <= dev) g_img.resize(dev + 1, nullptr);
+    if (!g_img[dev]) {
+        static const std::vector<uint32_t> host = small_image_host();
+        void* d = nullptr;
+        hipStream_t s = nullptr;
+        hipError_t e = hipMalloc(&d, kSmImage);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMemcpyAsync(d, host.data(), kSmImage, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (s) (void)hipStreamDestroy(s);
+        if (e != hipSuccess) {
+            if (d) (void)hipFree(d);
+            return hip_fail(e, "small-buffer table image");
+        }
+        g_img[dev] = static_cast<uint32_t*>(d);
+    }
+    *out = g_img[dev];
+    return 0;
+}
+
+// The small kernel's geometry for [p, p + n), or false when the block span
+// exceeds kSmallBlocks (the long kernel's case).
+bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a) {
+    const uintptr_t d = reinterpret_cast<uintptr_t>(p);
+    const uint64_t s0 = d & 15u, eoff = s0 + n;
+    const uint64_t cover = eoff > s0 + 4 ? eoff : s0 + 4;  // the seed's 4 bytes lie inside the grid
+    const uint64_t nb = (cover + 15) >> 4;
+    if (nb > kSmallBlocks) return false;
+    a->a0 = reinterpret_cast<const uint8_t*>(d - s0);
+    a->nb = (uint32_t)nb;
+    a->s0 = (uint32_t)s0;
+    a->eoff = (uint32_t)eoff;
+    a->k = (uint32_t)(16 * nb - eoff);
+    a->seed = seed;
+    return true;
 }
 
 }  // namespace
@@ -1310,23 +1426,16 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     memcpy(a.xq, pw.p64[1], sizeof(a.xq));
     memcpy(a.xr, pw.p64[2], sizeof(a.xr));
     memcpy(a.xsb, pw.xsb64, sizeof(a.xsb));
-    void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
-    bool leased = false;
-    if (lp.grid > 1) {
-        if (int rc = long_state(st, &state, &leased)) return rc;
+    return long_launch(st, lp.grid, "crc64_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint64_t*>(state);
-    }
-    if (lp.lanes == 32)
-        hipLaunchKernelGGL((crc64_long_kernel<32>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(32));
-    else
-        hipLaunchKernelGGL((crc64_long_kernel<64>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(64));
-    const hipError_t e = hipGetLastError();
-    int rc = e == hipSuccess ? 0 : hip_fail(e, "crc64_long_kernel launch");
-    if (leased) {
-        const int frc = scratch_free(state, st);
-        if (!rc) rc = frc;
-    }
-    return rc;
+        a.tbase = base;
+        a.treset = reset;
+        if (lp.lanes == 32)
+            hipLaunchKernelGGL((crc64_long_kernel<32>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(32));
+        else
+            hipLaunchKernelGGL((crc64_long_kernel<64>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts64(64));
+        return hipGetLastError();
+    });
 }
 
 int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,
@@ -1403,6 +1512,14 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
+    SmallArgs sa{};
+    if (small_args(d_data, nbytes, seed, &sa)) {  // <= 256 KiB: one workgroup, latency path
+        if (int rc = small_image(dev, &sa.image)) return rc;
+        sa.out = d_out;
+        hipLaunchKernelGGL(crc32c_small_kernel, dim3(1), dim3(1024), 0, st, sa);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "crc32c_small_kernel launch");
+    }
     const LongPlan lp = long_plan(d_data, nbytes, cus, false);
     const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
@@ -1419,23 +1536,16 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     memcpy(a.xp, pw.xpj32, sizeof(a.xp));
     memcpy(a.xq, pw.p32[1], sizeof(a.xq));
     memcpy(a.xr, pw.p32[2], sizeof(a.xr));
-    void* state = nullptr;  // long_reduce's ticket + slots, the ticket left zero by the kernel
-    bool leased = false;
-    if (lp.grid > 1) {
-        if (int rc = long_state(st, &state, &leased)) return rc;
+    return long_launch(st, lp.grid, "crc32c_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint32_t*>(state);
-    }
-    if (lp.lanes == 32)
-        hipLaunchKernelGGL((crc32c_long_kernel<32, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(32));
-    else
-        hipLaunchKernelGGL((crc32c_long_kernel<64, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(64));
-    const hipError_t e = hipGetLastError();
-    int rc = e == hipSuccess ? 0 : hip_fail(e, "crc32c_long_kernel launch");
-    if (leased) {
-        const int frc = scratch_free(state, st);
-        if (!rc) rc = frc;
-    }
-    return rc;
+        a.tbase = base;
+        a.treset = reset;
+        if (lp.lanes == 32)
+            hipLaunchKernelGGL((crc32c_long_kernel<32, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(32));
+        else
+            hipLaunchKernelGGL((crc32c_long_kernel<64, 4>), dim3(lp.grid), dim3(kBlock), 0, st, a, lane_consts(64));
+        return hipGetLastError();
+    });
 }
 
 }  // extern "C"
@@ -1636,22 +1746,86 @@ uint32_t host_crc_of_device(const uint8_t* p, size_t n, uint32_t crc) {
     return crc;
 }
 
-// Run f(d_tmp) with `bytes` of stream-ordered device scratch on the default
-// stream, copy `out_bytes` of it to `h_out`, and wait.
+// Routed calls run on a stream leased from a per-device pool of non-blocking
+// streams (created on demand and kept), never on the null stream: a routed
+// call does not serialise against the process's other blocking streams, and
+// routed calls from many threads each get a stream of their own (VERDICT r3
+// next #3). Each pooled stream carries 64 bytes of pinned, device-mapped
+// host memory that a kernel writes its result into: the caller waits for
+// the stream and reads the word, no D2H copy.
+struct RoutedStream {
+    int dev;
+    hipStream_t st;
+    void* h;  // host address of the result area
+    void* d;  // its device address
+};
+std::mutex g_rs_mu;
+std::vector<RoutedStream*> g_rs_free;
+
+int routed_lease(int dev, RoutedStream** out) {
+    {
+        std::lock_guard<std::mutex> lk(g_rs_mu);
+        for (size_t i = 0; i < g_rs_free.size(); ++i)
+            if (g_rs_free[i]->dev == dev) {
+                *out = g_rs_free[i];
+                g_rs_free.erase(g_rs_free.begin() + (long)i);
+                return 0;
+            }
+    }
+    auto* r = new RoutedStream{dev, nullptr, nullptr, nullptr};
+    hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipHostMalloc(&r->h, 64, hipHostMallocMapped | hipHostMallocPortable);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&r->d, r->h, 0);
+    if (e != hipSuccess) {
+        if (r->h) (void)hipHostFree(r->h);
+        if (r->st) (void)hipStreamDestroy(r->st);
+        delete r;
+        return hip_fail(e, "routed stream");
+    }
+    *out = r;
+    return 0;
+}
+
+void routed_return(RoutedStream* r) {
+    std::lock_guard<std::mutex> lk(g_rs_mu);
+    g_rs_free.push_back(r);
+}
+
+// Run f(d_result, stream) on a leased routed stream and wait; the kernel's
+// `bytes`-byte result lands in pinned memory and is copied to h_out.
 template <typename F>
-int with_scratch(uint64_t bytes, void* h_out, uint64_t out_bytes, F f) {
+int routed_call(int dev, void* h_out, size_t bytes, F f) {
+    RoutedStream* r = nullptr;
+    if (int rc = routed_lease(dev, &r)) return rc;
+    int rc = f(r->d, r->st);
+    const hipError_t e = hipStreamSynchronize(r->st);  // also after a failed enqueue: nothing left running
+    if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize(routed)");
+    if (!rc) memcpy(h_out, r->h, bytes);
+    routed_return(r);
+    return rc;
+}
+
+// Run f(d_tmp, stream) with `bytes` of leased device scratch on a leased
+// routed stream, copy `out_bytes` of it to `h_out`, and wait.
+template <typename F>
+int with_scratch(int dev, uint64_t bytes, void* h_out, uint64_t out_bytes, F f) {
+    RoutedStream* r = nullptr;
+    if (int rc = routed_lease(dev, &r)) return rc;
     void* tmp = nullptr;
-    if (int arc = scratch_alloc(&tmp, bytes, nullptr)) return arc;
-    int rc = f(tmp);
+    int rc = scratch_alloc(&tmp, bytes, r->st);
     hipError_t e;
     if (!rc) {
-        e = hipMemcpyAsync(h_out, tmp, out_bytes, hipMemcpyDeviceToHost, nullptr);
-        if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync");
+        rc = f(tmp, r->st);
+        if (!rc) {
+            e = hipMemcpyAsync(h_out, tmp, out_bytes, hipMemcpyDeviceToHost, r->st);
+            if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync");
+        }
+        const int frc = scratch_free(tmp, r->st);
+        if (!rc) rc = frc;
     }
-    const int frc = scratch_free(tmp, nullptr);
-    if (!rc) rc = frc;
-    e = hipStreamSynchronize(nullptr);
+    e = hipStreamSynchronize(r->st);
     if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    routed_return(r);
     return rc;
 }
 
@@ -1660,8 +1834,8 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     if (dev < 0) return host_engine(&g_host_crc)(p, n, crc);
     DeviceScope scope(dev);
     uint32_t r = 0;
-    int rc = with_scratch(4, &r, 4, [&](void* d) {
-        return photon_crc32c_extend_device(p, n, crc, static_cast<uint32_t*>(d), nullptr);
+    int rc = routed_call(dev, &r, 4, [&](void* d, hipStream_t st) {
+        return photon_crc32c_extend_device(p, n, crc, static_cast<uint32_t*>(d), st);
     });
     if (!rc) return r;
     routed_failure("crc32c_extend", rc);
@@ -1676,18 +1850,24 @@ void dispatch_series(const uint8_t* buf, uint32_t part, uint32_t n, uint32_t* pa
     // crc.cpp:481-500); when the saved host engine is crc32c_series_sw those
     // parts get their real CRCs (crc.cpp:474-478), so run the plain batch.
     const bool sw = host_engine(&g_host_series) == crc32c_series_sw;
-    auto run = [&](uint32_t* out) {
-        return sw ? photon_crc32c_batch_strided(buf, part, part, n, 0, nullptr, out, nullptr)
-                  : photon_crc32c_series_device(buf, part, n, out, nullptr);
+    auto run = [&](uint32_t* out, hipStream_t st) {
+        return sw ? photon_crc32c_batch_strided(buf, part, part, n, 0, nullptr, out, st)
+                  : photon_crc32c_series_device(buf, part, n, out, st);
     };
     const bool parts_on_dev = device_of(parts) == dev;
     int rc;
     if (parts_on_dev) {
-        rc = run(parts);
-        hipError_t e = rc ? hipSuccess : hipStreamSynchronize(nullptr);
-        if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+        RoutedStream* r = nullptr;
+        rc = routed_lease(dev, &r);
+        if (!rc) {
+            rc = run(parts, r->st);
+            hipError_t e = hipStreamSynchronize(r->st);
+            if (!rc && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+            routed_return(r);
+        }
     } else {
-        rc = with_scratch(4ull * n, parts, 4ull * n, [&](void* d) { return run(static_cast<uint32_t*>(d)); });
+        rc = with_scratch(dev, 4ull * n, parts, 4ull * n,
+                          [&](void* d, hipStream_t st) { return run(static_cast<uint32_t*>(d), st); });
     }
     if (!rc) return;
     routed_failure("crc32c_series", rc);
@@ -1714,9 +1894,9 @@ uint32_t dispatch_combine_series(uint32_t* crc, uint32_t part, uint32_t n) {
     const int dev = n ? device_of(crc) : -1;
     if (dev < 0) return host_engine(&g_host_cseries)(crc, part, n);
     DeviceScope scope(dev);
-    uint32_t r = 0;
-    int rc = with_scratch(4, &r, 4, [&](void* d) {
-        return photon_crc32c_combine_series_device(crc, part, n, static_cast<uint32_t*>(d), nullptr);
+    uint32_t r = 0;  // device scratch, not the pinned word: the kernel accumulates with device atomics
+    int rc = with_scratch(dev, 4, &r, 4, [&](void* d, hipStream_t st) {
+        return photon_crc32c_combine_series_device(crc, part, n, static_cast<uint32_t*>(d), st);
     });
     if (!rc) return r;
     routed_failure("crc32c_combine_series", rc);
@@ -1731,8 +1911,8 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     if (dev < 0) return host_engine(&g_host_crc64)(p, n, crc);
     DeviceScope scope(dev);
     uint64_t r = 0;
-    int rc = with_scratch(8, &r, 8, [&](void* d) {
-        return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), nullptr);
+    int rc = routed_call(dev, &r, 8, [&](void* d, hipStream_t st) {
+        return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), st);
     });
     if (!rc) return r;
     routed_failure("crc64ecma_extend", rc);

@@ -1422,7 +1422,9 @@ struct LongArgs {
     uint32_t xs;        // X^S
     uint64_t stride;    // S: lane groups in the grid
     uint32_t* out;
-    uint32_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes, ticket zero; grid > 1 only)
+    uint32_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes; grid > 1 only)
+    uint64_t tbase;     // long_reduce: the state's ticket count before this launch
+    uint32_t treset;    // long_reduce: put the ticket back to 0 (a leased state)
     uint32_t xp[64];    // J X^j, J = x^-(8 (chunk - L_last)) (kOne when T == 1): every group's
                         // final factor carries J once, so the total needs no last multiply
     uint32_t xq[64];    // X^(64 j)
@@ -1437,42 +1439,67 @@ struct LongArgs {
 // slots (8 + 8 * kLongMaxGrid bytes).
 //
 // Ordering without fences: every access to the state is a device-scope
-// (agent) atomic -- the slot store and the slot loads are `sc1` accesses,
-// coherent across the XCDs' separate L2s by themselves -- and the slot store
-// has completed (s_waitcnt vmcnt(0)) before the ticket is taken; the last
-// workgroup issues its slot loads only after its ticket returned. This is
-// the LLVM AMDGPU memory model's mapping of monotonic agent-scope atomics on
-// gfx942/gfx950; an acquire/release pair is only needed to order plain
-// (non-atomic) accesses, and at agent scope it costs a `buffer_wbl2 sc1`
-// (write back the XCD's L2) plus `buffer_inv sc1`. FENCED (bench probe,
-// ABL 8) keeps that pair: 5.7 µs more per 1 GiB launch
-// (repo:profiles/r03b_ab_long_tail_ablations.jsonl). Round 3's first form,
-// device-scope atomicXor into one accumulator or eight with a second level,
-// was a chain of 4-7 dependent atomics with fences (8 µs after the last chunk).
+// (agent) atomic, the slot store has completed before the ticket is taken,
+// and the last workgroup issues its slot loads only after its ticket
+// returned. In the LLVM AMDGPU memory model's code sequences for GFX942
+// (AMDGPUUsage "Memory Model GFX942"; gfx950 follows it), the rows used are
+//   store atomic monotonic, agent, global  -> global_store sc1
+//   load atomic monotonic, agent, global   -> global_load sc1
+//   atomicrmw monotonic, agent, global     -> global_atomic (sc0: returns)
+// and the release sequence a fetch_add(release, agent) would add is
+// `buffer_wbl2 sc1; s_waitcnt vmcnt(0)`: the write-back only concerns
+// earlier NON-atomic stores cached in this XCD's L2 (there are none: the
+// slot store is itself an sc1 agent-scope store), and the `s_waitcnt
+// vmcnt(0)` is kept here explicitly -- on GFX9 stores are counted in vmcnt,
+// so the slot store is acknowledged at agent scope before the ticket atomic
+// issues. The acquire side's `buffer_inv sc1` only matters for later
+// non-atomic loads; the slot loads are sc1 atomics issued after the ticket's
+// value came back (control dependency through the readfirstlane'd branch).
+// Emitted code (hipcc -S, crc32c_long_kernel<32,4>): global_store_dword
+// ... sc1; s_waitcnt vmcnt(0); global_atomic_add ... sc0; s_waitcnt
+// vmcnt(0); ... global_load_dword ... sc1. The stores-in-vmcnt rule is GFX9's
+// (GFX10+ count stores in vscnt), hence the #error for other targets below.
+// FENCED (bench probe, ABL 8) keeps the release/acquire pair: 5.7 µs more
+// per 1 GiB launch (repo:profiles/r03b_ab_long_tail_ablations.jsonl). Round
+// 3's first form, device-scope atomicXor into one accumulator or eight with
+// a second level, was a chain of 4-7 dependent atomics with fences (8 µs
+// after the last chunk). tests/test_gpu_fullsize.py runs 1,000 back-to-back
+// full-grid launches over alternating data through one state.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "long_reduce's fence-free ordering relies on GFX9's stores-in-vmcnt (s_waitcnt 0x0F70 = vmcnt(0)): gfx942/gfx950 only"
+#endif
 constexpr uint32_t kLongMaxGrid = 512;
 template <typename T, typename F, bool FENCED = false>
-__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
+__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset) {
     const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
     if (grid == 1) {
         if (lane == 0) *out = fin(v);
         return;
     }
-    // The same layout for both widths (the zeroed scratch class is shared by
-    // the CRC32C and CRC-64 kernels): a 32-bit ticket in bytes 0-3 (4-7 stay
-    // zero), slots from byte 8.
-    unsigned int* ticket = reinterpret_cast<unsigned int*>(state);
+    // The same layout for both widths: a 64-bit ticket in bytes 0-7, slots
+    // from byte 8. The ticket is never reset on a per-stream state: it counts
+    // every workgroup of every launch, the host passes the count before this
+    // launch (`base`, kept per state and advanced under a lock in launch
+    // order), and the workgroup that draws base + grid - 1 is the last. So a
+    // launch that overlapped another on the same state (a destroyed stream's
+    // last launch still running when a new stream got its handle)
+    // can only spoil those two launches' results: the count stays exact for
+    // every later launch. A leased state (reset != 0) starts at 0 and is put
+    // back to 0 (leases are exclusive, ordered by their event).
+    unsigned long long* ticket = reinterpret_cast<unsigned long long*>(state);
     T* slot = reinterpret_cast<T*>(reinterpret_cast<char*>(state) + 8);
+    const unsigned long long mine = base + grid - 1;
     uint32_t last = 0;
     if (lane == 0) {
         if constexpr (FENCED) {
             slot[blockIdx.x] = v;
-            last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+            last = __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == mine;
         } else {
             __hip_atomic_store(slot + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler order only
             __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): the slot store has completed
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grid - 1;
+            last = __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine;
         }
     }
     if (!__shfl(last, 0)) return;
@@ -1485,7 +1512,7 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin) {
         x = group_xor<64>(x);
     if (lane == 0) {
         *out = fin(x);
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (reset) __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1598,9 +1625,10 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
         if constexpr (ABL & 20) {
             if (lane == 0) *a.out = v;
         } else if constexpr (ABL & 8) {
-            long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(v, a.acc, a.out, [](uint32_t x) { return x; });
+            long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(v, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase,
+                                                                a.treset);
         } else {
-            long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; });
+            long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
         }
     }
     if constexpr (STAMP) {
@@ -1625,6 +1653,133 @@ __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneCon
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
     __shared__ uint32_t red[kWaves];
     long_run<G, U>(a, kc, lds, red, nullptr);
+}
+
+// ------------------------------------------------ one small buffer (latency)
+// photon_crc32c_extend_device for buffers whose 16-byte block span is at most
+// kSmallBlocks (256 KiB): the reference's small perf shape (128 KiB at
+// buf+1, test_checksum.cpp:125-168) and the routed drop-in on a device
+// pointer (crc32c.h:30-33) are latency, not bandwidth. ONE workgroup of 1024
+// threads, no table prologue: the tables are copied from a device-resident
+// image built once per device (photon_crc32c_extend_device's first call), the
+// copy issued first and the payload loads right behind it, all in flight at
+// once (the 1024 threads x 16 rows cover 256 KiB).
+// Geometry: the block grid [a0, a0 + 16 nb) covers the data from its aligned
+// start through the end rounded up to 16 bytes (and at least the 4 seed
+// bytes). The 1024 threads are ONE lane group: thread t walks column t of
+// rows of 1024 blocks anchored at the END (block b = nb - 1024 (rows - r) + t
+// in row r; b < 0 is a leading zero block, which does not change a CRC), so
+// every thread's last block is in the last row and its distance to the end
+// is 1023 - t = 64 (15 - wave) + (63 - lane). Masking: bytes before the data
+// start and at or after its end are zero, the seed is XORed into the data's
+// first 4 bytes (head_word_sel). The k zero bytes after the end multiply the
+// CRC by x^(8k): the result is multiplied by x^(-8k) at the end, which also
+// makes a seed over fewer than 4 data bytes exact (crc32c_extend(D, n, s) =
+// crc(D) ^ s x^(8n)).
+// Per thread: Q <- Q * x^(8*16384) ^ lag16(block) over its rows (S table);
+// then Q -> P and the lane shift x^(128 (63 - lane)) through A_dl, B_dh (the
+// batch kernel's G >= 16 finish tables), XOR over the wave, the wave's shift
+// x^(8192 (15 - wave)) as a lane-parallel multiply (basis words from the
+// image), XOR over the waves in LDS, x^(-8k) (lane-parallel), store.
+// Single-replica tables: a few bank conflicts cost cycles on a path bound
+// by its dependent LDS round trips, not by LDS throughput.
+constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of blocks: 16 rows of 1024
+constexpr uint32_t kSmD = 0, kSmS = 4096, kSmA = 8192, kSmB = kSmA + 8u * 4096u;
+constexpr uint32_t kSmLds = kSmB + 7u * 4096u;                // 69632 B of tables in LDS
+constexpr uint32_t kSmWave = kSmLds;                          // 16 x 32 words: basis of x^(8192 (15 - w))
+constexpr uint32_t kSmTail = kSmWave + 16u * 32u * 4u;        // 32 x 32 words: basis of x^(-8 k), k < 32
+constexpr uint32_t kSmImage = kSmTail + 32u * 32u * 4u;       // bytes of the device image
+
+struct SmallArgs {
+    const uint8_t* a0;   // aligned start (data start & ~15)
+    const uint32_t* image;
+    uint32_t* out;
+    uint32_t nb;         // blocks of the grid, <= kSmallBlocks
+    uint32_t s0;         // data start - a0 (0..15)
+    uint32_t eoff;       // data end - a0: bytes at or past it are zero
+    uint32_t k;          // grid end - data end (0..31): the result is multiplied by x^(-8k)
+    uint32_t seed;
+};
+
+// p * K through the 4 single-replica byte-slice tables of K at T.
+__device__ __forceinline__ uint32_t small_mul(const uint32_t* T, uint32_t p) {
+    return xor3(xor3(T[p & 0xffu], T[256 + ((p >> 8) & 0xffu)], T[512 + ((p >> 16) & 0xffu)]), T[768 + (p >> 24)], 0u);
+}
+
+// Bytes of the word at `off` (from a0) at or past `eoff` zeroed (branch-free).
+__device__ __forceinline__ uint32_t tail_word(uint32_t w, int off, int eoff) {
+    const int m = eoff - off;                  // data bytes of this word
+    const int mc = m < 0 ? 0 : m > 4 ? 4 : m;
+    return mc == 4 ? w : w & (uint32_t)((1ull << (8 * mc)) - 1ull);
+}
+
+__global__ __launch_bounds__(1024) void crc32c_small_kernel(SmallArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSmLds / 4];
+    __shared__ uint32_t red[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id(), l32 = lane & 31u;
+    // 1. The table copy first (vmcnt counts in issue order: waiting for it
+    //    does not wait for the payload), then every payload row, then the two
+    //    basis words this thread needs at the end.
+    constexpr uint32_t kVec = kSmLds / 16;  // 4352 16-byte pieces
+    u32x4 tv[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t j = (uint32_t)i * 1024u + tid;
+        tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
+    }
+    const uint32_t rows = (a.nb + 1023u) >> 10;
+    const int first = (int)a.nb - (int)(rows << 10) + (int)tid;  // this thread's block in row 0
+    uint4 w[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int b = first + r * 1024;
+        w[r] = ((uint32_t)r < rows && b >= 0) ? load16(a.a0 + 16 * (uint32_t)b) : make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t bw_wave = a.image[kSmWave / 4 + wave * 32u + l32];
+    const uint32_t bw_tail = a.image[kSmTail / 4 + a.k * 32u + l32];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t j = (uint32_t)i * 1024u + tid;
+        if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
+    }
+    lds_barrier();
+    const uint32_t* D = lds + kSmD / 4;
+    const uint32_t* S = lds + kSmS / 4;
+    // 2. The column: lagged blocks (as lag16) and the row shift.
+    uint32_t q = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if ((uint32_t)r >= rows) continue;  // rows is uniform: a skipped row is a scalar branch
+        const int b = first + r * 1024;
+        uint4 v = w[r];
+        if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + seed
+            const int off = b * 16;
+            v.x = head_word_sel(tail_word(v.x, off, (int)a.eoff), off, (int)a.s0, a.seed);
+            v.y = head_word_sel(tail_word(v.y, off + 4, (int)a.eoff), off + 4, (int)a.s0, a.seed);
+            v.z = head_word_sel(tail_word(v.z, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.seed);
+            v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
+            if (b < 0) v = make_uint4(0, 0, 0, 0);
+        }
+        uint32_t c = small_mul(D, v.x) ^ v.y;
+        c = small_mul(D, c) ^ v.z;
+        c = small_mul(D, c) ^ v.w;
+        q = small_mul(S, q) ^ c;
+    }
+    // 3. Q -> P and the shift to the end: x^(32 + 128 dl) then x^(1024 dh), d = 63 - lane.
+    const uint32_t d = 63u - lane, dh = d >> 3;
+    const uint32_t x = small_mul(lds + kSmA / 4 + (d & 7u) * 1024u, q);
+    const uint32_t y = small_mul(lds + kSmB / 4 + (dh ? dh - 1u : 0u) * 1024u, x);
+    uint32_t v = group_xor<64>(dh ? y : x);
+    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (15 - wave)), valid in both halves
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t ^= red[i];
+        t = mul_lanes(t, bw_tail, l32);  // x^(-8k): the zero bytes after the end
+        if (lane == 0) *a.out = t;
+    }
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {

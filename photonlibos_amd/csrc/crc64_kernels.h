@@ -666,7 +666,9 @@ struct Long64Args {
     uint64_t jinv, xs;  // as LongArgs, mod P64
     uint64_t stride;
     uint64_t* out;
-    uint64_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes, ticket zero; grid > 1 only)
+    uint64_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes; grid > 1 only)
+    uint64_t tbase;     // long_reduce: the state's ticket count before this launch
+    uint32_t treset;    // long_reduce: put the ticket back to 0 (a leased state)
     uint64_t xp[64];    // J X^j, X = x^(8*chunk) mod P64
     uint64_t xq[64];    // X^(64 j)
     uint64_t xr[64];    // X^(4096 j)
@@ -744,7 +746,7 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
         uint64_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        long_reduce(v, a.acc, a.out, [](uint64_t x) { return ~x; });  // crc.cpp:119-122: inverted out
+        long_reduce(v, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122: inverted out
     }
 }
 

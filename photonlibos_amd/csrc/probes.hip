@@ -470,6 +470,7 @@ int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* ou
     a.stride = lp.stride;
     a.out = out;
     a.acc = state;
+    a.treset = 1;  // the caller's zeroed buffer, put back to 0 by every launch
     memcpy(a.xp, pw.xpj32, sizeof(a.xp));
     memcpy(a.xq, pw.p32[1], sizeof(a.xq));
     memcpy(a.xr, pw.p32[2], sizeof(a.xr));

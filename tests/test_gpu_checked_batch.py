@@ -327,6 +327,33 @@ def test_ioalloc_binding_against_reference_headers(torch_dev):
 
 
 
+def test_trusted_device_memory_object_body(torch_dev, oracle):
+    """a TRUSTED batch whose message object lives in device memory
+    (no host write into it: the batch masks m_checksum itself)."""
+    torch = torch_dev
+    rng = random.Random(23)
+    objs = torch.from_numpy(np.frombuffer(rng.randbytes(64 * 48), np.uint8).copy()).cuda()
+    host = objs.cpu().numpy()
+    b = MessageBatch(64, 128, TRUSTED)
+    want = []
+    for i in range(64):
+        z = bytearray(host[48 * i:48 * i + 48].tobytes())
+        z[:4] = b"\0\0\0\0"
+        want.append(oracle.crc32c(bytes(z)))
+        assert b.add([], (objs.data_ptr() + 48 * i, 48), want[-1] ^ (i % 2)) == i
+    b.submit()
+    assert b.wait() == 32
+    for i in range(64):
+        assert b.result(i) == (i % 2 == 0, want[i]), i
+    assert np.array_equal(objs.cpu().numpy(), host)  # the objects were not written
+    # a 4-byte object is m_checksum alone: crc32c of 4 zero bytes
+    b.reset()
+    b.add([], (objs.data_ptr(), 4), oracle.crc32c(bytes(4)))
+    b.submit()
+    assert b.wait() == 0
+    b.close()
+
+
 def _object_messages(alloc, rng, nmsg):
     """Photon's layout: payload segments, then the message struct whose first
     4 bytes are m_checksum (the CheckedMessage<> base), 48 bytes."""
@@ -380,14 +407,26 @@ def test_message_object_body_matches_reference_semantics(torch_dev, oracle, flag
             alloc.view(t, n)[4 + rng.randrange(44)] ^= 0x01
             body_bad.add(i)
     b = MessageBatch(len(msgs), 4096, flags)
+    claims = []
     for i, (segs, body) in enumerate(msgs):
-        alloc.view(body[0], 4)[:] = np.frombuffer(rng.randbytes(4), np.uint8)  # m_checksum holds the claim
+        claims.append(rng.randbytes(4))
+        alloc.view(body[0], 4)[:] = np.frombuffer(claims[-1], np.uint8)  # m_checksum holds the claim
         assert b.add(segs, body, want[i]) == i
-        assert not alloc.view(body[0], 4).any()  # validate_checksum's m_checksum = 0
     b.submit()
     assert b.wait() == len(body_bad)
-    for i in range(len(msgs)):
+    for i, (segs, body) in enumerate(msgs):
         assert b.result(i)[0] == (i not in body_bad), i
+        # the batch reads m_checksum as 0 but never writes the caller's object
+        assert bytes(alloc.view(body[0], 4)) == claims[i], i
+    # resubmit after the bodies were refilled (new fields AND a new m_checksum
+    # claim): the word is masked again, the verdicts follow the new contents
+    for i, (segs, (t, n)) in enumerate(msgs):
+        alloc.view(t, n)[:] = np.frombuffer(rng.randbytes(n), np.uint8)
+    want2 = [_photon_checksum(alloc, oracle, s, body) for s, body in msgs]
+    b.submit()
+    b.wait()
+    for i in range(len(msgs)):
+        assert b.result(i)[1] == want2[i], i
     b.close()
     # the same messages, payload hashed (DETACHED_BODY: payload then struct)
     d = MessageBatch(len(msgs), 4096, flags | DETACHED_BODY)

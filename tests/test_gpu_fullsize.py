@@ -238,6 +238,114 @@ def test_extend_device_concurrent_streams(torch_dev, oracle):
     del d
 
 
+def test_extend_device_small_path_edges(torch_dev, oracle):
+    """The one-workgroup latency kernel (crc32c_small_kernel: block span <=
+    256 KiB, tables copied from the device image): every length 0..259 at
+    every start offset 0..15 with a seed (seeds over fewer than 4 data bytes,
+    heads and tails in one block), random lengths, and the span limit
+    itself: 256 KiB spans at offsets 0 and 15 (the last small case / the
+    first long one), all against the oracle."""
+    torch = torch_dev
+    n_max = (256 << 10) + 64
+    d = torch.empty(n_max + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0D00)
+    host = d.cpu().numpy()
+    base = (-d.data_ptr()) % 16  # offset of a 16-byte-aligned address
+    out = torch.zeros(260 * 16, dtype=torch.int32, device="cuda")
+    cases = []
+    for n in range(260):
+        for off in range(16):
+            cases.append((base + off, n, (n * 0x9E3779B1 + off) & 0xFFFFFFFF))
+    rng = np.random.default_rng(0x5EED0D01)
+    for _ in range(200):
+        n = int(rng.integers(260, 256 << 10))
+        cases.append((base + int(rng.integers(0, 16)), n, int(rng.integers(0, 1 << 32))))
+    span = 256 << 10
+    cases += [(base, span, 1), (base + 15, span - 15, 2), (base + 15, span - 14, 3), (base, span + 1, 4),
+              (base + 1, span - 4, 5), (base + 12, span - 16, 6)]
+    for k0 in range(0, len(cases), out.numel()):
+        part = cases[k0:k0 + out.numel()]
+        for k, (off, n, seed) in enumerate(part):
+            ck.extend_device(d.data_ptr() + off, n, seed, out[k:k + 1])
+        torch.cuda.synchronize()
+        got = _u32(out)
+        for k, (off, n, seed) in enumerate(part):
+            assert int(got[k]) == oracle.crc32c(host[off:off + n], seed), (off - base, n, seed)
+
+
+def test_extend_device_thousand_back_to_back_launches(torch_dev, oracle):
+    """the fence-free cross-workgroup reduce (long_reduce)
+    reused by 1,000 back-to-back full-grid launches on ONE stream (one state:
+    ticket + per-workgroup slots), consecutive launches over DIFFERENT data
+    (8 buffers of 64-72 MiB at odd offsets, cycled, with a new seed each
+    launch), so a slot read before its store landed, or a stale slot of the
+    previous launch, gives a wrong CRC. Every result is checked against the
+    oracle: CRC(buffer j, seed) = crc32c_combine(seed, CRC(buffer j, 0), n_j)
+    (linearity, crc.cpp:393-405), the 8 base CRCs computed on the host."""
+    torch = torch_dev
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    nbuf, launches = 8, 1000
+    lens = [(64 << 20) + j * (1 << 20) + 4099 * j + 1 for j in range(nbuf)]
+    offs = [1 + 7 * j for j in range(nbuf)]
+    bufs = []
+    for j in range(nbuf):
+        b = torch.empty(lens[j] + 64, dtype=torch.uint8, device="cuda")
+        ck.fill_splitmix(b, b.numel(), b.numel(), 1, 0x5EED0B00 + j)
+        bufs.append(b)
+    base = [oracle.crc32c(bufs[j].cpu().numpy()[offs[j]:offs[j] + lens[j]], 0) for j in range(nbuf)]
+    rng = np.random.default_rng(0x5EED0B10)
+    seeds = [int(x) for x in rng.integers(1, 1 << 32, launches, dtype=np.uint64)]
+    out = torch.zeros(launches, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    for k in range(launches):
+        j = k % nbuf
+        ck.extend_device(bufs[j].data_ptr() + offs[j], lens[j], seeds[k], out[k:k + 1], stream=st)
+    torch.cuda.synchronize()
+    got = _u32(out)
+    # every launch filled the grid (the 16 KiB chunk floor: >= 16 waves x cus chunks)
+    assert min(lens) >= 16 * cus * (16 << 10)
+    for k in range(launches):
+        j = k % nbuf
+        assert int(got[k]) == oracle.combine(seeds[k], base[j], lens[j]), (k, j)
+    del bufs
+
+
+def test_extend_device_graph_capture(torch_dev, oracle):
+    """a long-buffer call over 256 KiB is refused (-ENOTSUP) while
+    its stream is captured into a HIP graph (its reduce state is per stream);
+    up to 256 KiB (one workgroup, no state) it captures and replays exactly."""
+    torch = torch_dev
+    d = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0C00)
+    host = d.cpu().numpy()
+    out = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ck.extend_device(d.data_ptr() + 3, 128 << 10, 9, out[0:1])  # the device's table image exists before capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    refused = []
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream()
+        ck.extend_device(d.data_ptr() + 3, 128 << 10, 9, out[0:1], stream=st)
+        try:
+            ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[1:2], stream=st)
+        except ck.CrcError as e:
+            refused.append(e.code)
+    assert refused == [-95]  # ENOTSUP
+    for seed_fill in (0x5EED0C01, 0x5EED0C02):  # new data, same graph
+        ck.fill_splitmix(d, d.numel(), d.numel(), 1, seed_fill)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(_u32(out)[0]) == oracle.crc32c(d.cpu().numpy()[3:3 + (128 << 10)], 9)
+    assert host is not None
+    # the same stream outside capture runs the long call again
+    ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[1:2])
+    torch.cuda.synchronize()
+    assert int(_u32(out)[1]) == oracle.crc32c(d.cpu().numpy()[3:3 + (1 << 20) - 64], 9)
+
+
 @pytest.mark.parametrize("shape", [(0, 0), (64, 1), (64, 2), (32, 1), (32, 2), (32, 3)])
 def test_extend_device_aligned_grid_edges(torch_dev, oracle, shape):
     # The chunk grid is anchored at the first 4 KiB boundary at or after the

@@ -68,9 +68,12 @@ def test_shards_are_disjoint(config):
 def test_bench_defaults():
     a = bench.parse([])
     assert a.gpus == 1 and a.config == "c2" and a.steps > 0 and a.warmup > 0
-    # N > 1 defaults to the 8-GPU config's shard (C4: 32 Ki x 1 MiB per GPU)
-    a = bench.parse(["--gpus", "8"])
-    assert a.config == "c4" and bench.CONFIGS["c4"]["count"] * 8 == 256 * 1024
+    # Every N runs the same per-GPU workload (C2 per GPU, weak scaling), so the
+    # driver's 1/2/4/8-GPU lines compare like with like;
+    # the 8-GPU config's shard stays available as --config c4.
+    for n in (2, 4, 8):
+        assert bench.parse(["--gpus", str(n)]).config == "c2"
+    assert bench.CONFIGS["c4"]["count"] * 8 == 256 * 1024
 
 
 def _run_bench(*argv, timeout=240):
@@ -100,6 +103,21 @@ def test_launcher_two_ranks_cpu(oracle):
     # whole-job value = both ranks' bytes over the slowest rank's wall time
     slow = max(p["wall_s"] for p in res["per_rank"])
     assert res["value"] == pytest.approx(2 * 3 * 64 * 65536 / slow / (1 << 30), rel=0.05)
+
+
+def test_scaling_lines_name_one_workload():
+    """The N = 1 and N = 2 lines of a scaling sweep (plain `--gpus 1`, and
+    `--gpus 2` through bench.py's own launcher) name the same per-GPU
+    workload, the metric's C2 config (VERDICT r3 next #4)."""
+    lines = {}
+    for n in (1, 2):
+        r = _run_bench("--gpus", str(n), "--cpu-rehearsal", "--steps", "2", "--warmup", "1")
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+        assert res["n_gpus"] == n and res["scaling"] == "weak"
+        lines[n] = res["config"]
+    assert lines[1]["workload"] == lines[2]["workload"] == bench.CONFIGS["c2"]["workload"]
+    assert lines[1]["config"] == lines[2]["config"] == "c2"
 
 
 def test_launcher_refuses_missing_gpus():
