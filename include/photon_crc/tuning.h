@@ -93,6 +93,17 @@ void photon_crc_test_fail_next(int n);
  * Returns the number of words written to out[n], or a negative error. */
 int photon_crc_test_tables(int which, uint32_t* out, int n);
 
+/* The long-buffer plan and launch constants (photonlibos_amd/csrc/long_plan.h)
+ * the library would use for a buffer at address `addr` (not dereferenced) of
+ * n bytes on a device with `cus` compute units, shape as
+ * photon_crc_set_long_shape (0, 0 = automatic), CRC-64 constants if crc64.
+ * out[0..8] = head, chunk, nchunks, last, rounds, grid, stride, lead, lanes;
+ * then CRC-32C: xsb[32], xb[32], zt[16], ft[grid]; CRC-64: xsb[64], x,
+ * zt[16], ft[grid] (one word each). For CPU tests that replay the kernels'
+ * staged combine with the oracle. Returns the words written, or -EINVAL. */
+int photon_crc_test_long_plan(uint64_t addr, uint64_t n, int cus, int lanes, int rounds, int crc64, uint64_t* out,
+                              int nout);
+
 /* Test/bench utility (not on the checksum path): fill count buffers of
  * nbytes at d_base + i*stride with the splitmix64 byte stream of seed
  * (seed_base + i), i.e. word k = mix64(seed + (k+1)*0x9E3779B97F4A7C15),

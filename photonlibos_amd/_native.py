@@ -84,6 +84,8 @@ def _declare(L):
     # tuning / test hooks (include/photon_crc/tuning.h)
     fn("photon_crc_lanes_for", ctypes.c_int, u64)
     fn("photon_crc_test_fail_next", None, ctypes.c_int)
+    fn("photon_crc_test_long_plan", ctypes.c_int, u64, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+       vp, ctypes.c_int)
     fn("photon_crc32c_series_device", ctypes.c_int, vp, u32, u32, vp, vp)
     fn("photon_crc32c_combine_series_device", ctypes.c_int, vp, u32, u32, vp, vp)
     fn("photon_crc32c_trim_batch", ctypes.c_int, vp, vp, vp, u64, vp, vp, vp)

@@ -940,6 +940,31 @@ int photon_crc_test_tables(int which, uint32_t* out, int n) {
     return fail(-EINVAL, "bad table id");
 }
 
+int photon_crc_test_long_plan(uint64_t addr, uint64_t n, int cus, int lanes, int rounds, int crc64, uint64_t* out,
+                              int nout) {
+    if (!out || cus < 1 || (lanes != 0 && lanes != 32 && lanes != 64) || rounds < 0 || rounds > 64)
+        return fail(-EINVAL, "bad plan arguments");
+    const LongPlan lp = long_plan_for(reinterpret_cast<const void*>(addr), n, cus,
+                                      (uint32_t)lanes | (uint32_t)rounds << 8, 0, crc64 != 0);
+    const LongPowers& pw = long_powers(lp, crc64 != 0);
+    std::vector<uint64_t> w = {lp.head, lp.chunk, lp.nchunks, lp.last, lp.rounds, lp.grid, lp.stride, lp.lead,
+                               (uint64_t)lp.lanes};
+    if (crc64) {
+        w.insert(w.end(), pw.xsb64, pw.xsb64 + 64);
+        w.push_back(pw.x64);
+        w.insert(w.end(), pw.zt64, pw.zt64 + 16);
+        w.insert(w.end(), pw.ft64, pw.ft64 + lp.grid);
+    } else {
+        w.insert(w.end(), pw.xsb32, pw.xsb32 + 32);
+        w.insert(w.end(), pw.xb32, pw.xb32 + 32);
+        w.insert(w.end(), pw.zt32, pw.zt32 + 16);
+        w.insert(w.end(), pw.ft32, pw.ft32 + lp.grid);
+    }
+    if ((int)w.size() > nout) return fail(-EINVAL, "short output");
+    memcpy(out, w.data(), w.size() * 8);
+    return (int)w.size();
+}
+
 int photon_crc_set_generic_rows(int rows_per_step) {
     if (rows_per_step != -1 && rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
         return fail(-EINVAL, "rows per step must be -1 (auto), 0 (fused kernel), 2, 4 or 8");
@@ -1412,20 +1437,7 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     const LongPlan lp = long_plan(d_data, nbytes, cus, true);
     const LongPowers& pw = long_powers(lp, true);
     Long64Args a{};
-    a.data = static_cast<const uint8_t*>(d_data);
-    a.nbytes = nbytes;
-    a.head = lp.head;
-    a.chunk = lp.chunk;
-    a.nchunks = lp.nchunks;
-    a.seed = seed;
-    a.jinv = pw.jinv64;
-    a.xs = pw.xs64;
-    a.stride = lp.stride;
-    a.out = d_out;
-    memcpy(a.xp, pw.xpj64, sizeof(a.xp));
-    memcpy(a.xq, pw.p64[1], sizeof(a.xq));
-    memcpy(a.xr, pw.p64[2], sizeof(a.xr));
-    memcpy(a.xsb, pw.xsb64, sizeof(a.xsb));
+    long_args64(&a, lp, pw, d_data, seed, d_out);
     return long_launch(st, lp.grid, "crc64_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint64_t*>(state);
         a.tbase = base;
@@ -1523,19 +1535,7 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
     const LongPlan lp = long_plan(d_data, nbytes, cus, false);
     const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
-    a.data = static_cast<const uint8_t*>(d_data);
-    a.nbytes = nbytes;
-    a.head = lp.head;
-    a.chunk = lp.chunk;
-    a.nchunks = lp.nchunks;
-    a.seed = seed;
-    a.jinv = pw.jinv32;
-    a.xs = pw.xs32;
-    a.stride = lp.stride;
-    a.out = d_out;
-    memcpy(a.xp, pw.xpj32, sizeof(a.xp));
-    memcpy(a.xq, pw.p32[1], sizeof(a.xq));
-    memcpy(a.xr, pw.p32[2], sizeof(a.xr));
+    long_args(&a, lp, pw, d_data, seed, d_out);
     return long_launch(st, lp.grid, "crc32c_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint32_t*>(state);
         a.tbase = base;

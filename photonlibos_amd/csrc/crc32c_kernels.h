@@ -1389,46 +1389,53 @@ __global__ void crc32c_trim_kernel(const photon_crc_component* all, const photon
 
 // ------------------------------------------------------- one long buffer
 // photon_crc32c_extend_device (crc32c_extend, crc32c.h:30-33, over ONE
-// device buffer) in ONE launch that fills the chip. The buffer is cut into T
-// chunks on a grid anchored at an ABSOLUTE 4 KiB boundary A (the first one at
-// or after the data start): chunk 0 = [data, A) (the unaligned head, 0..4095
-// bytes, with the seed), chunk t >= 1 = [A + (t-1) chunk, A + t chunk), the
-// last one cut at the end of the buffer (L_last bytes, 0 < L_last <= chunk).
-// Every chunk but the two ends is aligned and whole, so no chunk has a masked
-// head or a byte-serial tail (round 3's first form anchored the grid at the
-// END of the buffer: at the reference's base+1 every chunk paid both).
-// By linearity (crc.cpp:393-405) the CRC is the XOR of the chunks' CRCs each
-// shifted by the bytes after it: with X = x^(8 chunk) and c'_t = crc_t
-// (t < T-1), c'_(T-1) = crc_(T-1) * x^(8 (chunk - L_last)) (the last chunk as
-// if it were whole), CRC = J * XOR_t c'_t X^(T-1-t), J = x^-(8 (chunk -
-// L_last)). A lane group's chunks are t_k = t_0 + k S (S = lane groups in the
-// grid), so it accumulates them in Horner form, acc <- acc X^S ^ c'_t: ONE
-// multiply by the launch constant X^S per chunk, done lane-parallel (each of
-// 32 lanes holds one basis word of X^S, a select and a 32-lane XOR), and at
-// the end one multiply by the group's factor J X^(T-1-t_last), lane-parallel
-// too (its basis words computed after the group's first chunk, off the
-// launch's critical tail). Round 3's first form: three 32-step bit-serial
-// multiplies per chunk (~600 VALU on every lane) and J at the very end.
-// Waves XOR-reduce in registers and LDS; workgroups through long_reduce.
+// device buffer of more than 256 KiB) in ONE launch that fills the chip. The
+// cut (long_plan.h): the head [data, A) up to the first 4 KiB boundary A
+// carries the seed; the body [A, end) is T chunks of `chunk` bytes (the last
+// one L bytes), every one aligned and whole but the last, so no body chunk
+// has a masked head. R*S slots (S lane groups, R rounds): slot v belongs to
+// group v % S in round v / S; body chunk t sits in slot v = t + D, D = R*S - T
+// (empty slots at the FRONT: leading zeros do not change a CRC), the head in
+// slot D - 1 (slot -1, a round before group S-1's first, when D = 0).
+// By linearity (crc.cpp:393-405), with X = x^(8 chunk) and J = x^-(8 (chunk
+// - L)): CRC = J * XOR_v c_v X^(R S - 1 - v) ^ c_last, the last (short) body
+// chunk entering with factor 1 (J X^0 x^(8 (chunk - L)) = 1). With v = g +
+// r S and g = (16 b + w) GPW + grp (workgroup b, wave w, group grp):
+//   X^(R S - 1 - v) = X^(S (R - 1 - r)) X^(GPW - 1 - grp) Z^(15 - w) Y^(grid - 1 - b)
+// (Z = X^GPW, Y = Z^16), so the factors are applied in stages, each a
+// multiplication by ONE constant per group / wave / workgroup, done
+// lane-parallel (lane l of a 32-lane half holds basis word l of the
+// constant: a select and a 32-lane XOR, mul_lanes):
+//   group: Horner over its rounds, acc <- acc X^S ^ c (basis words of X^S
+//          from the host);
+//   wave (GPW = 2): acc_0 X ^ acc_1 (basis words of X from the host);
+//   wave: * Z^(15 - w) (basis words computed at kernel start from the
+//          host's constant, 31 select steps per lane, off the tail);
+//   workgroup: XOR of its waves in LDS, * J Y^(grid - 1 - b) (wave 0, basis
+//          words computed at kernel start), ^ c_last in the last workgroup;
+//   grid: the workgroups' values XORed by long_reduce.
+// Round 3 multiplied every group's accumulator by its own J X^(T - 1 - t_last)
+// after the chunk loop: three dependent 32-step bit-serial multiplies (1.7
+// µs of the 1 GiB launch's tail; CRC-64: two 64-step ones).
+constexpr uint32_t kLongMaxFt = 256;  // workgroups of a long launch (the workgroup factors in the arguments)
 struct LongArgs {
     const uint8_t* data;
-    uint64_t nbytes;
-    uint64_t head;      // bytes of chunk 0 = A - data (the whole buffer when T == 1)
-    uint64_t chunk;
-    uint64_t nchunks;   // T
-    uint32_t seed;
-    uint32_t jinv;      // x^(8 (chunk - L_last)) (kOne when T == 1); J jinv = 1, so the kernel folds the
-                        // last chunk in after its group's factor instead (probe ablation 2 multiplies)
-    uint32_t xs;        // X^S
+    uint64_t head;      // bytes before A (0..4095): slot D - 1, with the seed
+    uint64_t chunk;     // body chunk bytes (a 1 KiB multiple)
+    int64_t nchunks;    // T
+    uint64_t last;      // L: bytes of the last body chunk
+    int64_t lead;       // D = R S - T
     uint64_t stride;    // S: lane groups in the grid
+    uint32_t rounds;    // R
+    uint32_t seed;
     uint32_t* out;
     uint32_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes; grid > 1 only)
     uint64_t tbase;     // long_reduce: the state's ticket count before this launch
     uint32_t treset;    // long_reduce: put the ticket back to 0 (a leased state)
-    uint32_t xp[64];    // J X^j, J = x^-(8 (chunk - L_last)) (kOne when T == 1): every group's
-                        // final factor carries J once, so the total needs no last multiply
-    uint32_t xq[64];    // X^(64 j)
-    uint32_t xr[64];    // X^(4096 j)
+    uint32_t xsb[32];   // basis words of X^S
+    uint32_t xb[32];    // basis words of X (GPW = 2)
+    uint32_t zt[16];    // Z^(15 - w)
+    uint32_t ft[kLongMaxFt];  // J Y^(grid - 1 - b)
 };
 
 // The long kernels' cross-workgroup XOR, called by EVERY thread of wave 0
@@ -1516,15 +1523,6 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64
     }
 }
 
-// crc * J X^m for m < 2^18 from the three power tables (xp holds J X^j).
-template <typename A>
-__device__ __forceinline__ uint32_t long_shift(uint32_t crc, uint64_t m, const A& a) {
-    crc = mulmod(crc, a.xp[m & 63u]);
-    if (m >= 64) crc = mulmod(crc, a.xq[(m >> 6) & 63u]);
-    if (m >= 4096) crc = mulmod(crc, a.xr[(m >> 12) & 63u]);
-    return crc;
-}
-
 // v * x mod P (reflected: bit j = coefficient of x^(31-j)).
 __device__ __forceinline__ uint32_t mulx(uint32_t v) { return (v >> 1) ^ ((0u - (v & 1u)) & kPoly); }
 
@@ -1542,28 +1540,72 @@ __device__ __forceinline__ uint32_t mul_lanes(uint32_t v, uint32_t bw, uint32_t 
     return group_xor<32>(((v >> l32) & 1u) ? bw : 0u);
 }
 
-// The chunk of a long buffer: [*p, *p + *n).
+// The bytes of slot v: [*p, *p + *n) and the seed (empty slots: 0 bytes).
 template <typename A>
-__device__ __forceinline__ void long_chunk(const A& a, uint64_t t, const uint8_t** p, uint64_t* n) {
-    if (t == 0) {
+__device__ __forceinline__ void long_slot(const A& a, int64_t v, const uint8_t** p, uint64_t* n, bool* last) {
+    const int64_t t = v - a.lead;  // body chunk, or -1 for the head
+    *last = t == a.nchunks - 1;
+    if (t == -1) {
         *p = a.data;
         *n = a.head;
-        return;
+    } else if (t < 0) {
+        *p = a.data;
+        *n = 0;
+    } else {
+        *p = a.data + a.head + (uint64_t)t * a.chunk;
+        *n = *last ? a.last : a.chunk;
     }
-    const uint64_t off = a.head + (t - 1) * a.chunk;
-    *p = a.data + off;
-    *n = t >= a.nchunks ? 0 : (a.nbytes - off < a.chunk ? a.nbytes - off : a.chunk);
+}
+
+// Every wave: its workgroup's value (after the wave and workgroup factors),
+// valid on lane 0 of wave 0 and written through long_reduce. `acc` is the
+// group's Horner value (valid on every lane of the group), `lastc` the last
+// body chunk's CRC where this group holds it (else 0). STAMP / ABL: as
+// long_run. W is the CRC word type (uint32_t here; crc64_kernels.h has its
+// own).
+template <int G, bool STAMP = false, int ABL = 0>
+__device__ __forceinline__ void long_finish(const LongArgs& a, uint32_t acc, uint32_t lastc, uint32_t bw_x,
+                                            uint32_t bw_z, uint32_t bw_f, uint32_t* red) {
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_id(), l32 = lane & 31u;
+    uint32_t v = acc;
+    if constexpr (G == 32) {  // acc_0 * X ^ acc_1: the wave's two groups
+        const uint32_t m = mul_lanes(acc, bw_x, l32);
+        v = lane < 32 ? m : acc;
+        v ^= (uint32_t)__shfl_xor((int)v, 32, 64);
+        lastc ^= (uint32_t)__shfl_xor((int)lastc, 32, 64);  // the other group's (one of them is 0)
+    }
+    if constexpr (!(ABL & 32)) v = mul_lanes(v, bw_z, l32);  // * Z^(15 - w)
+    if (lane == 0) {
+        red[wave] = v;
+        red[kWaves + wave] = lastc;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t u = 0, e = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            u ^= red[w];
+            e ^= red[kWaves + w];
+        }
+        if constexpr (!(ABL & 32)) u = mul_lanes(u, bw_f, l32);  // * J Y^(grid - 1 - b)
+        u ^= e;
+        if constexpr (ABL & 16) {
+            if (lane == 0) *a.out = u;
+        } else if constexpr (ABL & 8) {
+            long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase,
+                                                                a.treset);
+        } else {
+            long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
+        }
+    }
 }
 
 // G lanes per chunk (64: one wavefront; 32: two chunks per wavefront), U rows
 // per step. STAMP and ABL are for the bench-only probe (probes.hip): STAMP =
 // per-wave s_memrealtime stamps into t (8 words per wave); ABL bits = cost
-// attribution, results NOT the CRC unless noted: 1 = chunks without the
-// lead-row preload (correct), 2 = every chunk shifted on its own, no Horner
-// (correct), 4 = no final shift and no cross-workgroup reduce, 8 = the
-// reduce WITH the agent-scope release/acquire (correct), 16 = no
-// cross-workgroup reduce (the final shift kept), 32 = no final shift (the
-// reduce kept).
+// attribution, results NOT the CRC unless noted: 8 = the reduce WITH the
+// agent-scope release/acquire (correct), 16 = no cross-workgroup reduce
+// (each workgroup writes its value), 32 = no wave and workgroup factors.
 template <int G, int U, bool STAMP = false, int ABL = 0>
 __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc, uint32_t* lds, uint32_t* red,
                                          uint64_t* t) {
@@ -1579,58 +1621,38 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
     const uint32_t wave = wave_id();
     const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr la = lane_addr(lane);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
     const uint32_t l32 = lane & 31u;
-    // The group's chunks: tf, tf + S, ..., tl (none when tf >= T).
-    const uint64_t tf = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
-    const uint32_t bw = (ABL & 2) ? 0u : basis_word(a.xs, l32);  // basis word of X^S
+    const int64_t S = (int64_t)a.stride;
+    const int64_t g = ((int64_t)blockIdx.x * kWaves + wave) * GPW + grp;
+    // Basis words: X^S and X from the host; Z^(15 - w) and (wave 0) the
+    // workgroup factor computed here, before any chunk.
+    const uint32_t bw_xs = a.xsb[l32];
+    const uint32_t bw_x = G == 32 ? a.xb[l32] : 0u;
+    const uint32_t bw_z = basis_word(a.zt[wave], l32);
+    const uint32_t bw_f = wave == 0 ? basis_word(a.ft[blockIdx.x], l32) : 0u;
     uint32_t acc = 0, lastc = 0;
-    uint64_t tl = 0;
-    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
-        const uint64_t tc = wv * GPW + grp;
-        const bool active = tc < a.nchunks;
+    // Rounds; a first round -1 when the head is slot -1 (D = 0: group S-1).
+    for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
+        const int64_t v = g + (int64_t)r * S;
         const uint8_t* p;
         uint64_t n;
-        long_chunk(a, tc, &p, &n);
-        const uint32_t crc = buffer_crc<G, U, (ABL & 1) ? false : PCRC_LONG_LEAD>(lds, p, n, tc ? 0u : a.seed, gl, la);
-        if constexpr (ABL & 2) {
-            if (active) acc ^= long_shift(tc == a.nchunks - 1 ? mulmod(crc, a.jinv) : crc, a.nchunks - 1 - tc, a);
-        } else {
-            // The last chunk (always its group's last) is kept out of the
-            // fold: (acc X^S ^ crc jinv) J = acc X^S J ^ crc, so it needs no
-            // multiply (a general GF(2) multiply here, 32 unrolled steps,
-            // made the compiler reduce the row loop's blocks one at a time:
-            // 32 waits per 4 rows instead of 22).
-            const bool last = tc == a.nchunks - 1;
-            const uint32_t m = mul_lanes(acc, bw, l32);  // every lane: the halves stay convergent
-            if (active) {
-                acc = last ? m : m ^ crc;
-                lastc = last ? crc : lastc;
-                tl = tc;
-            }
-        }
+        bool last;
+        long_slot(a, v, &p, &n, &last);
+        const uint32_t seed = v == a.lead - 1 ? a.seed : 0u;  // the head carries the seed
+        uint32_t crc = 0;
+        if (__ballot(n != 0 || seed != 0))  // a wave with only empty slots skips the round's loads
+            crc = buffer_crc<G, U, PCRC_LONG_LEAD>(lds, p, n, seed, gl, la);
+        // The last chunk stays out of the Horner fold (it enters with factor
+        // 1); keeping a general multiply out of this loop keeps the row loop's
+        // schedule (round 3: a 32-step multiply here made the compiler reduce
+        // the blocks one at a time).
+        const uint32_t m = mul_lanes(acc, bw_xs, l32);  // every lane: the halves stay convergent
+        acc = last ? m : m ^ crc;
+        lastc = last ? crc : lastc;
     }
-    (void)tf;
-    // acc * J X^(T-1-tl) (three table multiplies, once per group), then the last chunk.
-    if constexpr (!(ABL & 6) && !(ABL & 32)) acc = long_shift(acc, a.nchunks - 1 - tl, a) ^ lastc;
     uint64_t t_body = 0;
     if constexpr (STAMP) t_body = __builtin_amdgcn_s_memrealtime();
-    acc = group_xor<64>(gl == 0 ? acc : 0u);  // the groups' first lanes hold their values
-    if (lane == 0) red[wave] = acc;
-    __syncthreads();
-    if (wave == 0) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        if constexpr (ABL & 20) {
-            if (lane == 0) *a.out = v;
-        } else if constexpr (ABL & 8) {
-            long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(v, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase,
-                                                                a.treset);
-        } else {
-            long_reduce(v, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
-        }
-    }
+    long_finish<G, STAMP, ABL>(a, acc, lastc, bw_x, bw_z, bw_f, red);
     if constexpr (STAMP) {
         const uint64_t c1 = __builtin_amdgcn_s_memtime();
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -1651,7 +1673,7 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
 template <int G, int U>
 __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneConsts kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
-    __shared__ uint32_t red[kWaves];
+    __shared__ uint32_t red[2 * kWaves];
     long_run<G, U>(a, kc, lds, red, nullptr);
 }
 

@@ -654,25 +654,31 @@ __global__ void crc64_msg_fold_kernel(const photon_crc_iovec* iov, const uint64_
 }
 
 // photon_crc64ecma_extend_device in one launch: crc32c_long_kernel's scheme
-// (crc32c_kernels.h "one long buffer": chunk grid anchored at a 4 KiB
-// boundary, Horner accumulation per lane group with a lane-parallel multiply
-// by X^S, one general shift per group, workgroups XOR-reduced by
-// long_reduce) on the raw CRC-64 register: chunk 0 starts from ~seed, the
-// others from 0, the result is inverted (crc.cpp:119-122).
+// (crc32c_kernels.h "one long buffer": the same cut and slots, Horner per
+// lane group with a lane-parallel multiply by X^S, the wave / workgroup
+// factors applied in stages, workgroups XOR-reduced by long_reduce) on the
+// raw CRC-64 register: the head starts from ~seed, body chunks from 0, the
+// result is inverted (crc.cpp:119-122). A 64-bit lane-parallel multiply
+// takes 64 basis words: one per lane of a wave, or two per lane of a 32-lane
+// group. Round 3 applied each group's own factor after the chunk loop with
+// two dependent 64-step bit-serial multiplies per wave.
 struct Long64Args {
     const uint8_t* data;
-    uint64_t nbytes, head, chunk, nchunks;
-    uint64_t seed;
-    uint64_t jinv, xs;  // as LongArgs, mod P64
+    uint64_t head, chunk;
+    int64_t nchunks;
+    uint64_t last;
+    int64_t lead;
     uint64_t stride;
+    uint32_t rounds;
+    uint64_t seed;
     uint64_t* out;
     uint64_t* acc;      // long_reduce state (8 + 8 * kLongMaxGrid bytes; grid > 1 only)
     uint64_t tbase;     // long_reduce: the state's ticket count before this launch
     uint32_t treset;    // long_reduce: put the ticket back to 0 (a leased state)
-    uint64_t xp[64];    // J X^j, X = x^(8*chunk) mod P64
-    uint64_t xq[64];    // X^(64 j)
-    uint64_t xr[64];    // X^(4096 j)
+    uint64_t x;         // X (its basis words are computed on the device, G = 32 only)
     uint64_t xsb[64];   // basis words of X^S: (1 << i) * X^S (host-computed, long_powers)
+    uint64_t zt[16];    // Z^(15 - w)
+    uint64_t ft[kLongMaxFt];  // J Y^(grid - 1 - b)
 };
 
 __device__ __forceinline__ uint64_t mulx64(uint64_t v) { return (v >> 1) ^ ((0ull - (v & 1ull)) & kPoly64); }
@@ -690,63 +696,79 @@ __device__ __forceinline__ uint64_t xor_lanes64(uint64_t v, int width) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// v * c for a v held by every lane of a wave, lane l holding basis word l of c.
+__device__ __forceinline__ uint64_t mul_wave64(uint64_t v, uint64_t bw, uint32_t lane) {
+    return xor_lanes64(((v >> lane) & 1ull) ? bw : 0ull, 64);
+}
+
 template <int G>
 __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneConsts64 kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
-    __shared__ uint64_t red[kWaves];
+    __shared__ uint64_t red[2 * kWaves];
     build_tables64<G>(lds, kc);
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
     const uint32_t gl = lane & (G - 1), grp = lane / G;
     const LaneAddr64 la = lane_addr64(lane);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    const int64_t S = (int64_t)a.stride;
+    const int64_t g = ((int64_t)blockIdx.x * kWaves + wave) * GPW + grp;
     // Basis words of X^S from the host: 64 lanes one each (G = 64), or two
     // per lane of a 32-lane half (bits l and l + 32). Nothing but the chunk
-    // loop's own work sits in the loop (crc32c_kernels.h long_run: any
-    // general multiply there serialises the row loop's lookups).
+    // loop's own work sits in the loop (crc32c_kernels.h long_run).
     const uint32_t l = G == 64 ? lane : (lane & 31u);
     const uint64_t bw0 = a.xsb[l], bw1 = G == 64 ? 0ull : a.xsb[l + 32];
-    auto mul_basis_lanes = [&](uint64_t v) {
-        uint64_t term = ((v >> l) & 1ull) ? bw0 : 0ull;
-        if (G != 64) term ^= ((v >> (l + 32)) & 1ull) ? bw1 : 0ull;
+    auto mul_group = [&](uint64_t v, uint64_t b0, uint64_t b1) {
+        uint64_t term = ((v >> l) & 1ull) ? b0 : 0ull;
+        if (G != 64) term ^= ((v >> (l + 32)) & 1ull) ? b1 : 0ull;
         return xor_lanes64(term, G == 64 ? 64 : 32);
     };
+    // The wave's and (wave 0) the workgroup's factor: basis words computed
+    // here, one per lane, before any chunk; X's for the 32-lane form.
+    const uint64_t bw_z = basis_word64(a.zt[wave], lane);
+    const uint64_t bw_f = wave == 0 ? basis_word64(a.ft[blockIdx.x], lane) : 0ull;
+    const uint64_t bx0 = G == 32 ? basis_word64(a.x, l) : 0ull, bx1 = G == 32 ? basis_word64(a.x, l + 32) : 0ull;
     uint64_t acc = 0, lastc = 0;  // uniform across the group (reg and the lane XOR are)
-    for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < a.nchunks; wv += nwaves) {
-        const uint64_t t = wv * GPW + grp;
-        const bool active = t < a.nchunks;
+    for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
+        const int64_t v = g + (int64_t)r * S;
         const uint8_t* p;
         uint64_t n;
-        long_chunk(a, t, &p, &n);
-        uint64_t reg = buffer_reg64<G>(lds, p, n, t ? 0ull : ~a.seed, gl, lane, la);  // valid on gl == 0
-        reg = __shfl(reg, lane & ~(uint32_t)(G - 1), 64);                        // the whole group
-        // the last chunk after the group's factor (J x^(8(chunk-L)) = 1; long_run)
-        const bool last = t == a.nchunks - 1;
-        const uint64_t m = mul_basis_lanes(acc);
-        if (active) {
-            acc = last ? m : m ^ reg;
-            lastc = last ? reg : lastc;
+        bool last;
+        long_slot(a, v, &p, &n, &last);
+        const bool head = v == a.lead - 1;  // the head carries the (inverted) seed
+        uint64_t reg = 0;
+        if (__ballot(n != 0 || head)) {
+            reg = buffer_reg64<G>(lds, p, n, head ? ~a.seed : 0ull, gl, lane, la);  // valid on gl == 0
+            reg = __shfl(reg, lane & ~(uint32_t)(G - 1), 64);                        // the whole group
         }
+        const uint64_t m = mul_group(acc, bw0, bw1);
+        acc = last ? m : m ^ reg;
+        lastc = last ? reg : lastc;
     }
-    // The group's final factor J X^(T-1-tl) (tl its last chunk), applied to the
-    // group-uniform accumulator with bit-serial multiplies after the loop.
-    const uint64_t t0 = ((uint64_t)blockIdx.x * kWaves + wave) * GPW + grp;
-    if (t0 < a.nchunks) {
-        const uint64_t m = (a.nchunks - 1 - t0) % a.stride;  // T-1-tl
-        uint64_t k = a.xp[m & 63u];
-        if (m >= 64) k = mulmod64(k, a.xq[(m >> 6) & 63u]);
-        if (m >= 4096) k = mulmod64(k, a.xr[(m >> 12) & 63u]);
-        acc = mulmod64(acc, k) ^ lastc;
+    uint64_t v = acc;
+    if constexpr (G == 32) {  // acc_0 * X ^ acc_1
+        const uint64_t m = mul_group(acc, bx0, bx1);
+        v = lane < 32 ? m : acc;
+        v ^= ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), 32, 64) << 32) |
+             (uint32_t)__shfl_xor((int)(uint32_t)v, 32, 64);
+        lastc ^= ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(lastc >> 32), 32, 64) << 32) |
+                 (uint32_t)__shfl_xor((int)(uint32_t)lastc, 32, 64);
     }
-    acc = xor_lanes64(gl == 0 ? acc : 0ull, 64);
-    if (lane == 0) red[wave] = acc;
+    v = mul_wave64(v, bw_z, lane);  // * Z^(15 - w)
+    if (lane == 0) {
+        red[wave] = v;
+        red[kWaves + wave] = lastc;
+    }
     __syncthreads();
     if (wave == 0) {
-        uint64_t v = 0;
+        uint64_t u = 0, e = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) v ^= red[w];
-        long_reduce(v, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122: inverted out
+        for (int w = 0; w < kWaves; ++w) {
+            u ^= red[w];
+            e ^= red[kWaves + w];
+        }
+        u = mul_wave64(u, bw_f, lane) ^ e;  // * J Y^(grid - 1 - b), then the last chunk
+        long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122: inverted out
     }
 }
 

@@ -1,8 +1,25 @@
 // long_plan.h -- host side of the one-long-buffer kernels (crc32c_kernels.h
 // "one long buffer", crc64_kernels.h crc64_long_kernel): how a buffer is cut
-// into chunks and the launch constants of a cut. Shared by the product
-// (crc32c_device.hip) and the bench-only probes (probes.hip), so a probe
-// times exactly the product's plan.
+// into chunks, which lane group takes which chunk, and the launch constants
+// of a cut. Shared by the product (crc32c_device.hip) and the bench-only
+// probes (probes.hip), so a probe times exactly the product's plan.
+//
+// The cut (round 4). A = the first 4 KiB boundary at or after the data start;
+// the HEAD [data, A) (0..4095 bytes) carries the seed; the BODY [A, end) is
+// cut into T chunks of `chunk` bytes (a 1 KiB multiple, >= 16 KiB), the last
+// one of L bytes (0 < L <= chunk). The grid has S lane groups and R rounds:
+// R*S virtual slots v = 0 .. R*S-1, slot v belongs to group v % S in round
+// v / S, and body chunk t sits in slot v = t + D with D = R*S - T: the
+// EMPTY slots are at the front (leading zeros do not change a CRC), so the
+// last chunk is always slot R*S-1 (group S-1, last round) and every group's
+// factor to the end of the buffer is X^(S-1-g) (X = x^(8 chunk)) whatever T
+// is. The head is slot D-1 -- an empty slot of group D-1 when D >= 1, or a
+// slot "-1" before group S-1's first round when D = 0 (then that group's
+// last chunk is the short one: at the reference's 1 GiB at buf+1, head +
+// last = one chunk exactly, so every group reads the same bytes). Round 3's
+// cut gave the head a slot of its own: T - 1 slots for the body, chunks
+// rounded up to 1 KiB, so at 1 GiB / buf+1 every group read 130 KiB instead
+// of 128 and 250 groups had half as much.
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -16,114 +33,115 @@
 namespace pcrc {
 
 struct LongPlan {
-    uint64_t head, chunk, nchunks, last, grid, stride;  // stride S: lane groups in the grid
+    uint64_t head;    // bytes before A (the head task; 0..4095)
+    uint64_t chunk;   // body chunk bytes
+    uint64_t nchunks; // T body chunks
+    uint64_t last;    // L: bytes of the last body chunk
+    uint64_t rounds;  // R
+    uint64_t grid;    // workgroups
+    uint64_t stride;  // S: lane groups in the grid
+    uint64_t lead;    // D = R*S - T: leading empty slots
     int lanes;
 };
 
 // force_chunk (bench-only probes): that chunk size instead of the computed one.
+// Long buffers only: the small kernel takes block spans up to 256 KiB.
 inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t shape, uint64_t force_chunk = 0,
                               bool crc64 = false) {
+    // automatic shape (r03 interleaved A/B, scripts/ab_long.py; re-measured in r04):
+    //  CRC-32C: 64 lanes x 2 rounds; 32 x 2 from 512 MiB; 64 x 1 from 1.5 GiB
+    //  CRC-64: 64 lanes; 1 round from 1 GiB, else 2
+    //  up to 256 KiB (CRC-64 only: CRC-32C has its small kernel): 1 round of
+    //  chunks of >= 4 KiB, one workgroup
     const bool small = n <= (256u << 10);
-    // automatic (r03 interleaved A/B, scripts/ab_long.py):
-    //  CRC-32C: 64 lanes x 2 rounds; 32 x 2 from 512 MiB (1 GiB 32x2 0.177 ms
-    //    vs 64x1 0.184 / 64x2 0.196; 256 MiB 64x2 0.060 vs 32x2 0.060 / 64x1
-    //    0.065); 64 x 1 from 1.5 GiB (2 GiB 0.326 vs 32x2 0.367, 4 GiB 0.633
-    //    vs 0.650; chunks near 128 KiB read slowly, profiles/r03e_ab_long_crc32c_big.jsonl)
-    //  CRC-64: 64 lanes; 1 round from 1 GiB, else 2 (1 GiB 64x1 0.176 vs 32x2
-    //    0.180 / 64x2 0.188; 2 GiB 0.331 / 0.372 / 0.336; 512 MiB 64x2 0.100
-    //    vs 0.109 / 0.111; profiles/r03e_ab_long_crc64_*.jsonl)
     const bool huge = n >= (512ull << 20), giant = n >= (3ull << 29);
-    const int lanes = small ? 64 : (shape & 0xff) ? (int)(shape & 0xff) : (huge && !giant && !crc64) ? 32 : 64;
-    const uint64_t one = crc64 ? n >= (1ull << 30) : giant;
-    const uint64_t rounds = small ? 1 : (shape >> 8) ? shape >> 8 : one ? 1 : 2;
+    const int lanes = (shape & 0xff) ? (int)(shape & 0xff) : (huge && !giant && !crc64) ? 32 : 64;
+    const uint64_t one = small || (crc64 ? n >= (1ull << 30) : giant);
+    uint64_t rounds = (shape >> 8) ? shape >> 8 : one ? 1 : 2;
     const uint64_t gpw = 64 / (uint64_t)lanes;
-    const uint64_t slots = small ? 16 : 16ull * (uint64_t)cus * gpw * rounds;
+    const uint64_t maxgrid = (uint64_t)cus < kLongMaxFt ? (uint64_t)cus : kLongMaxFt;
     LongPlan p{};
     p.lanes = lanes;
+    p.rounds = rounds;
     const uintptr_t d = reinterpret_cast<uintptr_t>(data);
-    const uint64_t head = ((d + 4095) & ~uintptr_t(4095)) - d;
-    if (head >= n || slots < 2) {  // one chunk: the whole buffer
-        p.head = n;
-        p.chunk = p.last = 4096;
-        p.nchunks = 1;
-    } else {
-        // whole rows, and at least 1 KiB: 512-byte-aligned chunks (32 lanes)
-        // read 13 % slower than 1 KiB-aligned ones (r03, scripts/ab_long.py)
-        const uint64_t m = n - head, gran = 1024;
-        uint64_t chunk = ((m + slots - 2) / (slots - 1) + gran - 1) / gran * gran;
-        const uint64_t lo = small ? 4096 : 16384;
-        if (chunk < lo) chunk = lo;
-        if (force_chunk) chunk = force_chunk;
-        while ((m + chunk - 1) / chunk + 1 > (1u << 18)) chunk <<= 1;  // the kernels' three 64-entry power tables
-        p.head = head;
-        p.chunk = chunk;
-        p.nchunks = 1 + (m + chunk - 1) / chunk;
-        p.last = m - (p.nchunks - 2) * chunk;
-    }
-    const uint64_t waves = (p.nchunks + gpw - 1) / gpw;
-    p.grid = (waves + kWaves - 1) / kWaves;
-    if (p.grid > (uint64_t)cus) p.grid = cus;
-    if (p.grid > kLongMaxGrid) p.grid = kLongMaxGrid;  // long_reduce's slots
-    p.stride = p.grid * kWaves * gpw;
+    uint64_t head = ((d + 4095) & ~uintptr_t(4095)) - d;
+    if (head > n) head = n;
+    const uint64_t m = n - head;  // 0 only when the whole buffer lies before A (then the head is all of it)
+    const uint64_t slots = 16ull * maxgrid * gpw * rounds;
+    uint64_t chunk = ((m + slots - 1) / slots + 1023) / 1024 * 1024;  // whole rows, 1 KiB aligned
+    const uint64_t lo = small ? 4096 : 16384;
+    if (chunk < lo) chunk = lo;
+    if (force_chunk) chunk = force_chunk;
+    p.head = head;
+    p.chunk = chunk;
+    p.nchunks = (m + chunk - 1) / chunk;
+    p.last = m ? m - (p.nchunks - 1) * chunk : chunk;  // no body: the head is slot R S - 1, factor 1
+    const uint64_t per_wg = 16ull * gpw * rounds;
+    p.grid = p.nchunks ? (p.nchunks + per_wg - 1) / per_wg : 1;
+    if (p.grid > maxgrid) p.grid = maxgrid;  // only with a forced chunk: then chunks > slots
+    p.stride = p.grid * 16ull * gpw;
+    if (p.nchunks > rounds * p.stride) p.rounds = rounds = (p.nchunks + p.stride - 1) / p.stride;
+    p.lead = rounds * p.stride - p.nchunks;
     return p;
 }
 
-// Launch constants of a plan, CRC-32C or CRC-64/ECMA: X^j, X^(64 j),
-// X^(4096 j) for j < 64 (X = x^(8 chunk)), X^S, and the last-chunk factors
-// x^(+-8 (chunk - last)). Computed on first use per (chunk, last, S) and
-// kept (callers repeat sizes and alignments).
+// Launch constants of a plan (CRC-32C or CRC-64/ECMA), X = x^(8 chunk):
+// X^S and X (basis words for the lane-parallel multiplies), Z^(15-w) with
+// Z = X^GPW (a wave's factor), and J Y^(grid-1-b) with Y = Z^16 and J =
+// x^-(8 (chunk - L)) (a workgroup's factor, J because the last chunk is
+// short: it enters the result with factor 1 instead). Computed on first use
+// per plan and kept (callers repeat sizes and alignments).
 struct LongPowers {
-    uint64_t chunk, last, stride;
-    uint32_t p32[3][64];
-    uint64_t p64[3][64];
-    uint32_t xpj32[64];  // J X^j: the kernels' xp (every group's final factor carries J)
-    uint64_t xpj64[64];
-    uint32_t xs32, j32, jinv32;
-    uint64_t xs64, j64, jinv64;
-    uint64_t xsb64[64];  // (1 << i) * X^S mod P64: crc64_long_kernel's lane basis words
+    uint64_t chunk, last, stride, grid, lanes;
+    uint32_t xsb32[32], xb32[32], zt32[16], ft32[kLongMaxFt];
+    uint64_t xsb64[64], x64, zt64[16], ft64[kLongMaxFt];
 };
 
 inline const LongPowers& long_powers(const LongPlan& lp, bool crc64) {
     static std::mutex mu;
     static std::vector<LongPowers*> cache[2];
     thread_local LongPowers overflow;
+    auto same = [&](const LongPowers* e) {
+        return e->chunk == lp.chunk && e->last == lp.last && e->stride == lp.stride && e->grid == lp.grid &&
+               e->lanes == (uint64_t)lp.lanes;
+    };
     {
         std::lock_guard<std::mutex> lk(mu);
         for (auto* e : cache[crc64])
-            if (e->chunk == lp.chunk && e->last == lp.last && e->stride == lp.stride) return *e;
+            if (same(e)) return *e;
     }
     LongPowers* t = new LongPowers();
     t->chunk = lp.chunk;
     t->last = lp.last;
     t->stride = lp.stride;
-    const uint64_t s = lp.stride, pad = 8 * (lp.chunk - lp.last);
-    for (int lvl = 0; lvl < 3; ++lvl) {
-        const uint64_t bits = (8 * lp.chunk) << (6 * lvl);  // X^(64^lvl)
-        if (crc64) {
-            const uint64_t y = xpow64(bits);
-            t->p64[lvl][0] = kOne64;
-            for (int j = 1; j < 64; ++j) t->p64[lvl][j] = mulmod64(t->p64[lvl][j - 1], y);
-        } else {
-            const uint32_t x = xpow(bits);
-            t->p32[lvl][0] = kOne;
-            for (int j = 1; j < 64; ++j) t->p32[lvl][j] = mulmod(t->p32[lvl][j - 1], x);
-        }
-    }
+    t->grid = lp.grid;
+    t->lanes = (uint64_t)lp.lanes;
+    const uint64_t gpw = 64 / (uint64_t)lp.lanes, pad = 8 * (lp.chunk - lp.last), bits = 8 * lp.chunk;
     if (crc64) {
-        t->xs64 = mulmod64(mulmod64(t->p64[0][s & 63], t->p64[1][(s >> 6) & 63]), t->p64[2][(s >> 12) & 63]);
-        t->jinv64 = xpow64(pad);
-        t->j64 = xpow64_inv(pad);
-        for (int j = 0; j < 64; ++j) t->xpj64[j] = mulmod64(t->p64[0][j], t->j64);
-        for (int i = 0; i < 64; ++i) t->xsb64[i] = mulmod64(1ull << i, t->xs64);
+        const uint64_t x = xpow64(bits), z = gpw == 2 ? mulmod64(x, x) : x;
+        uint64_t y = z;
+        for (int i = 0; i < 4; ++i) y = mulmod64(y, y);  // Z^16
+        const uint64_t xs = xpow64(bits * lp.stride);
+        for (int i = 0; i < 64; ++i) t->xsb64[i] = mulmod64(1ull << i, xs);
+        t->x64 = x;
+        uint64_t zk = kOne64;  // Z^(15 - w), w = 15 .. 0
+        for (int w = 15; w >= 0; --w, zk = mulmod64(zk, z)) t->zt64[w] = zk;
+        uint64_t f = xpow64_inv(pad);  // J Y^(grid - 1 - b), b = grid-1 .. 0
+        for (int64_t b = (int64_t)lp.grid - 1; b >= 0; --b, f = mulmod64(f, y)) t->ft64[b] = f;
     } else {
-        t->xs32 = mulmod(mulmod(t->p32[0][s & 63], t->p32[1][(s >> 6) & 63]), t->p32[2][(s >> 12) & 63]);
-        t->jinv32 = xpow(pad);
-        t->j32 = xpow_inv(pad);
-        for (int j = 0; j < 64; ++j) t->xpj32[j] = mulmod(t->p32[0][j], t->j32);
+        const uint32_t x = xpow(bits), z = gpw == 2 ? mulmod(x, x) : x;
+        uint32_t y = z;
+        for (int i = 0; i < 4; ++i) y = mulmod(y, y);
+        mul_basis(xpow(bits * lp.stride), t->xsb32);
+        mul_basis(x, t->xb32);
+        uint32_t zk = kOne;
+        for (int w = 15; w >= 0; --w, zk = mulmod(zk, z)) t->zt32[w] = zk;
+        uint32_t f = xpow_inv(pad);
+        for (int64_t b = (int64_t)lp.grid - 1; b >= 0; --b, f = mulmod(f, y)) t->ft32[b] = f;
     }
     std::lock_guard<std::mutex> lk(mu);
     for (auto* e : cache[crc64])
-        if (e->chunk == lp.chunk && e->last == lp.last && e->stride == lp.stride) {
+        if (same(e)) {
             delete t;
             return *e;
         }
@@ -134,6 +152,43 @@ inline const LongPowers& long_powers(const LongPlan& lp, bool crc64) {
     }
     cache[crc64].push_back(t);
     return *t;
+}
+
+// The kernels' arguments for a plan (CRC-32C; crc64 below).
+inline void long_args(LongArgs* a, const LongPlan& lp, const LongPowers& pw, const void* data, uint32_t seed,
+                      uint32_t* out) {
+    a->data = static_cast<const uint8_t*>(data);
+    a->head = lp.head;
+    a->chunk = lp.chunk;
+    a->nchunks = lp.nchunks;
+    a->last = lp.last;
+    a->lead = lp.lead;
+    a->stride = lp.stride;
+    a->rounds = (uint32_t)lp.rounds;
+    a->seed = seed;
+    a->out = out;
+    memcpy(a->xsb, pw.xsb32, sizeof(a->xsb));
+    memcpy(a->xb, pw.xb32, sizeof(a->xb));
+    memcpy(a->zt, pw.zt32, sizeof(a->zt));
+    memcpy(a->ft, pw.ft32, sizeof(uint32_t) * lp.grid);
+}
+
+inline void long_args64(Long64Args* a, const LongPlan& lp, const LongPowers& pw, const void* data, uint64_t seed,
+                        uint64_t* out) {
+    a->data = static_cast<const uint8_t*>(data);
+    a->head = lp.head;
+    a->chunk = lp.chunk;
+    a->nchunks = lp.nchunks;
+    a->last = lp.last;
+    a->lead = lp.lead;
+    a->stride = lp.stride;
+    a->rounds = (uint32_t)lp.rounds;
+    a->seed = seed;
+    a->out = out;
+    a->x = pw.x64;
+    memcpy(a->xsb, pw.xsb64, sizeof(a->xsb));
+    memcpy(a->zt, pw.zt64, sizeof(a->zt));
+    memcpy(a->ft, pw.ft64, sizeof(uint64_t) * lp.grid);
 }
 
 }  // namespace pcrc

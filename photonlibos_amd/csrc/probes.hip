@@ -280,7 +280,7 @@ template <int G, int ABL>
 __global__ __launch_bounds__(pcrc::kBlock) void long_stamped_kernel(pcrc::LongArgs a, pcrc::LaneConsts kc, uint64_t* t) {
     using namespace pcrc;
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
-    __shared__ uint32_t red[kWaves];
+    __shared__ uint32_t red[2 * kWaves];
     long_run<G, 4, true, ABL>(a, kc, lds, red, t);
 }
 
@@ -449,31 +449,18 @@ int probe_read_rows(const void* base, uint64_t stride, uint64_t rows, uint64_t c
 // * kLongMaxGrid bytes, the first 8 zero (left zero); t = 8 words per wave of
 // grid * 16 waves; *grid_out = the grid. force_chunk: a chunk size (a 1 KiB
 // multiple) instead of the plan's (0 = the plan's). rounds | ablation << 8
-// (long_run's ABL bits: 0..5, 8, 16, 32).
+// (long_run's ABL bits: 8, 16, 32 and 16|32).
 int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* out, uint32_t* state, uint64_t* t,
                        int cus, int lanes, int rounds, uint64_t force_chunk, int* grid_out, void* stream) {
     using namespace pcrc;
     if ((lanes != 64 && lanes != 32) || (rounds & 255) < 1 || (rounds & 255) > 64) return -22;
     if (force_chunk & 1023) return -22;
     const LongPlan lp = long_plan_for(data, n, cus, (uint32_t)lanes | (uint32_t)(rounds & 255) << 8, force_chunk);
-    if (lp.nchunks > (1u << 18)) return -22;
     const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
-    a.data = static_cast<const uint8_t*>(data);
-    a.nbytes = n;
-    a.head = lp.head;
-    a.chunk = lp.chunk;
-    a.nchunks = lp.nchunks;
-    a.seed = seed;
-    a.jinv = pw.jinv32;
-    a.xs = pw.xs32;
-    a.stride = lp.stride;
-    a.out = out;
+    long_args(&a, lp, pw, data, seed, out);
     a.acc = state;
     a.treset = 1;  // the caller's zeroed buffer, put back to 0 by every launch
-    memcpy(a.xp, pw.xpj32, sizeof(a.xp));
-    memcpy(a.xq, pw.p32[1], sizeof(a.xq));
-    memcpy(a.xr, pw.p32[2], sizeof(a.xr));
     LaneConsts kc{};
     kc.kshift = xpow(8ull * 16ull * (uint64_t)lp.lanes);
     mul_basis(kc.kshift, kc.sbasis);
@@ -483,14 +470,10 @@ int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* ou
 #define LSK(G, B) hipLaunchKernelGGL((long_stamped_kernel<G, B>), dim3(lp.grid), dim3(kBlock), 0, s, a, kc, t)
 #define LSG(B) if (lp.lanes == 64) LSK(64, B); else LSK(32, B)
     switch (abl) {
-        case 1: LSG(1); break;
-        case 2: LSG(2); break;
-        case 3: LSG(3); break;
-        case 4: LSG(4); break;
-        case 5: LSG(5); break;
         case 8: LSG(8); break;
         case 16: LSG(16); break;
         case 32: LSG(32); break;
+        case 48: LSG(48); break;
         default: LSG(0); break;
     }
 #undef LSG
