@@ -151,14 +151,15 @@ int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, 
  *                    on a grid anchored at a 4 KiB boundary, each lane group's
  *                    chunks folded in registers, the workgroups' values
  *                    XOR-combined by the last workgroup to finish; up to a
- *                    256 KiB block span, one workgroup with no table
- *                    prologue (the latency path). Above that the launches of
- *                    one stream share the reduce's state (a ticket counting
- *                    every workgroup of the stream's launches, a slot per
- *                    workgroup): the calls are safe from any number of
- *                    streams and threads, but such a call cannot be captured
- *                    into a HIP graph (-ENOTSUP while `stream` is capturing;
- *                    the latency path may be captured).
+ *                    256 KiB block span, the latency path (up to 32 small
+ *                    workgroups, no table prologue). Launches of more than
+ *                    one workgroup share, per stream, the reduce's state (a
+ *                    ticket counting every workgroup of the stream's
+ *                    launches, a slot per workgroup): the calls are safe
+ *                    from any number of streams and threads, but such a call
+ *                    cannot be captured into a HIP graph (-ENOTSUP while
+ *                    `stream` is capturing; one-workgroup calls, block spans
+ *                    up to 4 KiB, may be captured).
  * Asynchronous on `stream` like the batches. */
 int photon_crc32c_series_device(const void* d_buffer, uint32_t part_size, uint32_t n_parts, uint32_t* d_crc_parts,
                                 void* stream);

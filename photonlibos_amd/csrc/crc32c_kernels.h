@@ -1679,53 +1679,67 @@ __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneCon
 
 // ------------------------------------------------ one small buffer (latency)
 // photon_crc32c_extend_device for buffers whose 16-byte block span is at most
-// kSmallBlocks (256 KiB): the reference's small perf shape (128 KiB at
-// buf+1, test_checksum.cpp:125-168) and the routed drop-in on a device
-// pointer (crc32c.h:30-33) are latency, not bandwidth. ONE workgroup of 1024
-// threads, no table prologue: the tables are copied from a device-resident
-// image built once per device (photon_crc32c_extend_device's first call), the
-// copy issued first and the payload loads right behind it, all in flight at
-// once (the 1024 threads x 16 rows cover 256 KiB).
+// kSmallBlocks (256 KiB): the reference's small perf shape (128 KiB at buf+1,
+// test_checksum.cpp:125-168) and the routed drop-in on a device pointer
+// (crc32c.h:30-33) are latency, not bandwidth. Up to kSmallWg workgroups of
+// 256 threads, no table prologue: each copies 8.5 KiB of nibble tables from
+// a device-resident image built once per device, with its payload loads
+// issued right behind the copy. (Round 4's first form was ONE workgroup of
+// 1024 threads: 12 µs for 128 KiB, all 131 K lookups on one CU's LDS.)
 // Geometry: the block grid [a0, a0 + 16 nb) covers the data from its aligned
-// start through the end rounded up to 16 bytes (and at least the 4 seed
-// bytes). The 1024 threads are ONE lane group: thread t walks column t of
-// rows of 1024 blocks anchored at the END (block b = nb - 1024 (rows - r) + t
-// in row r; b < 0 is a leading zero block, which does not change a CRC), so
-// every thread's last block is in the last row and its distance to the end
-// is 1023 - t = 64 (15 - wave) + (63 - lane). Masking: bytes before the data
-// start and at or after its end are zero, the seed is XORed into the data's
-// first 4 bytes (head_word_sel). The k zero bytes after the end multiply the
-// CRC by x^(8k): the result is multiplied by x^(-8k) at the end, which also
-// makes a seed over fewer than 4 data bytes exact (crc32c_extend(D, n, s) =
-// crc(D) ^ s x^(8n)).
-// Per thread: Q <- Q * x^(8*16384) ^ lag16(block) over its rows (S table);
-// then Q -> P and the lane shift x^(128 (63 - lane)) through A_dl, B_dh (the
-// batch kernel's G >= 16 finish tables), XOR over the wave, the wave's shift
-// x^(8192 (15 - wave)) as a lane-parallel multiply (basis words from the
-// image), XOR over the waves in LDS, x^(-8k) (lane-parallel), store.
-// Single-replica tables: a few bank conflicts cost cycles on a path bound
-// by its dependent LDS round trips, not by LDS throughput.
-constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of blocks: 16 rows of 1024
-constexpr uint32_t kSmD = 0, kSmS = 4096, kSmA = 8192, kSmB = kSmA + 8u * 4096u;
-constexpr uint32_t kSmLds = kSmB + 7u * 4096u;                // 69632 B of tables in LDS
-constexpr uint32_t kSmWave = kSmLds;                          // 16 x 32 words: basis of x^(8192 (15 - w))
-constexpr uint32_t kSmTail = kSmWave + 16u * 32u * 4u;        // 32 x 32 words: basis of x^(-8 k), k < 32
+// start through its end rounded up to 16 bytes (and at least the 4 seed
+// bytes). All threads of the kSmallWg x 256 slots form ONE lane group of
+// V = 8192 virtual lanes walking rows of V blocks anchored at the END: slot
+// vt (workgroup b, wave w, lane l: vt = (4 b + w) 64 + l) takes block
+// nb - V (rows - r) + vt in row r (a negative block is a leading zero block,
+// which does not change a CRC). Every slot's last block is in the last row,
+// V - 1 - vt blocks before the end, so every factor is a constant of the
+// layout, independent of the buffer: the lane's x^(32 + 128 (63 - l))
+// (nibble tables A_dl, B_dh: Q -> P and the shift inside the wave) and the
+// wave's x^(8192 (127 - (4 b + w))) (basis words from the image). Only the
+// workgroups that hold data are launched (the last ones). Masking: bytes
+// before the data start and at or after its end are zero, the seed is XORed
+// into the data's first 4 bytes; the k zero bytes after the end multiply the
+// CRC by x^(8k), undone by x^(-8k) (which also makes a seed over fewer than 4
+// data bytes exact: crc32c_extend(D, n, s) = crc(D) ^ s x^(8n)).
+// Nibble tables (8 positions x 16 values per multiplier, 512 B): the 64
+// lanes of a lookup read one position's 16 words, at most 16 distinct
+// addresses in 16 consecutive words: conflict-free with one copy.
+// Result: each workgroup's value (all factors applied) goes to slots[b]
+// when `slots` is set (the routed drop-in: pinned host memory, the host XORs
+// them), else to *out through long_reduce (one workgroup: directly).
+constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of blocks
+constexpr uint32_t kSmallWg = 32, kSmallLanes = kSmallWg * 256;  // V = 8192 virtual lanes
+constexpr uint32_t kSmallRows = (kSmallBlocks + 1 + kSmallLanes - 1) / kSmallLanes;  // 3
+constexpr uint32_t kNib = 512;                                // bytes of one nibble-sliced multiplier
+constexpr uint32_t kSmD = 0, kSmS = kNib, kSmA = 2 * kNib, kSmB = kSmA + 8 * kNib;
+constexpr uint32_t kSmLds = kSmB + 7 * kNib;                  // 8704 B of tables in LDS
+constexpr uint32_t kSmWave = kSmLds;                          // 128 x 32 words: basis of x^(8192 (127 - wave))
+constexpr uint32_t kSmTail = kSmWave + 4u * kSmallWg * 32u * 4u;  // 32 x 32 words: basis of x^(-8 k), k < 32
 constexpr uint32_t kSmImage = kSmTail + 32u * 32u * 4u;       // bytes of the device image
 
 struct SmallArgs {
     const uint8_t* a0;   // aligned start (data start & ~15)
     const uint32_t* image;
-    uint32_t* out;
-    uint32_t nb;         // blocks of the grid, <= kSmallBlocks
+    uint32_t* out;       // the CRC (device), through long_reduce when grid > 1
+    uint32_t* slots;     // or: workgroup b's value at slots[b] (mapped host memory), out unused
+    uint32_t* acc;       // long_reduce state (grid > 1, slots == nullptr)
+    uint64_t tbase;      // long_reduce ticket base
+    uint32_t treset;
+    uint32_t nb;         // blocks of the grid, <= kSmallBlocks + 1
     uint32_t s0;         // data start - a0 (0..15)
     uint32_t eoff;       // data end - a0: bytes at or past it are zero
     uint32_t k;          // grid end - data end (0..31): the result is multiplied by x^(-8k)
     uint32_t seed;
+    uint32_t wg0;        // workgroup index of blockIdx.x == 0 (kSmallWg - grid)
 };
 
-// p * K through the 4 single-replica byte-slice tables of K at T.
-__device__ __forceinline__ uint32_t small_mul(const uint32_t* T, uint32_t p) {
-    return xor3(xor3(T[p & 0xffu], T[256 + ((p >> 8) & 0xffu)], T[512 + ((p >> 16) & 0xffu)]), T[768 + (p >> 24)], 0u);
+// p * K through the nibble-sliced tables of K at T (8 conflict-free lookups).
+__device__ __forceinline__ uint32_t nib_mul(const uint32_t* T, uint32_t p) {
+    uint32_t v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = T[t * 16 + ((p >> (4 * t)) & 15u)];
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
 }
 
 // Bytes of the word at `off` (from a0) at or past `eoff` zeroed (branch-free).
@@ -1735,44 +1749,42 @@ __device__ __forceinline__ uint32_t tail_word(uint32_t w, int off, int eoff) {
     return mc == 4 ? w : w & (uint32_t)((1ull << (8 * mc)) - 1ull);
 }
 
-__global__ __launch_bounds__(1024) void crc32c_small_kernel(SmallArgs a) {
+__global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSmLds / 4];
-    __shared__ uint32_t red[16];
+    __shared__ uint32_t red[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id(), l32 = lane & 31u;
-    // 1. The table copy first (vmcnt counts in issue order: waiting for it
-    //    does not wait for the payload), then every payload row, then the two
-    //    basis words this thread needs at the end.
-    constexpr uint32_t kVec = kSmLds / 16;  // 4352 16-byte pieces
-    u32x4 tv[5];
+    const uint32_t wg = a.wg0 + blockIdx.x;               // position in the layout
+    const uint32_t vt = wg * 256u + tid;                   // virtual lane
+    // 1. The table copy first (vmcnt counts in issue order), then the payload
+    //    rows, then the basis words this thread needs at the end.
+    constexpr uint32_t kVec = kSmLds / 16;  // 544 16-byte pieces
+    u32x4 tv[3];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const uint32_t j = (uint32_t)i * 1024u + tid;
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t j = (uint32_t)i * 256u + tid;
         tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
     }
-    const uint32_t rows = (a.nb + 1023u) >> 10;
-    const int first = (int)a.nb - (int)(rows << 10) + (int)tid;  // this thread's block in row 0
-    uint4 w[16];
+    const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
+    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;  // this thread's block in row 0
+    uint4 w[kSmallRows];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int b = first + r * 1024;
+    for (int r = 0; r < (int)kSmallRows; ++r) {
+        const int b = first + r * (int)kSmallLanes;
         w[r] = ((uint32_t)r < rows && b >= 0) ? load16(a.a0 + 16 * (uint32_t)b) : make_uint4(0, 0, 0, 0);
     }
-    const uint32_t bw_wave = a.image[kSmWave / 4 + wave * 32u + l32];
+    const uint32_t bw_wave = a.image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
     const uint32_t bw_tail = a.image[kSmTail / 4 + a.k * 32u + l32];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const uint32_t j = (uint32_t)i * 1024u + tid;
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t j = (uint32_t)i * 256u + tid;
         if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
     }
     lds_barrier();
-    const uint32_t* D = lds + kSmD / 4;
-    const uint32_t* S = lds + kSmS / 4;
-    // 2. The column: lagged blocks (as lag16) and the row shift.
-    uint32_t q = 0;
+    // 2. The column: lagged blocks (independent per row) and the row shift.
+    uint32_t c[kSmallRows];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        if ((uint32_t)r >= rows) continue;  // rows is uniform: a skipped row is a scalar branch
-        const int b = first + r * 1024;
+    for (int r = 0; r < (int)kSmallRows; ++r) {
+        const int b = first + r * (int)kSmallLanes;
         uint4 v = w[r];
         if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + seed
             const int off = b * 16;
@@ -1780,27 +1792,32 @@ __global__ __launch_bounds__(1024) void crc32c_small_kernel(SmallArgs a) {
             v.y = head_word_sel(tail_word(v.y, off + 4, (int)a.eoff), off + 4, (int)a.s0, a.seed);
             v.z = head_word_sel(tail_word(v.z, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.seed);
             v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
-            if (b < 0) v = make_uint4(0, 0, 0, 0);
+            if (b < 0 || (uint32_t)r >= rows) v = make_uint4(0, 0, 0, 0);
         }
-        uint32_t c = small_mul(D, v.x) ^ v.y;
-        c = small_mul(D, c) ^ v.z;
-        c = small_mul(D, c) ^ v.w;
-        q = small_mul(S, q) ^ c;
+        uint32_t x = nib_mul(lds + kSmD / 4, v.x) ^ v.y;
+        x = nib_mul(lds + kSmD / 4, x) ^ v.z;
+        c[r] = nib_mul(lds + kSmD / 4, x) ^ v.w;
     }
-    // 3. Q -> P and the shift to the end: x^(32 + 128 dl) then x^(1024 dh), d = 63 - lane.
+    uint32_t q = c[0];
+#pragma unroll
+    for (int r = 1; r < (int)kSmallRows; ++r)
+        if ((uint32_t)r < rows) q = nib_mul(lds + kSmS / 4, q) ^ c[r];
+    // 3. Q -> P and the shift to the end of the wave: x^(32 + 128 dl), then x^(1024 dh), d = 63 - lane.
     const uint32_t d = 63u - lane, dh = d >> 3;
-    const uint32_t x = small_mul(lds + kSmA / 4 + (d & 7u) * 1024u, q);
-    const uint32_t y = small_mul(lds + kSmB / 4 + (dh ? dh - 1u : 0u) * 1024u, x);
+    const uint32_t x = nib_mul(lds + (kSmA + (d & 7u) * kNib) / 4, q);
+    const uint32_t y = nib_mul(lds + (kSmB + (dh ? dh - 1u : 0u) * kNib) / 4, x);
     uint32_t v = group_xor<64>(dh ? y : x);
-    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (15 - wave)), valid in both halves
+    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (127 - (4 wg + wave))): the wave to the end of the layout
     if (lane == 0) red[wave] = v;
     __syncthreads();
     if (wave == 0) {
-        uint32_t t = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) t ^= red[i];
-        t = mul_lanes(t, bw_tail, l32);  // x^(-8k): the zero bytes after the end
-        if (lane == 0) *a.out = t;
+        uint32_t u = red[0] ^ red[1] ^ red[2] ^ red[3];
+        u = mul_lanes(u, bw_tail, l32);  // x^(-8k): the zero bytes after the end (linear: per workgroup)
+        if (a.slots) {
+            if (lane == 0) a.slots[blockIdx.x] = u;
+        } else {
+            long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
+        }
     }
 }
 

@@ -312,38 +312,36 @@ def test_extend_device_thousand_back_to_back_launches(torch_dev, oracle):
 
 
 def test_extend_device_graph_capture(torch_dev, oracle):
-    """a long-buffer call over 256 KiB is refused (-ENOTSUP) while
-    its stream is captured into a HIP graph (its reduce state is per stream);
-    up to 256 KiB (one workgroup, no state) it captures and replays exactly."""
+    """a call launching more than one workgroup (a block span over
+    4 KiB) is refused (-ENOTSUP) while its stream is captured into a HIP graph
+    (its reduce state is per stream); a one-workgroup call captures and
+    replays exactly; the stream runs long calls again after the capture."""
     torch = torch_dev
     d = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0C00)
-    host = d.cpu().numpy()
-    out = torch.zeros(2, dtype=torch.int32, device="cuda")
-    ck.extend_device(d.data_ptr() + 3, 128 << 10, 9, out[0:1])  # the device's table image exists before capture
+    out = torch.zeros(3, dtype=torch.int32, device="cuda")
+    ck.extend_device(d.data_ptr() + 3, 3000, 9, out[0:1])  # the device's table image exists before capture
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     refused = []
-    torch.cuda.synchronize()
     with torch.cuda.graph(g):
         st = torch.cuda.current_stream()
-        ck.extend_device(d.data_ptr() + 3, 128 << 10, 9, out[0:1], stream=st)
-        try:
-            ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[1:2], stream=st)
-        except ck.CrcError as e:
-            refused.append(e.code)
-    assert refused == [-95]  # ENOTSUP
+        ck.extend_device(d.data_ptr() + 3, 3000, 9, out[0:1], stream=st)
+        for k, n in ((1, 128 << 10), (2, (1 << 20) - 64)):
+            try:
+                ck.extend_device(d.data_ptr() + 3, n, 9, out[k:k + 1], stream=st)
+            except ck.CrcError as e:
+                refused.append(e.code)
+    assert refused == [-95, -95]  # ENOTSUP
     for seed_fill in (0x5EED0C01, 0x5EED0C02):  # new data, same graph
         ck.fill_splitmix(d, d.numel(), d.numel(), 1, seed_fill)
         torch.cuda.synchronize()
         g.replay()
         torch.cuda.synchronize()
-        assert int(_u32(out)[0]) == oracle.crc32c(d.cpu().numpy()[3:3 + (128 << 10)], 9)
-    assert host is not None
-    # the same stream outside capture runs the long call again
-    ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[1:2])
+        assert int(_u32(out)[0]) == oracle.crc32c(d.cpu().numpy()[3:3 + 3000], 9)
+    ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[2:3])
     torch.cuda.synchronize()
-    assert int(_u32(out)[1]) == oracle.crc32c(d.cpu().numpy()[3:3 + (1 << 20) - 64], 9)
+    assert int(_u32(out)[2]) == oracle.crc32c(d.cpu().numpy()[3:3 + (1 << 20) - 64], 9)
 
 
 @pytest.mark.parametrize("shape", [(0, 0), (64, 1), (64, 2), (32, 1), (32, 2), (32, 3)])
