@@ -23,6 +23,10 @@ extern "C" {
  * lanes per buffer G in {4,8,16,32,64}; 0 = automatic (default). */
 int photon_crc_set_lanes_per_buffer(int g);
 
+/* Workgroups of the CRC32C batch kernel's persistent grid (tuning: fewer
+ * busy CUs at the same HBM rate); 0 = one per CU (default). */
+int photon_crc_set_batch_grid(int workgroups);
+
 /* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
  * lane run B, rows per step U and steps in flight D, one of (1,4,3), (2,2,3),
  * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4), (1,4,1),
@@ -62,7 +66,8 @@ int photon_crc_set_msg_rows(int rows_per_step);
  * group of the full grid (rounds, 1..64); 0 = automatic, by buffer size and
  * CRC width (photonlibos_amd/csrc/long_plan.h long_plan_for, which lists the
  * measurements behind each step): CRC-32C 64 lanes x 2 rounds, 32 x 2 from
- * 512 MiB, 64 x 1 from 1.5 GiB; CRC-64 64 lanes, 2 rounds, 1 from 1 GiB. */
+ * 512 MiB, 64 x 4 from 1.5 GiB, 64 x 2 from 3 GiB; CRC-64 64 lanes x 1
+ * round, 2 from 1 GiB, 4 from 1.5 GiB, 2 from 3 GiB. */
 int photon_crc_set_long_shape(int lanes, int rounds);
 
 /* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =

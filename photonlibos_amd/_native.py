@@ -46,6 +46,7 @@ def _declare(L):
     fn("photon_crc_last_error", ctypes.c_char_p)
     fn("photon_crc_scratch_release", ctypes.c_int64)
     fn("photon_crc_set_lanes_per_buffer", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc_set_batch_grid", ctypes.c_int, ctypes.c_int)
     fn("photon_crc32c_batch_strided", ctypes.c_int, vp, u64, u64, u64, u32, vp, vp, vp)
     fn("photon_crc32c_batch_strided_sync", ctypes.c_int, vp, u64, u64, u64, u32, vp, vp, vp)
     fn("photon_crc32c_batch_iov", ctypes.c_int, vp, u64, u32, vp, vp, vp)

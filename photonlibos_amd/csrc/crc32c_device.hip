@@ -71,6 +71,9 @@ thread_local std::string g_err;
 // an atomic word that a launch reads ONCE; a multi-field shape is packed into
 // one word so a launch never sees half of a concurrent setter's update.
 std::atomic<int> g_lanes_override{0};
+// Workgroups of the persistent batch grids (photon_crc_set_batch_grid,
+// tuning): 0 = one per CU (the default).
+std::atomic<int> g_grid_cap{0};
 // Batch kernel: rows per step of the generic kernel (2, 4, 8), or 0 = the
 // fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
 // the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
@@ -420,6 +423,7 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
     if (grid > (uint64_t)cus) grid = cus;
+    if (const int cap = g_grid_cap.load(std::memory_order_relaxed)) grid = grid > (uint64_t)cap ? (uint64_t)cap : grid;
     const int rows_per_step = batch_rows(g);
     if (rows_per_step == 0) {
         const FusedConsts& fc = fused_consts(g);
@@ -826,7 +830,7 @@ std::vector<uint32_t> small_image_host() {
         for (uint32_t t = 0; t < 8; ++t)
             for (uint32_t v = 0; v < 16; ++v) img[off / 4 + t * 16 + v] = mulmod(v << (4 * t), k);
     };
-    nibbles(kSmD, kPoly);                                   // x^32: the word step
+    for (uint32_t j = 1; j <= 3; ++j) nibbles(kSmD + (j - 1) * kNib, xpow(32ull * j));  // x^(32 j)
     nibbles(kSmS, xpow(8ull * 16ull * kSmallLanes));        // one row of V blocks
     for (uint32_t dl = 0; dl < 8; ++dl) nibbles(kSmA + dl * kNib, xpow(32ull + 128ull * dl));
     for (uint32_t dh = 1; dh < 8; ++dh) nibbles(kSmB + (dh - 1) * kNib, xpow(1024ull * dh));
@@ -912,6 +916,12 @@ int photon_crc_set_lanes_per_buffer(int g) {
 }
 
 int photon_crc_lanes_for(uint64_t nbytes) { return batch_lanes(nbytes); }
+
+int photon_crc_set_batch_grid(int workgroups) {
+    if (workgroups < 0) return fail(-EINVAL, "workgroups must be >= 0 (0 = one per CU)");
+    g_grid_cap.store(workgroups, std::memory_order_relaxed);
+    return 0;
+}
 
 void photon_crc_test_fail_next(int n) { g_fail_next = n > 0 ? n : 0; }
 

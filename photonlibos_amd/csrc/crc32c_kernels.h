@@ -1712,8 +1712,10 @@ constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of bloc
 constexpr uint32_t kSmallWg = 32, kSmallLanes = kSmallWg * 256;  // V = 8192 virtual lanes
 constexpr uint32_t kSmallRows = (kSmallBlocks + 1 + kSmallLanes - 1) / kSmallLanes;  // 3
 constexpr uint32_t kNib = 512;                                // bytes of one nibble-sliced multiplier
-constexpr uint32_t kSmD = 0, kSmS = kNib, kSmA = 2 * kNib, kSmB = kSmA + 8 * kNib;
-constexpr uint32_t kSmLds = kSmB + 7 * kNib;                  // 8704 B of tables in LDS
+// D_j: x^(32 j), j = 1..3 (a block's lagged CRC in ONE table step, not three
+// dependent ones), S: one row, A_dl, B_dh: the lane's finish.
+constexpr uint32_t kSmD = 0, kSmS = 3 * kNib, kSmA = 4 * kNib, kSmB = kSmA + 8 * kNib;
+constexpr uint32_t kSmLds = kSmB + 7 * kNib;                  // 9728 B of tables in LDS
 constexpr uint32_t kSmWave = kSmLds;                          // 128 x 32 words: basis of x^(8192 (127 - wave))
 constexpr uint32_t kSmTail = kSmWave + 4u * kSmallWg * 32u * 4u;  // 32 x 32 words: basis of x^(-8 k), k < 32
 constexpr uint32_t kSmImage = kSmTail + 32u * 32u * 4u;       // bytes of the device image
@@ -1757,7 +1759,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
     const uint32_t vt = wg * 256u + tid;                   // virtual lane
     // 1. The table copy first (vmcnt counts in issue order), then the payload
     //    rows, then the basis words this thread needs at the end.
-    constexpr uint32_t kVec = kSmLds / 16;  // 544 16-byte pieces
+    constexpr uint32_t kVec = kSmLds / 16;  // 608 16-byte pieces
     u32x4 tv[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -1794,9 +1796,9 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
             v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
             if (b < 0 || (uint32_t)r >= rows) v = make_uint4(0, 0, 0, 0);
         }
-        uint32_t x = nib_mul(lds + kSmD / 4, v.x) ^ v.y;
-        x = nib_mul(lds + kSmD / 4, x) ^ v.z;
-        c[r] = nib_mul(lds + kSmD / 4, x) ^ v.w;
+        // lag16: D(D(D(w0) ^ w1) ^ w2) ^ w3 = w0 x^96 ^ w1 x^64 ^ w2 x^32 ^ w3
+        c[r] = xor3(nib_mul(lds + (kSmD + 2 * kNib) / 4, v.x), nib_mul(lds + (kSmD + kNib) / 4, v.y),
+                    nib_mul(lds + kSmD / 4, v.z)) ^ v.w;
     }
     uint32_t q = c[0];
 #pragma unroll

@@ -48,16 +48,25 @@ struct LongPlan {
 // Long buffers only: the small kernel takes block spans up to 256 KiB.
 inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t shape, uint64_t force_chunk = 0,
                               bool crc64 = false) {
-    // automatic shape (r03 interleaved A/B, scripts/ab_long.py; re-measured in r04):
-    //  CRC-32C: 64 lanes x 2 rounds; 32 x 2 from 512 MiB; 64 x 1 from 1.5 GiB
-    //  CRC-64: 64 lanes; 1 round from 1 GiB, else 2
+    // automatic shape (r04 interleaved A/B over this cut, one process per
+    // size, scripts/ab_long.py; repo:profiles/r04b_ab_long_shapes_1g.jsonl,
+    // r04c_ab_long_shapes_sizes.jsonl; medians in ms, batch kernel over 64
+    // KiB pieces of the same bytes in brackets):
+    //  CRC-32C: 256 MiB 64x2 0.0541 (0.0545); 512 MiB 64x1 0.0919, 32x2
+    //    0.0937 (0.0889); 1 GiB 32x2 0.1679, 64x2 0.169, 64x1 0.179 (0.1647);
+    //    2 GiB 64x4 0.3242, 32x2 0.3425 (0.3186); 4 GiB 64x2 0.6328 (0.6236)
+    //  CRC-64: 256 MiB 64x1 0.0575 (0.058); 512 MiB 64x1 0.0961 (0.089);
+    //    1 GiB 64x2 0.1722, 64x1 0.1843 (0.1658); 2 GiB 64x4 0.3273 (0.322);
+    //    4 GiB 64x2 0.6341 (0.6304)
     //  up to 256 KiB (CRC-64 only: CRC-32C has its small kernel): 1 round of
     //  chunks of >= 4 KiB, one workgroup
     const bool small = n <= (256u << 10);
-    const bool huge = n >= (512ull << 20), giant = n >= (3ull << 29);
-    const int lanes = (shape & 0xff) ? (int)(shape & 0xff) : (huge && !giant && !crc64) ? 32 : 64;
-    const uint64_t one = small || (crc64 ? n >= (1ull << 30) : giant);
-    uint64_t rounds = (shape >> 8) ? shape >> 8 : one ? 1 : 2;
+    const uint64_t mib = n >> 20;
+    const int lanes = (shape & 0xff) ? (int)(shape & 0xff) : (!crc64 && mib >= 512 && mib < 1536) ? 32 : 64;
+    uint64_t rounds = (shape >> 8) ? shape >> 8
+                    : small ? 1
+                    : crc64 ? (mib < 1024 ? 1 : mib < 1536 ? 2 : mib < 3072 ? 4 : 2)
+                            : (mib < 1536 ? 2 : mib < 3072 ? 4 : 2);
     const uint64_t gpw = 64 / (uint64_t)lanes;
     const uint64_t maxgrid = (uint64_t)cus < kLongMaxFt ? (uint64_t)cus : kLongMaxFt;
     LongPlan p{};

@@ -19,6 +19,7 @@ without amdsmi the power sampler's mean power x time is used instead.
 Phases are separated by IDLE_S seconds of idle GPU. One JSON line per phase.
 
   KERNELS=crc,rows,read,crc  STEADY_S=3  IDLE_S=2  python scripts/probe_power.py [--stamps]
+  (crc@W: the product kernel on a grid capped at W workgroups, photon_crc_set_batch_grid)
 """
 import ctypes
 import json
@@ -138,7 +139,7 @@ def launch(kernel, k):
     elif STAMPS:
         rc = P.probe_crc_wave_times(buf.data_ptr(), n, cnt, out.data_ptr(), t, ticket.data_ptr(), 32, 0, 0, cus,
                                     st.cuda_stream)
-    else:
+    else:  # crc or crc@<workgroups>: the product kernel (on a capped grid)
         ck.batch_strided(buf, n, n, cnt, out, stream=st)
         rc = 0
     assert rc == 0, rc
@@ -159,6 +160,10 @@ def clocks(k_count):
 
 
 def phase(kernel, label):
+    grid_cap = int(kernel.split("@")[1]) if "@" in kernel else 0
+    kernel = kernel.split("@")[0]
+    from photonlibos_amd._native import lib as _lib
+    _lib().photon_crc_set_batch_grid(grid_cap)
     for t in ts:
         t.zero_()
     torch.cuda.synchronize()
@@ -201,7 +206,8 @@ def phase(kernel, label):
             r["J_per_GiB_sampled"] = round(float(np.mean(pw)) * (tb - ta) / (nl * nbytes / GIB), 4)
         return r
 
-    res = {"phase": label, "kernel": kernel + ("+stamps" if kernel == "crc" and STAMPS else ""),
+    res = {"phase": label, "kernel": kernel + ("+stamps" if kernel == "crc" and STAMPS else "") +
+           (f"@{grid_cap}" if grid_cap else ""),
            "window": {"launch_ms": ms, "mean_ms": round(float(np.mean(ms)), 4),
                       "frac_of_8TBps": round(nbytes / (float(np.mean(ms)) * 1e-3) / 8e12, 4),
                       **seg(e0, e1, t0, t1, WINDOW)},
@@ -220,7 +226,9 @@ for i, kern in enumerate(KERNELS):
     if i:
         time.sleep(IDLE_S)
     phase(kern, "fresh process, right after the fill" if i == 0 else f"after {IDLE_S:g} s idle")
-    if kern == "crc":
+    from photonlibos_amd._native import lib as _lib
+    _lib().photon_crc_set_batch_grid(0)
+    if kern.startswith("crc"):
         ck.batch_strided(buf, n, n, cnt, want, stream=st)
         torch.cuda.synchronize()
         assert torch.equal(out, want), "probe CRCs differ from the product's"

@@ -154,4 +154,4 @@ def test_reference_perf_shape_is_balanced():
     assert p["chunk"] == 64 << 10 and p["D"] == 0 and p["T"] == p["R"] * p["S"]
     assert p["head"] + p["L"] == p["chunk"]  # group S-1: head + (R-1) chunks + the short one = R chunks
     p64 = _plan(4096 * 100 + 1, 1 << 30, 256, crc64=True)
-    assert (p64["lanes"], p64["R"]) == (64, 1) and p64["head"] + p64["L"] == p64["chunk"] and p64["D"] == 0
+    assert (p64["lanes"], p64["R"]) == (64, 2) and p64["head"] + p64["L"] == p64["chunk"] and p64["D"] == 0
