@@ -7,6 +7,13 @@
 #ifndef PCRC64_U
 #define PCRC64_U 2  // rows per step of the CRC-64 batch kernel (2 > 4 by 0.9 points on the C2 shape; A/B builds: -DPCRC64_U=4)
 #endif
+// Bench-only ablation builds of buffer_reg64 (-DPCRC64_ABL=bits; results are
+// then NOT CRCs): 1 = no head masking, 2 = no finish multiply, 4 = no group
+// XOR, 8 = row shift replaced by an XOR (no S lookups), 16 = lagged block
+// replaced by lo ^ hi (no D lookups). 0 in the product.
+#ifndef PCRC64_ABL
+#define PCRC64_ABL 0
+#endif
 
 namespace pcrc {
 
@@ -140,6 +147,7 @@ __device__ __forceinline__ uint2 dstep64(const uint32_t* lds, uint2 x, const Lan
 // P * x^(8*16*G) mod P64 (^ e).
 __device__ __forceinline__ uint2 sstep64(const uint32_t* lds, uint2 p, const LaneAddr64& a,
                                          uint2 e = make_uint2(0, 0)) {
+    if constexpr ((PCRC64_ABL & 8) != 0) return make_uint2(p.y ^ e.x, p.x ^ e.y);
     return step64<1>(lds, p, a, e);
 }
 
@@ -149,6 +157,7 @@ __device__ __forceinline__ uint2 sstep64(const uint32_t* lds, uint2 p, const Lan
 // Q = P * x^-64 instead: Q <- Q * X ^ v, so each block costs one D step (8
 // lookups) + one S step (8) instead of 24 lookups; P = D(Q) once per buffer.
 __device__ __forceinline__ uint2 lag16_64(const uint32_t* lds, uint4 w, const LaneAddr64& a) {
+    if constexpr ((PCRC64_ABL & 16) != 0) return make_uint2(w.x ^ w.z, w.y ^ w.w);
     return dstep64(lds, make_uint2(w.x, w.y), a, make_uint2(w.z, w.w));
 }
 
@@ -359,7 +368,7 @@ __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint
         // Row 0 (head: masked leading bytes + inverted init).
         if (gl < nb) {
             uint4 w = w0;
-            if (gl < 2) {
+            if (!(PCRC64_ABL & 1) && gl < 2) {
                 const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
                 const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
                 w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
@@ -391,8 +400,8 @@ __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint
         }
         if (part) pc = sstep64(lds, pc, la, lag16_64(lds, wp, la));
         // Q * x^(64 + 128 d) (Q -> P and the shift to the end of the blocks), XOR over the group.
-        const uint64_t f = finish64<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds, lane);
-        reg = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+        const uint64_t f = (PCRC64_ABL & 2) ? u64of(pc) : finish64<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds, lane);
+        reg = (PCRC64_ABL & 4) ? f : ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
         if (gl == 0)
             for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
     }

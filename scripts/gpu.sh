@@ -15,6 +15,7 @@
 #                                        recorded with "ok": false, not a failure); AB_NEW=LIB2 puts
 #                                        another build on the "new" side; AB_ARGS adds bench.py arguments
 #                                        (e.g. AB_ARGS="--steps 20 --warmup 5": the driver's conditions)
+#   scripts/gpu.sh abn CONFIG ROUNDS LIB.. the in-tree build and every LIB, order reversed every other round
 # Several commands chain with "::", e.g.
 #   scripts/gpu.sh tests :: bench --steps 20 --warmup 5 :: prof c2
 set -o pipefail
@@ -67,6 +68,21 @@ run_one() {
               || { echo "ab $c $side failed"; tail -5 $O/ab.err; return 1; }  # (self-check false still prints its line: ablation builds)
             python -c "import json,sys; d=json.loads(open('$O/ab_tmp.json').read().splitlines()[-1]); r=d['roofline']; print(json.dumps({'round': $r, 'config': '$c', 'side': '$side', 'args': '$AB_ARGS', 'value': d['value'], 'frac_kernel': r['frac_kernel'], 'frac_steady': r['frac_steady_median_launch'], 'ok': d['self_check']}))" | tee -a $O/ab.jsonl
           done
+        done
+      done ;;
+    abn)
+      # abn CONFIG ROUNDS LIB... : every build (in-tree = "new"), order reversed every other round
+      local c=$1 rounds=$2; shift 2
+      local libs=(new "$@")
+      for r in $(seq 1 $rounds); do
+        local order=("${libs[@]}")
+        [ $((r % 2)) -eq 0 ] && order=($(printf '%s\n' "${libs[@]}" | tac))
+        for lib in "${order[@]}"; do
+          local envv=""; [ $lib != new ] && envv="PHOTON_CRC_LIB=$lib"
+          env $envv timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-live-pmc --no-shape64 $AB_ARGS \
+            > $O/ab_tmp.json 2>> $O/ab.err || [ "$(wc -l < $O/ab_tmp.json)" -gt 0 ] \
+            || { echo "abn $c $lib failed"; tail -5 $O/ab.err; return 1; }
+          python -c "import json,sys; d=json.loads(open('$O/ab_tmp.json').read().splitlines()[-1]); r=d['roofline']; print(json.dumps({'round': $r, 'config': '$c', 'lib': '$lib', 'value': d['value'], 'frac_kernel': r['frac_kernel'], 'frac_steady': r['frac_steady_median_launch'], 'ok': d['self_check']}))" | tee -a $O/abn.jsonl
         done
       done ;;
     *) echo "unknown command $cmd"; return 1 ;;
