@@ -78,15 +78,22 @@ def make(v, n):
             lib.photon_crc_set_long_shape(lanes, rounds)
             ck.extend64_device(d.data_ptr() + off, n, out64[k:k + 1], seed=7, stream=st)
         return fc64
-    if v.startswith("c64="):  # c64=<library path>: another build's CRC-64 extend_device
+    if v.startswith("c64="):  # c64=<library path>[#lanes/rounds]: another build's CRC-64 extend_device
         # (same kernel names in two loaded builds: only builds with the same
         # kernel argument layout compare reliably)
         path = v.split("=", 1)[1]
+        shape64 = (0, 0)
+        if "#" in path:
+            path, sh = path.split("#")
+            shape64 = tuple(int(x) for x in sh.split("/"))
         l64 = ctypes.CDLL(path if os.path.isabs(path) else os.path.join(REPO, path), mode=ctypes.RTLD_LOCAL)
         l64.photon_crc64ecma_extend_device.argtypes = [vp, u64, ctypes.c_uint64, vp, vp]
         l64.photon_crc64ecma_extend_device.restype = ci
+        l64.photon_crc_set_long_shape.argtypes = [ci, ci]
+        l64.photon_crc_set_long_shape.restype = ci
 
         def f64(k):
+            l64.photon_crc_set_long_shape(*shape64)
             rc = l64.photon_crc64ecma_extend_device(d.data_ptr() + off, n, 7, out64.data_ptr() + 8 * k,
                                                     ctypes.c_void_p(st.cuda_stream))
             assert rc == 0, (v, rc)

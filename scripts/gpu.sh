@@ -40,10 +40,10 @@ run_one() {
       cut -c1-400 $O/bench_$tag.json ;;
     prof)
       local c=$1; shift
-      (cd /tmp && true)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$c -o $c -- \
-        python3 bench.py --config $c --no-cpu-baseline --no-live-pmc "$@" > $O/prof_$c.log 2>&1 \
-        || { echo "prof $c failed"; tail -20 $O/prof_$c.log; return 1; } ;;
+      local pt; pt=$(echo "$c $*" | tr -c 'a-zA-Z0-9_' '_' | sed 's/__*/_/g;s/^_//;s/_$//')  # prof c2 --extend -> prof_c2_extend
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$pt -o $c -- \
+        python3 bench.py --config $c --no-cpu-baseline --no-live-pmc "$@" > $O/prof_$pt.log 2>&1 \
+        || { echo "prof $c failed"; tail -20 $O/prof_$pt.log; return 1; } ;;
     pmc)
       local c=$1
       timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_$c -o $c -- \

@@ -64,7 +64,10 @@ def stats(kind, k):
         start, body_end, end, xcc = t[:, 0], t[:, 1], t[:, 1], t[:, 3] & 7
     b = start.min()
     rel = (body_end - b) / 100.0
-    return {"span_us": (end.max() - b) / 100.0, "end_p50_us": float(np.median(rel)),
+    extra = {"start_p50_us": float(np.median(start - b)) / 100.0, "start_max_us": float((start - b).max()) / 100.0}
+    if kind == "long":  # table build + basis words: wave start -> first chunk
+        extra["prologue_p50_us"] = float(np.median(t[:, 1] - start)) / 100.0
+    return {**extra, "span_us": (end.max() - b) / 100.0, "end_p50_us": float(np.median(rel)),
             "end_p90_us": float(np.percentile(rel, 90)), "end_max_us": float(rel.max()),
             "tail_after_body_us": (end.max() - body_end.max()) / 100.0,
             "xcc_end_med_us": [float(np.median(rel[xcc == x])) for x in range(8)]}
