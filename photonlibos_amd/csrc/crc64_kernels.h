@@ -408,11 +408,28 @@ __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint
     return reg;
 }
 
+// Per-wave s_memrealtime stamps of the bench-only probe builds (probes.hip;
+// the product passes nullptr and STAMP = false): 8 words per wave.
+__device__ __forceinline__ void stamp64_write(uint64_t* t, const uint64_t (&v)[5]) {
+    if ((threadIdx.x & 63u) == 0) {
+        uint64_t* o = t + 8 * ((uint64_t)blockIdx.x * kWaves + wave_id());
+#pragma unroll
+        for (int i = 0; i < 5; ++i) o[i] = v[i];
+        o[5] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+        o[6] = __builtin_amdgcn_s_getreg(20 | (3 << 11));   // XCC_ID
+        o[7] = 0;
+    }
+}
+
 // Any pointer / length / seed (iovec batches, ragged and unaligned buffers).
-template <int G>
-__global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+// STAMP (probe builds): t0, tables built, first buffer done, loop done, end.
+template <int G, bool STAMP = false>
+__device__ __forceinline__ void crc64_batch_run(const Batch64Args& args, const LaneConsts64& kc, uint32_t* lds,
+                                                uint64_t* t) {
+    uint64_t ts[5] = {0, 0, 0, 0, 0};
+    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memrealtime();
     build_tables64<G>(lds, kc);
+    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
     const uint32_t grp = lane / G;
@@ -438,7 +455,21 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
         // crc.cpp:119-122: the register starts at ~crc and the result is inverted
         const uint64_t reg = buffer_reg64<G>(lds, p, n, ~seed, gl, lane, la);
         if (active && gl == 0) args.out[bi] = ~reg;
+        if constexpr (STAMP) {
+            if (ts[2] == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
+        }
     }
+    if constexpr (STAMP) {
+        ts[3] = __builtin_amdgcn_s_memrealtime();
+        ts[4] = ts[3];
+        stamp64_write(t, ts);
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, LaneConsts64 kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+    crc64_batch_run<G>(args, kc, lds, nullptr);
 }
 
 // Uniform batches (aligned base and stride, nbytes = R*16*G with R % U == 0):
@@ -710,11 +741,14 @@ __device__ __forceinline__ uint64_t mul_wave64(uint64_t v, uint64_t bw, uint32_t
     return xor_lanes64(((v >> lane) & 1ull) ? bw : 0ull, 64);
 }
 
-template <int G>
-__global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
-    __shared__ uint64_t red[2 * kWaves];
+// STAMP (probe builds): t0, tables built, basis words done, rounds done, end.
+template <int G, bool STAMP = false>
+__device__ __forceinline__ void crc64_long_run(const Long64Args& a, const LaneConsts64& kc, uint32_t* lds,
+                                               uint64_t* red, uint64_t* t) {
+    uint64_t ts[5] = {0, 0, 0, 0, 0};
+    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memrealtime();
     build_tables64<G>(lds, kc);
+    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memrealtime();
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = wave_id();
@@ -737,6 +771,10 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
     const uint64_t bw_z = basis_word64(a.zt[wave], lane);
     const uint64_t bw_f = wave == 0 ? basis_word64(a.ft[blockIdx.x], lane) : 0ull;
     const uint64_t bx0 = G == 32 ? basis_word64(a.x, l) : 0ull, bx1 = G == 32 ? basis_word64(a.x, l + 32) : 0ull;
+    if constexpr (STAMP) {
+        asm volatile("" ::"v"(bw_z), "v"(bw_f), "v"(bx0), "v"(bx1));  // the stamp after them
+        ts[2] = __builtin_amdgcn_s_memrealtime();
+    }
     uint64_t acc = 0, lastc = 0;  // uniform across the group (reg and the lane XOR are)
     for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
         const int64_t v = g + (int64_t)r * S;
@@ -754,6 +792,7 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
         acc = last ? m : m ^ reg;
         lastc = last ? reg : lastc;
     }
+    if constexpr (STAMP) ts[3] = __builtin_amdgcn_s_memrealtime();
     uint64_t v = acc;
     if constexpr (G == 32) {  // acc_0 * X ^ acc_1
         const uint64_t m = mul_group(acc, bx0, bx1);
@@ -779,6 +818,17 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
         u = mul_wave64(u, bw_f, lane) ^ e;  // * J Y^(grid - 1 - b), then the last chunk
         long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122: inverted out
     }
+    if constexpr (STAMP) {
+        ts[4] = __builtin_amdgcn_s_memrealtime();
+        stamp64_write(t, ts);
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneConsts64 kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+    __shared__ uint64_t red[2 * kWaves];
+    crc64_long_run<G>(a, kc, lds, red, nullptr);
 }
 
 }  // namespace pcrc

@@ -105,7 +105,10 @@ __global__ __launch_bounds__(1024) void group_rows_kernel(const uint8_t* base, u
 //           fetched before the current task runs);
 //   MODE 2: static for the first `static_rounds` rounds, tickets for the rest;
 //   MODE 3: as 2 with 8 per-XCC ticket regions and stealing across them;
-//   MODE 4: static with the chunk of workgroup b rotated by the round.
+//   MODE 4: static with the chunk of workgroup b rotated by the round;
+//   MODE 5: static, split by XCD parity (workgroup b on XCD b % 8): the
+//           even XCDs' waves take the first ntask/2 * (1 + static_rounds/1000)
+//           tasks, the odd XCDs' waves the rest (round-robin within each).
 // t[6*gw..6*gw+5] = s_memrealtime (100 MHz) at the wave start / end, HW_ID, XCC_ID,
 // s_memtime (shader clock) at the wave start / end: the in-kernel clock of a
 // wave is d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
@@ -141,7 +144,15 @@ __global__ __launch_bounds__(pcrc::kBlock) void crc_wave_times_kernel(pcrc::Batc
         const uint32_t crc = buffer_crc<G, 4>(lds, p, n, args.seed0, gl, la);
         if (active && gl == 0) args.out[bi] = crc;
     };
-    if (MODE == 4) {
+    if (MODE == 5) {
+        const uint64_t half = nwaves / 2;
+        const uint64_t par = blockIdx.x & 1u;
+        const uint64_t pidx = (uint64_t)(blockIdx.x >> 1) * kWaves + wave;
+        uint64_t e = (uint64_t)((double)ntask * 0.5 * (1000.0 + (double)static_rounds) / 1000.0);
+        if (e > ntask) e = ntask;
+        const uint64_t lo = par ? e : 0, hi = par ? ntask : e;
+        for (uint64_t wv = lo + pidx; wv < hi; wv += half) run(wv);
+    } else if (MODE == 4) {
         // Static, but workgroup b takes chunk (b + k) % grid in round k, so
         // every XCC (b % 8 under round-robin placement) cycles through every
         // chunk offset instead of always the same ones.
@@ -270,6 +281,23 @@ __global__ __launch_bounds__(1024) void group_rows_stamped_kernel(const uint8_t*
     ws.store(t, blockIdx.x * 16ull + wave);
 }
 
+// The product's CRC-64 long and batch kernels with per-wave stamps
+// (crc64_kernels.h crc64_long_run / crc64_batch_run, STAMP = true).
+template <int G>
+__global__ __launch_bounds__(pcrc::kBlock) void crc64_long_stamped_kernel(pcrc::Long64Args a, pcrc::LaneConsts64 kc,
+                                                                           uint64_t* t) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[pcrc::k64FLdsBytes / 4];
+    __shared__ uint64_t red[2 * pcrc::kWaves];
+    pcrc::crc64_long_run<G, true>(a, kc, lds, red, t);
+}
+
+template <int G>
+__global__ __launch_bounds__(pcrc::kBlock) void crc64_batch_stamped_kernel(pcrc::Batch64Args a, pcrc::LaneConsts64 kc,
+                                                                            uint64_t* t) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[pcrc::k64FLdsBytes / 4];
+    pcrc::crc64_batch_run<G, true>(a, kc, lds, t);
+}
+
 // The product's crc32c_long_kernel<G, 4> (one long buffer, chunks per lane
 // group: the same long_run) with 8 stamps per wave: s_memrealtime at the
 // start, after the LDS table prologue, after the wave's chunks and after the
@@ -330,7 +358,8 @@ int probe_crc_wave_times(const void* base, uint64_t nbytes, uint64_t count, uint
     if (g == 8) {
         if (mode == 1) WT(8, 1); else if (mode == 2) WT(8, 2); else if (mode == 3) WT(8, 3); else if (mode == 4) WT(8, 4); else WT(8, 0);
     } else {
-        if (mode == 1) WT(32, 1); else if (mode == 2) WT(32, 2); else if (mode == 3) WT(32, 3); else if (mode == 4) WT(32, 4); else WT(32, 0);
+        if (mode == 1) WT(32, 1); else if (mode == 2) WT(32, 2); else if (mode == 3) WT(32, 3); else if (mode == 4) WT(32, 4);
+        else if (mode == 5) WT(32, 5); else WT(32, 0);
     }
 #undef WT
     return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -478,6 +507,57 @@ int probe_long_stamped(const void* data, uint64_t n, uint32_t seed, uint32_t* ou
     }
 #undef LSG
 #undef LSK
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// crc64_long_stamped_kernel over [data, data + n) with the product's plan for
+// lanes x rounds (0 x 0: automatic); `state` 8 + 8 * 512 zeroed bytes, `t`
+// 8 words per wave of the grid (<= 256 x 16).
+int probe_crc64_long_stamped(const void* data, uint64_t n, uint64_t seed, uint64_t* out, uint64_t* state,
+                             uint64_t* t, int cus, int lanes, int rounds, int* grid_out, void* stream) {
+    using namespace pcrc;
+    const LongPlan lp = long_plan_for(data, n, cus, (uint32_t)lanes | (uint32_t)rounds << 8, 0, true);
+    const LongPowers& pw = long_powers(lp, true);
+    Long64Args a{};
+    long_args64(&a, lp, pw, data, seed, out);
+    a.acc = state;
+    a.treset = 1;
+    LaneConsts64 kc{};
+    kc.kshift = xpow64(8ull * 16ull * (uint64_t)lp.lanes);
+    for (int i = 0; i < 64; ++i) kc.sbasis[i] = mulmod64(1ull << i, kc.kshift);
+    *grid_out = (int)lp.grid;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (lp.lanes == 64)
+        hipLaunchKernelGGL((crc64_long_stamped_kernel<64>), dim3(lp.grid), dim3(kBlock), 0, s, a, kc, t);
+    else
+        hipLaunchKernelGGL((crc64_long_stamped_kernel<32>), dim3(lp.grid), dim3(kBlock), 0, s, a, kc, t);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// crc64_batch_stamped_kernel<g> over count strided buffers (one workgroup per
+// CU as the product); `t` 8 words per wave.
+int probe_crc64_batch_stamped(const void* base, uint64_t nbytes, uint64_t count, uint64_t* out, uint64_t* t, int g,
+                              int cus, void* stream) {
+    using namespace pcrc;
+    if (g != 32 && g != 64) return -22;
+    Batch64Args a{};
+    a.base = static_cast<const uint8_t*>(base);
+    a.stride = nbytes;
+    a.nbytes = nbytes;
+    a.count = count;
+    a.out = out;
+    a.seed0 = 0;
+    LaneConsts64 kc{};
+    kc.kshift = xpow64(8ull * 16ull * (uint64_t)g);
+    for (int i = 0; i < 64; ++i) kc.sbasis[i] = mulmod64(1ull << i, kc.kshift);
+    const uint64_t waves = (count + 64 / g - 1) / (64 / g);
+    uint64_t grid = (waves + kWaves - 1) / kWaves;
+    if (grid > (uint64_t)cus) grid = cus;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (g == 64)
+        hipLaunchKernelGGL((crc64_batch_stamped_kernel<64>), dim3(grid), dim3(kBlock), 0, s, a, kc, t);
+    else
+        hipLaunchKernelGGL((crc64_batch_stamped_kernel<32>), dim3(grid), dim3(kBlock), 0, s, a, kc, t);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
