@@ -67,7 +67,8 @@ int photon_crc_set_msg_rows(int rows_per_step);
  * CRC width (photonlibos_amd/csrc/long_plan.h long_plan_for, which lists the
  * measurements behind each step): CRC-32C 64 lanes x 2 rounds, 32 x 2 from
  * 512 MiB, 64 x 4 from 1.5 GiB, 64 x 2 from 3 GiB; CRC-64 64 lanes x 1
- * round, 2 from 1 GiB, 4 from 1.5 GiB, 2 from 3 GiB. */
+ * round, 64 x 2 from 512 MiB, 32 x 2 from 1 GiB, 64 x 4 from 1.5 GiB, 64 x 2
+ * from 3 GiB. */
 int photon_crc_set_long_shape(int lanes, int rounds);
 
 /* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =

@@ -1409,8 +1409,8 @@ __global__ void crc32c_trim_kernel(const photon_crc_component* all, const photon
 //   group: Horner over its rounds, acc <- acc X^S ^ c (basis words of X^S
 //          from the host);
 //   wave (GPW = 2): acc_0 X ^ acc_1 (basis words of X from the host);
-//   wave: * Z^(15 - w) (basis words computed at kernel start from the
-//          host's constant, 31 select steps per lane, off the tail);
+//   wave: * Z^(15 - w) (basis words from the host's constant through the
+//          LDS D tables at kernel start, basis_word_lds: 4 lookups per lane);
 //   workgroup: XOR of its waves in LDS, * J Y^(grid - 1 - b) (wave 0, basis
 //          words computed at kernel start), ^ c_last in the last workgroup;
 //   grid: the workgroups' values XORed by long_reduce.
@@ -1526,12 +1526,24 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64
 // v * x mod P (reflected: bit j = coefficient of x^(31-j)).
 __device__ __forceinline__ uint32_t mulx(uint32_t v) { return (v >> 1) ^ ((0u - (v & 1u)) & kPoly); }
 
-// Basis word i of a multiplication by c: (1 << i) * c = c * x^(31-i), by
-// 31 select steps (wave-uniform trip count; once per kernel).
-__device__ __forceinline__ uint32_t basis_word(uint32_t c, uint32_t i) {
-#pragma unroll 1
-    for (uint32_t k = 0; k < 31; ++k) c = k < 31 - i ? mulx(c) : c;
-    return c;
+// Basis word i of a multiplication by c: (1 << i) * c = c * x^(31-i), from
+// the D tables in LDS (after build_tables): k = 31 - i = 8a + b; the bit part
+// c * x^b = (c >> b) ^ D3[(c << (8 - b)) & 0xff] (D3[v] = v * x^8: the b bits
+// shifted out are a byte shifted out 8 - b positions early), the byte part
+// c1 * x^(8a) = (c1 >> 8a) ^ XOR_(j < a) D_(4-(a-j))[byte_j(c1)] (slice t holds
+// v * x^(32 - 8t)). 4 lookups instead of 31 dependent select steps (crc64:
+// basis_word64_lds). Lanes with a <= j look up entry 0 (= 0).
+__device__ __forceinline__ uint32_t basis_word_lds(const uint32_t* lds, uint32_t c, uint32_t i, uint32_t r4) {
+    const uint32_t k = 31u - i, b = k & 7u, a = k >> 3;
+    const uint32_t y = (c << (8u - b)) & 0xffu;
+    const uint32_t v = (c >> b) ^ lds_word(lds, (y << 8) + 3u * 32u + r4);
+    uint32_t r = v >> (8u * a);
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        const uint32_t byte = j < a ? (v >> (8u * j)) & 0xffu : 0u;
+        r ^= lds_word(lds, (byte << 8) + (((4u + j - a) & 3u) << 5) + r4);
+    }
+    return r;
 }
 
 // v * c for a v held by every lane of a 32-lane half (lane l of the half
@@ -1625,11 +1637,12 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
     const int64_t S = (int64_t)a.stride;
     const int64_t g = ((int64_t)blockIdx.x * kWaves + wave) * GPW + grp;
     // Basis words: X^S and X from the host; Z^(15 - w) and (wave 0) the
-    // workgroup factor computed here, before any chunk.
+    // workgroup factor from the LDS tables here, before any chunk.
     const uint32_t bw_xs = a.xsb[l32];
     const uint32_t bw_x = G == 32 ? a.xb[l32] : 0u;
-    const uint32_t bw_z = basis_word(a.zt[wave], l32);
-    const uint32_t bw_f = wave == 0 ? basis_word(a.ft[blockIdx.x], l32) : 0u;
+    const uint32_t bw_z = basis_word_lds(lds, a.zt[wave], l32, la.r4);
+    const uint32_t bw_f = wave == 0 ? basis_word_lds(lds, a.ft[blockIdx.x], l32, la.r4) : 0u;
+    asm volatile("" ::"v"(bw_z), "v"(bw_f));  // done before the chunk loop (crc64_long_run)
     uint32_t acc = 0, lastc = 0;
     // Rounds; a first round -1 when the head is slot -1 (D = 0: group S-1).
     for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
@@ -1734,6 +1747,8 @@ struct SmallArgs {
     uint32_t k;          // grid end - data end (0..31): the result is multiplied by x^(-8k)
     uint32_t seed;
     uint32_t wg0;        // workgroup index of blockIdx.x == 0 (kSmallWg - grid)
+    uint32_t tag;        // slots mode: nonzero = 64-bit slots {tag, value} stored at system scope (the
+                         // host spins on the tags instead of waiting for the stream)
 };
 
 // p * K through the nibble-sliced tables of K at T (8 conflict-free lookups).
@@ -1816,7 +1831,13 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
         uint32_t u = red[0] ^ red[1] ^ red[2] ^ red[3];
         u = mul_lanes(u, bw_tail, l32);  // x^(-8k): the zero bytes after the end (linear: per workgroup)
         if (a.slots) {
-            if (lane == 0) a.slots[blockIdx.x] = u;
+            if (lane == 0) {
+                if (a.tag)  // one 8-byte store: the host never sees a tag without its value
+                    __hip_atomic_store(reinterpret_cast<uint64_t*>(a.slots) + blockIdx.x,
+                                       (uint64_t)a.tag << 32 | u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else
+                    a.slots[blockIdx.x] = u;
+            }
         } else {
             long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
         }

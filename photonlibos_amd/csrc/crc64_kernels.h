@@ -723,17 +723,32 @@ struct Long64Args {
 
 __device__ __forceinline__ uint64_t mulx64(uint64_t v) { return (v >> 1) ^ ((0ull - (v & 1ull)) & kPoly64); }
 
-// (1 << i) * c = c * x^(63-i) (63 select steps, once per kernel).
-__device__ __forceinline__ uint64_t basis_word64(uint64_t c, uint32_t i) {
-#pragma unroll 1
-    for (uint32_t k = 0; k < 63; ++k) c = k < 63 - i ? mulx64(c) : c;
-    return c;
-}
-
 __device__ __forceinline__ uint64_t xor_lanes64(uint64_t v, int width) {
     const uint32_t lo = width == 64 ? group_xor<64>((uint32_t)v) : group_xor<32>((uint32_t)v);
     const uint32_t hi = width == 64 ? group_xor<64>((uint32_t)(v >> 32)) : group_xor<32>((uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
+}
+
+// The same basis word from the D64 tables in LDS (after build_tables64):
+// c * x^k with k = 63 - i = 8a + b. Bit part: c * x^b = (c >> b) ^ T[(c <<
+// (8 - b)) & 0xff] with T = slice 7 (v * x^8: the b bits shifted out are a
+// byte shifted out 8 - b positions early). Byte part: c1 * x^(8a) = (c1 >>
+// 8a) ^ XOR_(j < a) byte_j(c1) * x^(8 (a - j)), slice 8 - (a - j) holding v *
+// x^(8 (a - j)) (slice t = (v << 8t) * x^64). 8 lookups and ~30 VALU instead
+// of 63 dependent select steps (4-12 us of every launch's prologue at 64- /
+// 32-lane groups, repo:profiles/r04_probe_long_vs_batch64.jsonl). Lanes
+// whose a <= j look up entry 0 (= 0) of some slice.
+__device__ __forceinline__ uint64_t basis_word64_lds(const uint32_t* lds, uint64_t c, uint32_t i, uint32_t r8) {
+    const uint32_t k = 63u - i, b = k & 7u, a = k >> 3;
+    const uint32_t y = (uint32_t)(c << (8u - b)) & 0xffu;
+    const uint64_t v = (c >> b) ^ u64of(lds_u2(lds, (y << 8) + (7u << 5) + r8));
+    uint64_t r = v >> (8u * a);
+#pragma unroll
+    for (uint32_t j = 0; j < 7; ++j) {
+        const uint32_t byte = j < a ? (uint32_t)(v >> (8u * j)) & 0xffu : 0u;
+        r ^= u64of(lds_u2(lds, (byte << 8) + (((8u + j - a) & 7u) << 5) + r8));
+    }
+    return r;
 }
 
 // v * c for a v held by every lane of a wave, lane l holding basis word l of c.
@@ -768,13 +783,15 @@ __device__ __forceinline__ void crc64_long_run(const Long64Args& a, const LaneCo
     };
     // The wave's and (wave 0) the workgroup's factor: basis words computed
     // here, one per lane, before any chunk; X's for the 32-lane form.
-    const uint64_t bw_z = basis_word64(a.zt[wave], lane);
-    const uint64_t bw_f = wave == 0 ? basis_word64(a.ft[blockIdx.x], lane) : 0ull;
-    const uint64_t bx0 = G == 32 ? basis_word64(a.x, l) : 0ull, bx1 = G == 32 ? basis_word64(a.x, l + 32) : 0ull;
-    if constexpr (STAMP) {
-        asm volatile("" ::"v"(bw_z), "v"(bw_f), "v"(bx0), "v"(bx1));  // the stamp after them
-        ts[2] = __builtin_amdgcn_s_memrealtime();
-    }
+    const uint64_t bw_z = basis_word64_lds(lds, a.zt[wave], lane, la.r8);
+    const uint64_t bw_f = wave == 0 ? basis_word64_lds(lds, a.ft[blockIdx.x], lane, la.r8) : 0ull;
+    const uint64_t bx0 = G == 32 ? basis_word64_lds(lds, a.x, l, la.r8) : 0ull;
+    const uint64_t bx1 = G == 32 ? basis_word64_lds(lds, a.x, l + 32, la.r8) : 0ull;
+    // Complete them here: left to the scheduler, their LDS lookups were
+    // spread into the round loop and slowed it (1 GiB, 32 lanes: 0.192 vs
+    // 0.169 ms with this barrier, repo:profiles/r04f_ab_long_basis_lds.jsonl).
+    asm volatile("" ::"v"(bw_z), "v"(bw_f), "v"(bx0), "v"(bx1));
+    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memrealtime();
     uint64_t acc = 0, lastc = 0;  // uniform across the group (reg and the lane XOR are)
     for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
         const int64_t v = g + (int64_t)r * S;

@@ -55,17 +55,20 @@ inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t sh
     //  CRC-32C: 256 MiB 64x2 0.0541 (0.0545); 512 MiB 64x1 0.0919, 32x2
     //    0.0937 (0.0889); 1 GiB 32x2 0.1679, 64x2 0.169, 64x1 0.179 (0.1647);
     //    2 GiB 64x4 0.3242, 32x2 0.3425 (0.3186); 4 GiB 64x2 0.6328 (0.6236)
-    //  CRC-64: 256 MiB 64x1 0.0575 (0.058); 512 MiB 64x1 0.0961 (0.089);
-    //    1 GiB 64x2 0.1722, 64x1 0.1843 (0.1658); 2 GiB 64x4 0.3273 (0.322);
-    //    4 GiB 64x2 0.6341 (0.6304)
+    //  CRC-64: 256 MiB 64x1 0.0575 (0.058); 2 GiB 64x4 0.3273 (0.322);
+    //    4 GiB 64x2 0.6341 (0.6304); with the LDS basis words
+    //    (repo:profiles/r04g_ab_long_basis_barrier.jsonl): 512 MiB 64x2
+    //    0.0957, 32x2 0.0979, 64x1 0.1011 (0.0893); 1 GiB 32x2 0.1709, 64x2
+    //    0.1771, 64x1 0.1882 (0.1668)
     //  up to 256 KiB (CRC-64 only: CRC-32C has its small kernel): 1 round of
     //  chunks of >= 4 KiB, one workgroup
     const bool small = n <= (256u << 10);
     const uint64_t mib = n >> 20;
-    const int lanes = (shape & 0xff) ? (int)(shape & 0xff) : (!crc64 && mib >= 512 && mib < 1536) ? 32 : 64;
+    const int lanes = (shape & 0xff) ? (int)(shape & 0xff)
+                    : (crc64 ? mib >= 1024 && mib < 1536 : mib >= 512 && mib < 1536) ? 32 : 64;
     uint64_t rounds = (shape >> 8) ? shape >> 8
                     : small ? 1
-                    : crc64 ? (mib < 1024 ? 1 : mib < 1536 ? 2 : mib < 3072 ? 4 : 2)
+                    : crc64 ? (mib < 512 ? 1 : mib < 1536 ? 2 : mib < 3072 ? 4 : 2)
                             : (mib < 1536 ? 2 : mib < 3072 ? 4 : 2);
     const uint64_t gpw = 64 / (uint64_t)lanes;
     const uint64_t maxgrid = (uint64_t)cus < kLongMaxFt ? (uint64_t)cus : kLongMaxFt;

@@ -148,10 +148,58 @@ def test_reference_perf_shape_is_balanced():
     """1 GiB at buf+1 on 256 CUs (the automatic 32 lanes x 2 rounds): no empty
     slot, the head and the short last chunk share one group's last slot, so
     every lane group reads exactly 2 x 64 KiB (round 3's cut: 130 KiB for most
-    groups, 65 KiB for 250 of them)."""
+    groups, 65 KiB for 250 of them); CRC-64 takes the same shape."""
     p = _plan(4096 * 100 + 1, 1 << 30, 256)
     assert (p["lanes"], p["R"], p["grid"]) == (32, 2, 256)
     assert p["chunk"] == 64 << 10 and p["D"] == 0 and p["T"] == p["R"] * p["S"]
     assert p["head"] + p["L"] == p["chunk"]  # group S-1: head + (R-1) chunks + the short one = R chunks
     p64 = _plan(4096 * 100 + 1, 1 << 30, 256, crc64=True)
-    assert (p64["lanes"], p64["R"]) == (64, 2) and p64["head"] + p64["L"] == p64["chunk"] and p64["D"] == 0
+    assert (p64["lanes"], p64["R"]) == (32, 2) and p64["head"] + p64["L"] == p64["chunk"] and p64["D"] == 0
+
+
+def _mulx(v, width):
+    return (v >> 1) ^ ((P32 if width == 32 else P64) if v & 1 else 0)
+
+
+def _basis_word_lds(c, i, width):
+    """basis_word_lds / basis_word64_lds (crc32c_kernels.h, crc64_kernels.h)
+    restated over the LDS D tables' contents: slice t, byte v -> (v << 8t) *
+    x^width (the D table: one data word absorbed), so slice (nslices - 1) is
+    the classic byte table v * x^8."""
+    ns = width // 8
+
+    def slice_entry(t, v):
+        return _mulmod(v << (8 * t), _xpow(width, width), width)
+
+    k = width - 1 - i
+    b, a = k & 7, k >> 3
+    y = (c << (8 - b)) & 0xFF
+    v = (c >> b) ^ slice_entry(ns - 1, y)
+    r = v >> (8 * a)
+    for j in range(ns - 1):
+        byte = (v >> (8 * j)) & 0xFF if j < a else 0
+        r ^= slice_entry((ns + j - a) % ns, byte)
+    return r
+
+
+def _xpow(e, width):
+    """x^e mod P in the reflected representation (bit width-1 = x^0)."""
+    r = 1 << (width - 1)
+    for _ in range(e):
+        r = _mulx(r, width)
+    return r
+
+
+@pytest.mark.parametrize("width", [32, 64])
+def test_basis_words_from_the_byte_tables(width):
+    """The long kernels' basis words (1 << i) * c = c * x^(width-1-i), taken
+    from the byte tables in LDS, equal the bit-serial definition for every i."""
+    rng = np.random.default_rng(0x5EED0E20 + width)
+    for _ in range(8):
+        c = int(rng.integers(0, 1 << 62)) | (int(rng.integers(0, 4)) << 62) if width == 64 else int(rng.integers(0, 1 << 32))
+        for i in range(width):
+            want = c
+            for _ in range(width - 1 - i):
+                want = _mulx(want, width)
+            assert _basis_word_lds(c, i, width) == want, (width, hex(c), i)
+            assert want == _mulmod(1 << i, c, width)
