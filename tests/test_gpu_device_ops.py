@@ -218,6 +218,43 @@ def test_device_dispatch_dropin(torch_dev, oracle):
     assert ck.crc32c_extend_at(hbuf.ctypes.data, n, 77) == expect
 
 
+def test_device_dispatch_small_buffers_threads(torch_dev, oracle):
+    """Routed crc32c_extend on small device buffers (the small kernel, its
+    per-workgroup words collected by spinning on tagged slots in the routed
+    stream's pinned area) from 8 threads at once, 1 B .. 256 KiB at odd
+    offsets and seeds, back to back: every result equals the oracle's."""
+    import threading
+    torch = torch_dev
+    n = 1 << 20
+    dbuf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(dbuf, n, n, 1, 0x5EED0410)
+    torch.cuda.synchronize()
+    host = dbuf.cpu().numpy()
+    rng = random.Random(0x5EED0411)
+    cases = []
+    for _ in range(8 * 60):
+        ln = rng.choice([1, 15, 16, 17, 4095, 4096, 65537, 131072, 200000, 262144])
+        off = rng.randrange(0, n - ln)
+        seed = rng.getrandbits(32)
+        cases.append((off, ln, seed, oracle.crc32c(host[off:off + ln], seed)))
+    bad = []
+    ck.set_device_dispatch(True)
+
+    def worker(k):
+        for off, ln, seed, want in cases[k::8]:
+            got = ck.crc32c_extend_at(dbuf.data_ptr() + off, ln, seed)
+            if got != want:
+                bad.append((k, off, ln, seed, got, want))
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    ck.set_device_dispatch(False)
+    assert not bad, bad[:5]
+
+
 def test_device_dispatch_series_follows_saved_host_engine(torch_dev, oracle):
     # ADVICE r1 (low): a routed crc32c_series on device memory follows the
     # host engine it replaced -- crc32c_series_sw computes real CRCs for parts
