@@ -1870,6 +1870,9 @@ int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_ou
     if (!rc) {
         r->tag = r->tag == 0xffffffffu ? 1u : r->tag + 1u;
         sa.tag = r->tag;
+        // the previous call on this stream saw all its slots land: nothing
+        // writes them now, and no slot can carry this tag before the launch
+        memset(r->h, 0, 8ull * sgrid);
         sa.slots = static_cast<uint32_t*>(r->d);
         hipLaunchKernelGGL(crc32c_small_kernel, dim3(sgrid), dim3(256), 0, r->st, sa);
         const hipError_t e = hipGetLastError();
