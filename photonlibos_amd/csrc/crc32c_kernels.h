@@ -1466,6 +1466,11 @@ struct LongArgs {
 // ... sc1; s_waitcnt vmcnt(0); global_atomic_add ... sc0; s_waitcnt
 // vmcnt(0); ... global_load_dword ... sc1. The stores-in-vmcnt rule is GFX9's
 // (GFX10+ count stores in vscnt), hence the #error for other targets below.
+// Measured and not kept (round 4): tagged slots {launch tag, word} stored
+// without waiting and a ticket taken at once, the last workgroup reloading
+// until every tag is this launch's -- one acknowledgement less on paper,
+// ±0 for CRC-32C and 1.9 µs slower for CRC-64 on 1 GiB
+// (repo:profiles/r04_ab_tagged_reduce.jsonl).
 // FENCED (bench probe, ABL 8) keeps the release/acquire pair: 5.7 µs more
 // per 1 GiB launch (repo:profiles/r03b_ab_long_tail_ablations.jsonl). Round
 // 3's first form, device-scope atomicXor into one accumulator or eight with
