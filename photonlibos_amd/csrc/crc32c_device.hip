@@ -1369,6 +1369,11 @@ int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t
     a.seeds = d_seeds;
     a.out = d_out;
     a.seed0 = seed0;
+    if (PCRC64_SHIFT_INIT && !d_seeds && !(reinterpret_cast<uintptr_t>(d_base) & 15) && !(stride & 15) &&
+        nbytes >= 64) {
+        a.shift_init = 1;
+        a.init_shift = mulmod64(~seed0, xpow64(8ull * nbytes));
+    }
     return launch_batch64(a, nbytes, static_cast<hipStream_t>(stream));
 }
 

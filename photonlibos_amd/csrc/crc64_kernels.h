@@ -7,6 +7,16 @@
 #ifndef PCRC64_U
 #define PCRC64_U 2  // rows per step of the CRC-64 batch kernel (2 > 4 by 0.9 points on the C2 shape; A/B builds: -DPCRC64_U=4)
 #endif
+// 16-lane groups: the finish's second level lane-parallel (finish_xor16);
+// A/B builds: -DPCRC64_FIN16=0 for the two dependent 16-lookup levels.
+#ifndef PCRC64_FIN16
+#define PCRC64_FIN16 1
+#endif
+// Aligned strided batches take the init at the end (Batch64Args::shift_init;
+// A/B builds: -DPCRC64_SHIFT_INIT=0).
+#ifndef PCRC64_SHIFT_INIT
+#define PCRC64_SHIFT_INIT 1
+#endif
 // Bench-only ablation builds of buffer_reg64 (-DPCRC64_ABL=bits; results are
 // then NOT CRCs): 1 = no head masking, 2 = no finish multiply, 4 = no group
 // XOR, 8 = row shift replaced by an XOR (no S lookups), 16 = lagged block
@@ -73,6 +83,12 @@ struct Batch64Args {
     const uint64_t* seeds;
     uint64_t* out;
     uint64_t seed0;
+    // Aligned strided batches without per-buffer seeds: buffers start at 16-B
+    // boundaries, so nothing is masked, and the inverted init enters at the
+    // end as (~seed0) * x^(8 nbytes) (linearity, crc.cpp:393-405) instead of
+    // being XORed into every buffer's first words by two lanes per group.
+    uint64_t init_shift;
+    uint32_t shift_init;
 };
 
 struct Uniform64Args {
@@ -326,12 +342,32 @@ __device__ __forceinline__ uint64_t finish64(uint2 q, uint32_t d, const uint32_t
     return x;
 }
 
+__device__ __forceinline__ uint64_t group_xor64_16(uint64_t v) {
+    return ((uint64_t)group_xor<16>((uint32_t)(v >> 32)) << 32) | group_xor<16>((uint32_t)v);
+}
+
+// finish64<16> and the group XOR in one, with the second level lane-parallel:
+// lanes with d < 8 keep Q * A_d; the lanes with d >= 8 first XOR their Q *
+// A_(d-8) (= U), and U * x^1024 = XOR over positions t of B_1[t][nibble t of
+// U] is looked up ONE position per lane (lane gl takes position gl) and XORed
+// across the group: 16 + 1 lookups per lane instead of 16 + 16 dependent.
+__device__ __forceinline__ uint64_t finish_xor16(uint2 q, uint32_t d, const uint32_t* lds, uint32_t gl,
+                                                 uint32_t lane) {
+    const uint64_t x = nib_mul64(u64of(q), lds, k64FBase + (d & 7u) * 2048u, lane);
+    const bool hi = d >= 8u;
+    const uint64_t lo_sum = group_xor64_16(hi ? 0ull : x);
+    const uint64_t u = group_xor64_16(hi ? x : 0ull);
+    const uint64_t b = u64of(lds_u2(lds, k64FBBase + (((uint32_t)(u >> (4u * gl))) & 15u) * 128u + gl * 8u));
+    return lo_sum ^ group_xor64_16(b);
+}
+
 // The raw CRC-64 register after the bytes [p, p+n) from `init` (a group of
 // G lanes; valid on the group's first lane; crc64ecma_extend = ~reg with
 // init = ~crc, crc.cpp:119-122).
 template <int G>
 __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint8_t* p, uint64_t n, uint64_t init,
-                                                 uint32_t gl, uint32_t lane, const LaneAddr64& la) {
+                                                 uint32_t gl, uint32_t lane, const LaneAddr64& la,
+                                                 bool head = true) {
     constexpr int U = PCRC64_U;
     uint64_t reg;
     if (n < 64) {
@@ -368,7 +404,7 @@ __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint
         // Row 0 (head: masked leading bytes + inverted init).
         if (gl < nb) {
             uint4 w = w0;
-            if (!(PCRC64_ABL & 1) && gl < 2) {
+            if (head && !(PCRC64_ABL & 1) && gl < 2) {  // head == false: aligned, init 0
                 const uint64_t lo = head_word64(((uint64_t)w.y << 32) | w.x, (int)gl * 16, s0, init);
                 const uint64_t hi = head_word64(((uint64_t)w.w << 32) | w.z, (int)gl * 16 + 8, s0, init);
                 w = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
@@ -400,8 +436,13 @@ __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint
         }
         if (part) pc = sstep64(lds, pc, la, lag16_64(lds, wp, la));
         // Q * x^(64 + 128 d) (Q -> P and the shift to the end of the blocks), XOR over the group.
-        const uint64_t f = (PCRC64_ABL & 2) ? u64of(pc) : finish64<G>(pc, (rlast + G - 1 - gl) & (G - 1), lds, lane);
-        reg = (PCRC64_ABL & 4) ? f : ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+        const uint32_t d = (rlast + G - 1 - gl) & (G - 1);
+        if constexpr (G == 16 && PCRC64_FIN16 && !(PCRC64_ABL & 6)) {
+            reg = finish_xor16(pc, d, lds, gl, lane);
+        } else {
+            const uint64_t f = (PCRC64_ABL & 2) ? u64of(pc) : finish64<G>(pc, d, lds, lane);
+            reg = (PCRC64_ABL & 4) ? f : ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+        }
         if (gl == 0)
             for (const uint8_t* q = eb; q < e; ++q) reg = bytestep64(lds, reg, load8(q), la);
     }
@@ -453,7 +494,8 @@ __device__ __forceinline__ void crc64_batch_run(const Batch64Args& args, const L
             if (args.seeds) seed = args.seeds[bi];
         }
         // crc.cpp:119-122: the register starts at ~crc and the result is inverted
-        const uint64_t reg = buffer_reg64<G>(lds, p, n, ~seed, gl, lane, la);
+        const uint64_t reg = args.shift_init ? buffer_reg64<G>(lds, p, n, 0ull, gl, lane, la, false) ^ args.init_shift
+                                             : buffer_reg64<G>(lds, p, n, ~seed, gl, lane, la);
         if (active && gl == 0) args.out[bi] = ~reg;
         if constexpr (STAMP) {
             if (ts[2] == 0) ts[2] = __builtin_amdgcn_s_memrealtime();

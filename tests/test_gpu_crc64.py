@@ -46,7 +46,7 @@ def test_golden_checksum_crc64(torch_dev, golden_in):
     assert [int(x) for x in got] == golden_in["crc64ecma"]
 
 
-@pytest.mark.parametrize("g", [0, 4, 64])
+@pytest.mark.parametrize("g", [0, 4, 16, 64])
 def test_alphabet_and_reference_vectors(torch_dev, ref_vectors, g):
     ck.set_lanes_per_buffer(g)
     rv = ref_vectors
