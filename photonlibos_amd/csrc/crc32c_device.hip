@@ -1069,6 +1069,10 @@ int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nb
     a.seeds = d_seeds;
     a.out = d_out;
     a.seed0 = seed0;
+    if (PCRC_SHIFT_INIT && !d_seeds && !(reinterpret_cast<uintptr_t>(d_base) & 15) && !(stride & 15) && nbytes >= 64) {
+        a.shift_init = 1;
+        a.init_shift = mulmod(seed0, xpow(8ull * nbytes));
+    }
     return launch_batch(a, nbytes, static_cast<hipStream_t>(stream));
 }
 

@@ -27,6 +27,11 @@
 #ifndef PCRC_BODY
 #define PCRC_BODY 0
 #endif
+// Aligned strided batches take the seed at the end (BatchArgs::shift_init;
+// A/B builds: -DPCRC_SHIFT_INIT=0).
+#ifndef PCRC_SHIFT_INIT
+#define PCRC_SHIFT_INIT 1
+#endif
 
 namespace pcrc {
 
@@ -99,6 +104,11 @@ struct BatchArgs {
     const uint64_t* msg_start;
     uint64_t nmsg;
     uint32_t* msg_out;
+    // Aligned strided batches without per-buffer seeds (buffer mode only):
+    // no head to mask, and the seed enters at the end as seed0 * x^(8 nbytes)
+    // (linearity, crc.cpp:393-405) instead of through every lane's head words.
+    uint32_t init_shift;
+    uint32_t shift_init;
 };
 
 __device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_addr) {
@@ -515,16 +525,19 @@ __device__ __forceinline__ void buf_preload(const BufGeo& g, uint32_t gl, BufPre
 // The lane's lagged column partial Q over every row (the preloaded ones first).
 template <int G, int U, bool LEAD = false>
 __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& g, const BufPre<U, LEAD>& pre,
-                                             uint32_t seed, uint32_t gl, const LaneAddr& la) {
+                                             uint32_t seed, uint32_t gl, const LaneAddr& la, bool head = true) {
     if (g.tiny) return 0;
     // Row 0 holds the head: masked leading bytes + seed (branch-free; lanes
     // without a block in row 0 feed a zero block, whose lagged CRC is 0).
+    // head == false (uniform): an aligned buffer whose seed enters later.
     uint4 w = pre.w0;
-    const int off = (int)gl * 16;
-    w.x = head_word_sel(w.x, off, g.s0, seed);
-    w.y = head_word_sel(w.y, off + 4, g.s0, seed);
-    w.z = head_word_sel(w.z, off + 8, g.s0, seed);
-    w.w = head_word_sel(w.w, off + 12, g.s0, seed);
+    if (head) {
+        const int off = (int)gl * 16;
+        w.x = head_word_sel(w.x, off, g.s0, seed);
+        w.y = head_word_sel(w.y, off + 4, g.s0, seed);
+        w.z = head_word_sel(w.z, off + 8, g.s0, seed);
+        w.w = head_word_sel(w.w, off + 12, g.s0, seed);
+    }
     if (gl >= g.nb) w = make_uint4(0, 0, 0, 0);
     uint32_t pc = lag16(lds, w, la);
     // Full rows 1..full-1: U rows per step, the next U in flight.
@@ -644,11 +657,11 @@ __device__ __forceinline__ uint32_t buf_finish(const uint32_t* lds, const BufGeo
 // the result is valid on every lane of the group.
 template <int G, int U, bool LEAD = false>
 __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_t* p, uint64_t n, uint32_t seed,
-                                               uint32_t gl, const LaneAddr& la) {
+                                               uint32_t gl, const LaneAddr& la, bool head = true) {
     const BufGeo g = buf_geo<G>(p, n, gl);
     BufPre<U, LEAD> pre;
     buf_preload<G, U, LEAD>(g, gl, pre);
-    const uint32_t pc = buf_body<G, U, LEAD>(lds, g, pre, seed, gl, la);
+    const uint32_t pc = buf_body<G, U, LEAD>(lds, g, pre, seed, gl, la, head);
     return buf_finish<G>(lds, g, pc, p, n, seed, gl, la);
 }
 
@@ -810,8 +823,9 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             }
             if (args.seeds) seed = args.seeds[bi];
         }
-        const uint32_t crc = buffer_crc<G, U, PCRC_BATCH_LEAD>(lds, p, n, seed, gl, la);
-        if (active && gl == 0) args.out[bi] = crc;
+        const uint32_t crc = buffer_crc<G, U, PCRC_BATCH_LEAD>(lds, p, n, args.shift_init ? 0u : seed, gl, la,
+                                                               !args.shift_init);
+        if (active && gl == 0) args.out[bi] = crc ^ args.init_shift;  // init_shift is 0 unless shift_init
     }
 }
 
