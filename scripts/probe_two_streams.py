@@ -9,7 +9,8 @@ the C2 batch launched three ways (bench-only probe; one variant per process):
 Prints one JSON line: GiB/s over the timed steps (wall, synchronised), ms per
 step, and the CRCs checked against the single-stream result of step 0.
 
-  python scripts/probe_two_streams.py single|forkjoin|free
+  python scripts/probe_two_streams.py single|forkjoin|free|shape:G:U
+  (shape:G:U = single with lanes per buffer G and rows per step U, tuning.h)
 """
 import json
 import os
@@ -23,6 +24,10 @@ sys.path.insert(0, REPO)
 from photonlibos_amd import checksum as ck  # noqa: E402
 
 mode = sys.argv[1]
+if mode.startswith("shape:"):
+    _, g_, u_ = mode.split(":")
+    ck.set_lanes_per_buffer(int(g_))
+    ck.set_generic_rows(int(u_))
 W, K = 5, 20
 n, cnt = 65536, 65536
 h = cnt // 2
@@ -35,7 +40,7 @@ want = torch.zeros(cnt, dtype=torch.int32, device="cuda")
 
 
 def step():
-    if mode == "single":
+    if mode == "single" or mode.startswith("shape:"):
         ck.batch_strided(buf, n, n, cnt, out, stream=main)
         return
     if mode == "forkjoin":
