@@ -487,7 +487,12 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    const int g = choose_lanes(typical_len);
+    int g = choose_lanes(typical_len);
+    // 4-8 KiB CRC-64 buffers: 16 lanes (one-level finish + lane-parallel
+    // second level, init at the end): 80.7 vs 79.8 % and 79.2 vs 79.2 % on
+    // two boxes (repo:profiles/r04_ab_crc64_c3_lanes8_vs_16.jsonl,
+    // r04_ab_crc64_shift_init.jsonl)
+    if (!g_lanes_override.load(std::memory_order_relaxed) && typical_len >= 4096 && typical_len <= 8192) g = 16;
     const uint64_t gpw = 64 / g;
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
