@@ -868,6 +868,73 @@ int small_image(int dev, const uint32_t** out) {
     return 0;
 }
 
+// The CRC-64 small kernel's image (crc64_kernels.h crc64_small_kernel), as
+// small_image: nibble tables [position][value] of x^64, x^(128 V), x^(64 +
+// 128 dl), x^(1024 dh), then the wave and tail basis words.
+std::vector<uint64_t> small64_image_host() {
+    std::vector<uint64_t> img(kSm64Image / 8, 0ull);
+    auto nibbles = [&](uint32_t off, uint64_t k) {  // (v << 4t) * k, t < 16, v < 16
+        for (uint32_t t = 0; t < 16; ++t)
+            for (uint32_t v = 0; v < 16; ++v) img[off / 8 + t * 16 + v] = mulmod64((uint64_t)v << (4 * t), k);
+    };
+    nibbles(kSm64D, xpow64(64));
+    nibbles(kSm64S, xpow64(8ull * 16ull * kSmallLanes));
+    for (uint32_t dl = 0; dl < 8; ++dl) nibbles(kSm64A + dl * kNib64, xpow64(64ull + 128ull * dl));
+    for (uint32_t dh = 1; dh < 8; ++dh) nibbles(kSm64B + (dh - 1) * kNib64, xpow64(1024ull * dh));
+    for (uint32_t w = 0; w < 4 * kSmallWg; ++w) {
+        const uint64_t k = xpow64(8192ull * (4 * kSmallWg - 1 - w));
+        for (int i = 0; i < 64; ++i) img[kSm64Wave / 8 + w * 64 + i] = mulmod64(1ull << i, k);
+    }
+    for (uint32_t k = 0; k < 32; ++k) {
+        const uint64_t kk = xpow64_inv(8ull * k);
+        for (int i = 0; i < 64; ++i) img[kSm64Tail / 8 + k * 64 + i] = mulmod64(1ull << i, kk);
+    }
+    return img;
+}
+
+std::vector<uint64_t*> g_img64;
+
+int small64_image(int dev, const uint64_t** out) {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    if ((int)g_img64.size() <= dev) g_img64.resize(dev + 1, nullptr);
+    if (!g_img64[dev]) {
+        static const std::vector<uint64_t> host = small64_image_host();
+        void* d = nullptr;
+        hipStream_t s = nullptr;
+        hipError_t e = hipMalloc(&d, kSm64Image);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMemcpyAsync(d, host.data(), kSm64Image, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (s) (void)hipStreamDestroy(s);
+        if (e != hipSuccess) {
+            if (d) (void)hipFree(d);
+            return hip_fail(e, "CRC-64 small-buffer table image");
+        }
+        g_img64[dev] = static_cast<uint64_t*>(d);
+    }
+    *out = g_img64[dev];
+    return 0;
+}
+
+// The CRC-64 small kernel's geometry (as small_args; the grid covers the
+// init's 8 bytes).
+bool small64_args(const void* p, uint64_t n, uint64_t seed, Small64Args* a, uint32_t* grid) {
+    const uintptr_t d = reinterpret_cast<uintptr_t>(p);
+    const uint64_t s0 = d & 15u, eoff = s0 + n;
+    const uint64_t cover = eoff > s0 + 8 ? eoff : s0 + 8;
+    const uint64_t nb = (cover + 15) >> 4;
+    if (nb > kSmallBlocks) return false;
+    a->a0 = reinterpret_cast<const uint8_t*>(d - s0);
+    a->nb = (uint32_t)nb;
+    a->s0 = (uint32_t)s0;
+    a->eoff = (uint32_t)eoff;
+    a->k = (uint32_t)(16 * nb - eoff);
+    a->init = ~seed;
+    *grid = nb > kSmallLanes ? kSmallWg : (uint32_t)((nb + 255) / 256);
+    a->wg0 = kSmallWg - *grid;
+    return true;
+}
+
 // The small kernel's geometry for [p, p + n), or false when the block span
 // exceeds kSmallBlocks (the long kernel's case). *grid = the workgroups that
 // hold data (the last ones of the layout).
@@ -1463,6 +1530,19 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
+    Small64Args sa{};
+    uint32_t sgrid = 0;
+    if (small64_args(d_data, nbytes, seed, &sa, &sgrid)) {  // <= 256 KiB: the latency path
+        if (int rc = small64_image(dev, &sa.image)) return rc;
+        sa.out = d_out;
+        return long_launch(st, sgrid, "crc64_small_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
+            sa.acc = static_cast<uint64_t*>(state);
+            sa.tbase = base;
+            sa.treset = reset;
+            hipLaunchKernelGGL(crc64_small_kernel, dim3(sgrid), dim3(256), 0, st, sa);
+            return hipGetLastError();
+        });
+    }
     const LongPlan lp = long_plan(d_data, nbytes, cus, true);
     const LongPowers& pw = long_powers(lp, true);
     Long64Args a{};
@@ -1784,7 +1864,7 @@ uint32_t host_crc_of_device(const uint8_t* p, size_t n, uint32_t crc) {
 // streams (created on demand and kept), never on the null stream: a routed
 // call does not serialise against the process's other blocking streams, and
 // routed calls from many threads each get a stream of their own (VERDICT r3
-// next #3). Each pooled stream carries 256 bytes of pinned, device-mapped
+// next #3). Each pooled stream carries 512 bytes of pinned, device-mapped
 // host memory that a kernel writes its result into: the caller waits for
 // the stream and reads the word(s), no D2H copy. A small buffer's CRC comes
 // back as one word per workgroup of crc32c_small_kernel, XORed here: no
@@ -1813,8 +1893,8 @@ int routed_lease(int dev, RoutedStream** out) {
     hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
     // coherent: the small kernel's system-scope tag stores reach the host directly
     if (e == hipSuccess)
-        e = hipHostMalloc(&r->h, 256, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
-    if (e == hipSuccess) memset(r->h, 0, 256);
+        e = hipHostMalloc(&r->h, 512, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
+    if (e == hipSuccess) memset(r->h, 0, 512);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&r->d, r->h, 0);
     if (e != hipSuccess) {
         if (r->h) (void)hipHostFree(r->h);
@@ -1876,6 +1956,39 @@ int with_scratch(int dev, uint64_t bytes, void* h_out, uint64_t out_bytes, F f) 
 // stream that finished without all tags falls back to hipStreamSynchronize's
 // verdict. The stream's later work is ordered behind this kernel, so the
 // area is not rewritten before the kernel has ended.
+// Spin until the `per` tagged words of each of `n` workgroups (slots w[per
+// b + h]) carry `tag`; x[h] = XOR of their low words. Bounded: every 64 µs
+// the stream is queried, and a stream that finished (or failed) without all
+// tags returns its error.
+int spin_tagged(RoutedStream* r, uint32_t tag, uint32_t n, uint32_t* x, uint32_t per, const char* what) {
+    const volatile uint64_t* w = static_cast<const volatile uint64_t*>(r->h);
+    const uint32_t total = n * per;
+    auto t0 = std::chrono::steady_clock::now();
+    uint32_t done = 0;
+    for (;;) {
+        while (done < total && (uint32_t)(w[done] >> 32) == tag) {
+            x[done % per] ^= (uint32_t)w[done];
+            ++done;
+        }
+        if (done == total) return 0;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(64)) {
+            const hipError_t q = hipStreamQuery(r->st);
+            if (q == hipErrorNotReady) {
+                t0 = std::chrono::steady_clock::now();
+                continue;
+            }
+            // finished (or failed) without every tag seen yet: a last look, then its verdict
+            while (done < total && (uint32_t)(w[done] >> 32) == tag) {
+                x[done % per] ^= (uint32_t)w[done];
+                ++done;
+            }
+            if (done == total) return 0;
+            const hipError_t e = hipStreamSynchronize(r->st);
+            return hip_fail(e != hipSuccess ? e : hipErrorUnknown, what);
+        }
+    }
+}
+
 int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_out) {
     RoutedStream* r = nullptr;
     if (int rc = routed_lease(dev, &r)) return rc;
@@ -1893,29 +2006,38 @@ int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_ou
         if (e != hipSuccess) rc = hip_fail(e, "crc32c_small_kernel launch");
     }
     if (!rc) {
-        const volatile uint64_t* w = static_cast<const volatile uint64_t*>(r->h);
-        auto t0 = std::chrono::steady_clock::now();
-        uint32_t done = 0, x = 0;
-        for (;;) {
-            while (done < sgrid && (uint32_t)(w[done] >> 32) == sa.tag) x ^= (uint32_t)w[done++];
-            if (done == sgrid) break;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(64)) {
-                const hipError_t q = hipStreamQuery(r->st);
-                if (q == hipErrorNotReady) {
-                    t0 = std::chrono::steady_clock::now();
-                    continue;
-                }
-                // finished (or failed) without every tag seen yet: a last look, then its verdict
-                while (done < sgrid && (uint32_t)(w[done] >> 32) == sa.tag) x ^= (uint32_t)w[done++];
-                if (done == sgrid) break;
-                const hipError_t e = hipStreamSynchronize(r->st);
-                rc = hip_fail(e != hipSuccess ? e : hipErrorUnknown, "crc32c_small_kernel (routed)");
-                break;
-            }
-        }
+        uint32_t x = 0;
+        rc = spin_tagged(r, sa.tag, sgrid, &x, 1, "crc32c_small_kernel (routed)");
         if (!rc) *crc_out = x;
     } else {
         (void)hipStreamSynchronize(r->st);  // nothing left running on a returned stream
+    }
+    routed_return(r);
+    return rc;
+}
+
+// CRC-64 small buffers on a routed stream: the workgroups' raw values come
+// back as two tagged words each; the host XORs and inverts (crc.cpp:119-122).
+int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* crc_out) {
+    RoutedStream* r = nullptr;
+    if (int rc = routed_lease(dev, &r)) return rc;
+    Small64Args sa = sa0;
+    int rc = small64_image(dev, &sa.image);
+    if (!rc) {
+        r->tag = r->tag == 0xffffffffu ? 1u : r->tag + 1u;
+        sa.tag = r->tag;
+        sa.slots = static_cast<uint64_t*>(r->d);
+        memset(r->h, 0, 16ull * sgrid);  // as routed_small
+        hipLaunchKernelGGL(crc64_small_kernel, dim3(sgrid), dim3(256), 0, r->st, sa);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) rc = hip_fail(e, "crc64_small_kernel launch");
+    }
+    if (!rc) {
+        uint32_t x[2] = {0, 0};
+        rc = spin_tagged(r, sa.tag, sgrid, x, 2, "crc64_small_kernel (routed)");
+        if (!rc) *crc_out = ~(((uint64_t)x[1] << 32) | x[0]);
+    } else {
+        (void)hipStreamSynchronize(r->st);
     }
     routed_return(r);
     return rc;
@@ -2010,9 +2132,16 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     if (dev < 0) return host_engine(&g_host_crc64)(p, n, crc);
     DeviceScope scope(dev);
     uint64_t r = 0;
-    int rc = routed_call(dev, &r, 8, [&](void* d, hipStream_t st) {
-        return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), st);
-    });
+    Small64Args sa{};
+    uint32_t sgrid = 0;
+    int rc;
+    if (small64_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, folded here
+        rc = routed_small64(dev, sa, sgrid, &r);
+    } else {
+        rc = routed_call(dev, &r, 8, [&](void* d, hipStream_t st) {
+            return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), st);
+        });
+    }
     if (!rc) return r;
     routed_failure("crc64ecma_extend", rc);
     const auto eng = host_engine(&g_host_crc64);

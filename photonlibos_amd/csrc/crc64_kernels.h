@@ -890,4 +890,133 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
     crc64_long_run<G>(a, kc, lds, red, nullptr);
 }
 
+// photon_crc64ecma_extend_device for buffers whose 16-byte block span is at
+// most kSmallBlocks (256 KiB): crc32c_kernels.h crc32c_small_kernel's layout
+// (up to 32 workgroups x 256 threads = V = 8192 virtual lanes walking rows of
+// V blocks anchored at the end, every factor a constant of the layout, tables
+// copied from a device image) at 64 bits: a block's lagged value is lo * x^64
+// ^ hi (ONE nibble-sliced multiply), Q <- Q * x^(128 V) ^ v per row, then
+// Q * x^(64 + 128 dl), x^(1024 dh) (d = 63 - lane), the wave's
+// x^(8192 (127 - wave)) and x^(-8k) lane-parallel (basis words from the
+// image), long_reduce over the workgroups. The inverted init is XORed into
+// the data's first 8 bytes (the grid covers them even for n < 8: with the
+// x^(-8k) undo it contributes init * x^(8n), crc.cpp:119-122). Nibble tables:
+// 16 positions x 16 values x 8 B per multiplier (2 KiB); in lookup t all 64
+// lanes read position t's 16 entries: 128 contiguous bytes, no conflicts.
+// The reference times crc64ecma on 128 KiB at buf+1 (test_checksum.cpp:204-216).
+constexpr uint32_t kNib64 = 2048;
+constexpr uint32_t kSm64D = 0, kSm64S = kNib64, kSm64A = 2 * kNib64, kSm64B = kSm64A + 8 * kNib64;
+constexpr uint32_t kSm64Lds = kSm64B + 7 * kNib64;                      // 34 KiB of tables in LDS
+constexpr uint32_t kSm64Wave = kSm64Lds;                                // 128 x 64 words: x^(8192 (127 - wave))
+constexpr uint32_t kSm64Tail = kSm64Wave + 4u * kSmallWg * 64u * 8u;    // 32 x 64 words: x^(-8 k), k < 32
+constexpr uint32_t kSm64Image = kSm64Tail + 32u * 64u * 8u;
+
+struct Small64Args {
+    const uint8_t* a0;       // aligned start (data start & ~15)
+    const uint64_t* image;
+    uint64_t* out;           // the CRC (device), through long_reduce when grid > 1
+    uint64_t* acc;           // long_reduce state
+    uint64_t tbase;
+    uint32_t treset;
+    uint32_t nb;             // blocks of the grid, <= kSmallBlocks + 1
+    uint32_t s0;             // data start - a0
+    uint32_t eoff;           // data end - a0
+    uint32_t k;              // grid end - data end: the register is multiplied by x^(-8k)
+    uint32_t wg0;            // workgroup index of blockIdx.x == 0
+    uint64_t init;           // ~seed (the register's start, crc.cpp:119-122)
+    uint64_t* slots;         // routed calls: workgroup b's raw value as {tag, low word}, {tag, high word}
+    uint32_t tag;            //   at slots[2b], slots[2b + 1] (system scope; the host spins on the tags)
+};
+
+// p * K through the [position][value] nibble tables of K at byte offset `off`.
+__device__ __forceinline__ uint64_t nib_mul64_pos(const uint32_t* lds, uint32_t off, uint64_t p) {
+    uint2 v[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v[t] = lds_u2(lds, off + (uint32_t)(t * 16 + (int)((p >> (4 * t)) & 15u)) * 8u);
+    uint32_t lo = xor3(xor3(v[0].x, v[1].x, v[2].x), xor3(v[3].x, v[4].x, v[5].x), xor3(v[6].x, v[7].x, v[8].x));
+    uint32_t hi = xor3(xor3(v[0].y, v[1].y, v[2].y), xor3(v[3].y, v[4].y, v[5].y), xor3(v[6].y, v[7].y, v[8].y));
+    lo = xor3(lo, xor3(v[9].x, v[10].x, v[11].x), xor3(v[12].x, v[13].x, v[14].x)) ^ v[15].x;
+    hi = xor3(hi, xor3(v[9].y, v[10].y, v[11].y), xor3(v[12].y, v[13].y, v[14].y)) ^ v[15].y;
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Bytes of the 8-byte word at `off` (from a0) at or past `eoff` zeroed.
+__device__ __forceinline__ uint64_t tail_word64(uint64_t w, int off, int eoff) {
+    const int m = eoff - off;
+    return m >= 8 ? w : m <= 0 ? 0ull : w & ((1ull << (8 * m)) - 1ull);
+}
+
+__global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSm64Lds / 4];
+    __shared__ uint64_t red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t wg = a.wg0 + blockIdx.x;
+    const uint32_t vt = wg * 256u + tid;
+    // 1. Table copy first, then the payload rows, then the basis words.
+    constexpr uint32_t kVec = kSm64Lds / 16;  // 2176 16-byte pieces: up to 9 per thread
+    constexpr uint32_t kPer = (kVec + 255) / 256;
+    u32x4 tv[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t j = i * 256u + tid;
+        tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
+    }
+    const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
+    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
+    uint4 w[kSmallRows];
+#pragma unroll
+    for (int r = 0; r < (int)kSmallRows; ++r) {
+        const int b = first + r * (int)kSmallLanes;
+        w[r] = ((uint32_t)r < rows && b >= 0) ? load16(a.a0 + 16 * (uint32_t)b) : make_uint4(0, 0, 0, 0);
+    }
+    const uint64_t bw_wave = a.image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
+    const uint64_t bw_tail = a.image[kSm64Tail / 8 + a.k * 64u + lane];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t j = i * 256u + tid;
+        if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
+    }
+    lds_barrier();
+    // 2. The column: lagged blocks and the row shift.
+    uint64_t c[kSmallRows];
+#pragma unroll
+    for (int r = 0; r < (int)kSmallRows; ++r) {
+        const int b = first + r * (int)kSmallLanes;
+        uint64_t lo = ((uint64_t)w[r].y << 32) | w[r].x, hi = ((uint64_t)w[r].w << 32) | w[r].z;
+        if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + init
+            const int off = b * 16;
+            lo = head_word64(tail_word64(lo, off, (int)a.eoff), off, (int)a.s0, a.init);
+            hi = head_word64(tail_word64(hi, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.init);
+            if (b < 0 || (uint32_t)r >= rows) lo = hi = 0ull;
+        }
+        c[r] = nib_mul64_pos(lds, kSm64D, lo) ^ hi;
+    }
+    uint64_t q = c[0];
+#pragma unroll
+    for (int r = 1; r < (int)kSmallRows; ++r)
+        if ((uint32_t)r < rows) q = nib_mul64_pos(lds, kSm64S, q) ^ c[r];
+    // 3. Q -> P and the shift to the end of the wave, the wave's and the tail's factors.
+    const uint32_t d = 63u - lane, dh = d >> 3;
+    const uint64_t x = nib_mul64_pos(lds, kSm64A + (d & 7u) * kNib64, q);
+    const uint64_t y = nib_mul64_pos(lds, kSm64B + (dh ? dh - 1u : 0u) * kNib64, x);
+    uint64_t v = xor_lanes64(dh ? y : x, 64);
+    v = mul_wave64(v, bw_wave, lane);
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t u = red[0] ^ red[1] ^ red[2] ^ red[3];
+        u = mul_wave64(u, bw_tail, lane);
+        if (a.slots) {  // routed: the host XORs the workgroups' raw values and inverts
+            if (lane == 0) {
+                __hip_atomic_store(a.slots + 2 * blockIdx.x, (uint64_t)a.tag << 32 | (uint32_t)u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(a.slots + 2 * blockIdx.x + 1, (uint64_t)a.tag << 32 | (uint32_t)(u >> 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122
+        }
+    }
+}
+
 }  // namespace pcrc

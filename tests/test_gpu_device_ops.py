@@ -219,10 +219,11 @@ def test_device_dispatch_dropin(torch_dev, oracle):
 
 
 def test_device_dispatch_small_buffers_threads(torch_dev, oracle):
-    """Routed crc32c_extend on small device buffers (the small kernel, its
-    per-workgroup words collected by spinning on tagged slots in the routed
-    stream's pinned area) from 8 threads at once, 1 B .. 256 KiB at odd
-    offsets and seeds, back to back: every result equals the oracle's."""
+    """Routed crc32c_extend / crc64ecma_extend on small device buffers (the
+    small kernels, their per-workgroup words collected by spinning on tagged
+    slots in the routed stream's pinned area) from 8 threads at once, 1 B ..
+    256 KiB at odd offsets and seeds, back to back: every result equals the
+    oracle's."""
     import threading
     torch = torch_dev
     n = 1 << 20
@@ -232,19 +233,26 @@ def test_device_dispatch_small_buffers_threads(torch_dev, oracle):
     host = dbuf.cpu().numpy()
     rng = random.Random(0x5EED0411)
     cases = []
-    for _ in range(8 * 60):
-        ln = rng.choice([1, 15, 16, 17, 4095, 4096, 65537, 131072, 200000, 262144])
+    for i in range(8 * 60):
+        ln = rng.choice([1, 7, 15, 16, 17, 4095, 4096, 65537, 131072, 200000, 262144])
         off = rng.randrange(0, n - ln)
-        seed = rng.getrandbits(32)
-        cases.append((off, ln, seed, oracle.crc32c(host[off:off + ln], seed)))
+        if i % 2:  # CRC-64/ECMA: crc64_small_kernel, two tagged words per workgroup
+            seed = rng.getrandbits(64)
+            cases.append((64, off, ln, seed, oracle.crc64ecma(host[off:off + ln], seed)))
+        else:
+            seed = rng.getrandbits(32)
+            cases.append((32, off, ln, seed, oracle.crc32c(host[off:off + ln], seed)))
     bad = []
     ck.set_device_dispatch(True)
 
     def worker(k):
-        for off, ln, seed, want in cases[k::8]:
-            got = ck.crc32c_extend_at(dbuf.data_ptr() + off, ln, seed)
+        for width, off, ln, seed, want in cases[k::8]:
+            if width == 64:
+                got = ck.crc64ecma_extend_at(dbuf.data_ptr() + off, ln, seed)
+            else:
+                got = ck.crc32c_extend_at(dbuf.data_ptr() + off, ln, seed)
             if got != want:
-                bad.append((k, off, ln, seed, got, want))
+                bad.append((k, width, off, ln, seed, got, want))
 
     threads = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
     for t in threads:

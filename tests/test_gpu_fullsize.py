@@ -273,6 +273,39 @@ def test_extend_device_small_path_edges(torch_dev, oracle):
             assert int(got[k]) == oracle.crc32c(host[off:off + n], seed), (off - base, n, seed)
 
 
+def test_extend64_device_small_path_edges(torch_dev, oracle):
+    """crc64_small_kernel (CRC-64/ECMA, block span <= 256 KiB): every length
+    0..139 at every start offset 0..15 with a 64-bit seed (inits over fewer
+    than 8 data bytes, heads and tails in one block), random lengths, and the
+    span limit at offsets 0 and 15, all against the oracle."""
+    torch = torch_dev
+    n_max = (256 << 10) + 64
+    d = torch.empty(n_max + 64, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0D64)
+    host = d.cpu().numpy()
+    base = (-d.data_ptr()) % 16
+    out = torch.zeros(140 * 16, dtype=torch.int64, device="cuda")
+    cases = []
+    for n in range(140):
+        for off in range(16):
+            cases.append((base + off, n, (n * 0x9E3779B97F4A7C15 + off) & 0xFFFFFFFFFFFFFFFF))
+    rng = np.random.default_rng(0x5EED0D65)
+    for _ in range(150):
+        n = int(rng.integers(140, 256 << 10))
+        cases.append((base + int(rng.integers(0, 16)), n, int(rng.integers(0, 1 << 63)) * 2 + 1))
+    span = 256 << 10
+    cases += [(base, span, 1), (base + 15, span - 15, 2), (base + 15, span - 14, 3), (base, span + 1, 4),
+              (base + 1, 128 << 10, 5), (base + 12, span - 16, 6)]
+    for k0 in range(0, len(cases), out.numel()):
+        part = cases[k0:k0 + out.numel()]
+        for k, (off, n, seed) in enumerate(part):
+            ck.extend64_device(d.data_ptr() + off, n, out[k:k + 1], seed=seed)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64)
+        for k, (off, n, seed) in enumerate(part):
+            assert int(got[k]) == oracle.crc64ecma(host[off:off + n], seed), (off - base, n, hex(seed))
+
+
 def test_extend_device_thousand_back_to_back_launches(torch_dev, oracle):
     """the fence-free cross-workgroup reduce (long_reduce)
     reused by 1,000 back-to-back full-grid launches on ONE stream (one state:
