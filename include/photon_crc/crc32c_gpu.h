@@ -249,6 +249,11 @@ int photon_crc64ecma_combine_batch(const uint64_t* d_crc1, const uint64_t* d_crc
 int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_msg_start, uint64_t nmsg,
                                  uint64_t nseg, uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_seg_out,
                                  uint64_t* d_out, void* stream);
+/* photon_crc32c_extend_device for CRC-64/ECMA (crc64ecma_extend, crc.cpp:
+ * 119-122): the same latency path for spans up to 256 KiB (a small kernel of
+ * up to 32 workgroups), one launch over the chip above, the same per-stream
+ * state and capture rule (-ENOTSUP on a capturing stream for more than one
+ * workgroup; spans up to 4 KiB are capturable). */
 int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,
                                    void* stream);
 /* photon_crc32c_extend_spans for CRC-64/ECMA (crc64ecma_combine's identity:
