@@ -375,6 +375,25 @@ def test_extend_device_graph_capture(torch_dev, oracle):
     ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[2:3])
     torch.cuda.synchronize()
     assert int(_u32(out)[2]) == oracle.crc32c(d.cpu().numpy()[3:3 + (1 << 20) - 64], 9)
+    # CRC-64 (crc64_small_kernel): the same rule
+    out64 = torch.zeros(2, dtype=torch.int64, device="cuda")
+    ck.extend64_device(d.data_ptr() + 5, 4000, out64[0:1], seed=11)  # its table image exists before capture
+    torch.cuda.synchronize()
+    g64 = torch.cuda.CUDAGraph()
+    refused = []
+    with torch.cuda.graph(g64):
+        st = torch.cuda.current_stream()
+        ck.extend64_device(d.data_ptr() + 5, 4000, out64[0:1], seed=11, stream=st)
+        try:
+            ck.extend64_device(d.data_ptr() + 5, 64 << 10, out64[1:2], seed=11, stream=st)
+        except ck.CrcError as e:
+            refused.append(e.code)
+    assert refused == [-95]
+    ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0C03)
+    torch.cuda.synchronize()
+    g64.replay()
+    torch.cuda.synchronize()
+    assert int(out64.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(d.cpu().numpy()[5:5 + 4000], 11)
 
 
 @pytest.mark.parametrize("shape", [(0, 0), (64, 1), (64, 2), (32, 1), (32, 2), (32, 3)])
