@@ -957,6 +957,9 @@ bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t
 
 }  // namespace
 
+int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st, int cus,
+                       uint32_t tag);
+
 // For the other translation units of the library (internal.h).
 int report_error(int code, const char* what) { return fail(code, what); }
 int report_hip_error(hipError_t e, const char* what) { return hip_fail(e, what); }
@@ -1646,10 +1649,21 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
             return hipGetLastError();
         });
     }
+    return pcrc::extend_device_long(d_data, nbytes, seed, d_out, st, cus, 0);
+}
+
+}  // extern "C"
+
+namespace pcrc {
+// The long kernel for photon_crc32c_extend_device (and, with a tag, for a
+// routed call whose result word lands tagged in pinned memory).
+int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st, int cus,
+                       uint32_t tag) {
     const LongPlan lp = long_plan(d_data, nbytes, cus, false);
     const LongPowers& pw = long_powers(lp, false);
     LongArgs a{};
     long_args(&a, lp, pw, d_data, seed, d_out);
+    a.out_tag = tag;
     return long_launch(st, lp.grid, "crc32c_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint32_t*>(state);
         a.tbase = base;
@@ -1661,8 +1675,7 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
         return hipGetLastError();
     });
 }
-
-}  // extern "C"
+}  // namespace pcrc
 
 namespace pcrc {
 namespace {
@@ -2016,6 +2029,31 @@ int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_ou
     return rc;
 }
 
+// A long buffer on a routed stream: the last workgroup's tagged result word
+// (long_reduce) is spun on like the small kernels' words.
+int routed_long(int dev, const uint8_t* p, uint64_t n, uint32_t crc, uint32_t* crc_out) {
+    RoutedStream* r = nullptr;
+    if (int rc = routed_lease(dev, &r)) return rc;
+    int cus = 0;
+    int rc = current_device(&cus) < 0 ? -ENODEV : 0;
+    uint32_t tag = 0;
+    if (!rc) {
+        r->tag = r->tag == 0xffffffffu ? 1u : r->tag + 1u;
+        tag = r->tag;
+        memset(r->h, 0, 8);
+        rc = extend_device_long(p, n, crc, static_cast<uint32_t*>(r->d), r->st, cus, tag);
+    }
+    if (!rc) {
+        uint32_t x = 0;
+        rc = spin_tagged(r, tag, 1, &x, 1, "crc32c_long_kernel (routed)");
+        if (!rc) *crc_out = x;
+    } else {
+        (void)hipStreamSynchronize(r->st);
+    }
+    routed_return(r);
+    return rc;
+}
+
 // CRC-64 small buffers on a routed stream: the workgroups' raw values come
 // back as two tagged words each; the host XORs and inverts (crc.cpp:119-122).
 int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* crc_out) {
@@ -2054,9 +2092,7 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     if (small_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, XORed here
         rc = routed_small(dev, sa, sgrid, &r);
     } else {
-        rc = routed_call(dev, &r, 4, [&](void* d, hipStream_t st) {
-            return photon_crc32c_extend_device(p, n, crc, static_cast<uint32_t*>(d), st);
-        });
+        rc = routed_long(dev, p, n, crc, &r);
     }
     if (!rc) return r;
     routed_failure("crc32c_extend", rc);

@@ -1450,6 +1450,7 @@ struct LongArgs {
     uint32_t xb[32];    // basis words of X (GPW = 2)
     uint32_t zt[16];    // Z^(15 - w)
     uint32_t ft[kLongMaxFt];  // J Y^(grid - 1 - b)
+    uint32_t out_tag;   // routed calls: nonzero = *out is a tagged 8-byte word in pinned memory (long_reduce)
 };
 
 // The long kernels' cross-workgroup XOR, called by EVERY thread of wave 0
@@ -1496,10 +1497,24 @@ struct LongArgs {
 #endif
 constexpr uint32_t kLongMaxGrid = 512;
 template <typename T, typename F, bool FENCED = false>
-__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset) {
+__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
+                                            uint32_t tag = 0) {
     const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
+    // tag != 0 (routed CRC-32C calls, out in the routed stream's coherent
+    // pinned area): ONE 8-byte system-scope store {tag, crc}; the host spins
+    // on the tag instead of waiting for the stream
+    auto put = [&](T r) {
+        if constexpr (sizeof(T) == 4) {
+            if (tag) {
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(out), (uint64_t)tag << 32 | (uint32_t)r,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+            }
+        }
+        *out = r;
+    };
     if (grid == 1) {
-        if (lane == 0) *out = fin(v);
+        if (lane == 0) put(fin(v));
         return;
     }
     // The same layout for both widths: a 64-bit ticket in bytes 0-7, slots
@@ -1537,7 +1552,7 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64
     else
         x = group_xor<64>(x);
     if (lane == 0) {
-        *out = fin(x);
+        put(fin(x));
         if (reset) __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -1626,7 +1641,7 @@ __device__ __forceinline__ void long_finish(const LongArgs& a, uint32_t acc, uin
             long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase,
                                                                 a.treset);
         } else {
-            long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
+            long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset, a.out_tag);
         }
     }
 }
