@@ -959,6 +959,8 @@ bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t
 
 int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st, int cus,
                        uint32_t tag);
+int extend64_device_long(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
+                         int cus, uint32_t tag);
 
 // For the other translation units of the library (internal.h).
 int report_error(int code, const char* what) { return fail(code, what); }
@@ -1546,10 +1548,19 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
             return hipGetLastError();
         });
     }
+    return pcrc::extend64_device_long(d_data, nbytes, seed, d_out, st, cus, 0);
+}
+}  // extern "C"
+
+namespace pcrc {
+// The long kernel for photon_crc64ecma_extend_device (tag: as extend_device_long).
+int extend64_device_long(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
+                         int cus, uint32_t tag) {
     const LongPlan lp = long_plan(d_data, nbytes, cus, true);
     const LongPowers& pw = long_powers(lp, true);
     Long64Args a{};
     long_args64(&a, lp, pw, d_data, seed, d_out);
+    a.out_tag = tag;
     return long_launch(st, lp.grid, "crc64_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint64_t*>(state);
         a.tbase = base;
@@ -1561,6 +1572,9 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
         return hipGetLastError();
     });
 }
+}  // namespace pcrc
+
+extern "C" {
 
 int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, const uint32_t* d_len2,
                                 uint64_t count, uint32_t* d_out, void* stream) {
@@ -2054,6 +2068,30 @@ int routed_long(int dev, const uint8_t* p, uint64_t n, uint32_t crc, uint32_t* c
     return rc;
 }
 
+// routed_long for CRC-64: the result as two tagged words.
+int routed_long64(int dev, const uint8_t* p, uint64_t n, uint64_t crc, uint64_t* crc_out) {
+    RoutedStream* r = nullptr;
+    if (int rc = routed_lease(dev, &r)) return rc;
+    int cus = 0;
+    int rc = current_device(&cus) < 0 ? -ENODEV : 0;
+    uint32_t tag = 0;
+    if (!rc) {
+        r->tag = r->tag == 0xffffffffu ? 1u : r->tag + 1u;
+        tag = r->tag;
+        memset(r->h, 0, 16);
+        rc = extend64_device_long(p, n, crc, static_cast<uint64_t*>(r->d), r->st, cus, tag);
+    }
+    if (!rc) {
+        uint32_t x[2] = {0, 0};
+        rc = spin_tagged(r, tag, 1, x, 2, "crc64_long_kernel (routed)");
+        if (!rc) *crc_out = ((uint64_t)x[1] << 32) | x[0];  // long_reduce already inverted it
+    } else {
+        (void)hipStreamSynchronize(r->st);
+    }
+    routed_return(r);
+    return rc;
+}
+
 // CRC-64 small buffers on a routed stream: the workgroups' raw values come
 // back as two tagged words each; the host XORs and inverts (crc.cpp:119-122).
 int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* crc_out) {
@@ -2174,9 +2212,7 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     if (small64_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, folded here
         rc = routed_small64(dev, sa, sgrid, &r);
     } else {
-        rc = routed_call(dev, &r, 8, [&](void* d, hipStream_t st) {
-            return photon_crc64ecma_extend_device(p, n, crc, static_cast<uint64_t*>(d), st);
-        });
+        rc = routed_long64(dev, p, n, crc, &r);
     }
     if (!rc) return r;
     routed_failure("crc64ecma_extend", rc);

@@ -1500,16 +1500,17 @@ template <typename T, typename F, bool FENCED = false>
 __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
                                             uint32_t tag = 0) {
     const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
-    // tag != 0 (routed CRC-32C calls, out in the routed stream's coherent
-    // pinned area): ONE 8-byte system-scope store {tag, crc}; the host spins
-    // on the tag instead of waiting for the stream
+    // tag != 0 (routed calls, out in the routed stream's coherent pinned
+    // area): 8-byte system-scope stores {tag, 32-bit word} (one, or two for
+    // CRC-64); the host spins on the tags instead of waiting for the stream
     auto put = [&](T r) {
-        if constexpr (sizeof(T) == 4) {
-            if (tag) {
-                __hip_atomic_store(reinterpret_cast<uint64_t*>(out), (uint64_t)tag << 32 | (uint32_t)r,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                return;
-            }
+        if (tag) {  // one tagged word per 32 bits, low word first
+#pragma unroll
+            for (uint32_t h = 0; h < sizeof(T) / 4; ++h)
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(out) + h,
+                                   (uint64_t)tag << 32 | (uint32_t)((uint64_t)r >> (32 * h)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
         }
         *out = r;
     };

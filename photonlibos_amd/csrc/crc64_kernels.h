@@ -761,6 +761,7 @@ struct Long64Args {
     uint64_t xsb[64];   // basis words of X^S: (1 << i) * X^S (host-computed, long_powers)
     uint64_t zt[16];    // Z^(15 - w)
     uint64_t ft[kLongMaxFt];  // J Y^(grid - 1 - b)
+    uint32_t out_tag;   // routed calls: nonzero = the result as two tagged words in pinned memory (long_reduce)
 };
 
 __device__ __forceinline__ uint64_t mulx64(uint64_t v) { return (v >> 1) ^ ((0ull - (v & 1ull)) & kPoly64); }
@@ -875,7 +876,8 @@ __device__ __forceinline__ void crc64_long_run(const Long64Args& a, const LaneCo
             e ^= red[kWaves + w];
         }
         u = mul_wave64(u, bw_f, lane) ^ e;  // * J Y^(grid - 1 - b), then the last chunk
-        long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122: inverted out
+        long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset,
+                    a.out_tag);  // crc.cpp:119-122: inverted out
     }
     if constexpr (STAMP) {
         ts[4] = __builtin_amdgcn_s_memrealtime();

@@ -3,7 +3,7 @@
 test_checksum.cpp:204-216: 128 KiB and 1 GiB through crc64ecma_hw):
 photon_crc64ecma_extend_device kernel time (HIP events, median of 200 / 50
 launches) and enqueue + wait, and the routed crc64ecma_extend on a device
-pointer. Bench-only probe; prints one JSON line."""
+pointer (128 KiB and 1 GiB). Bench-only probe; prints one JSON line."""
 import json
 import os
 import sys
@@ -45,8 +45,16 @@ for _ in range(50):
     t0 = time.perf_counter()
     r = ck.crc64ecma_extend_at(d.data_ptr() + 1, 128 << 10, 7)
     routed.append(time.perf_counter() - t0)
+routed_1g = []
+for _ in range(10):  # the long kernel, result as two tagged words
+    t0 = time.perf_counter()
+    r1 = ck.crc64ecma_extend_at(d.data_ptr() + 1, n1, 7)
+    routed_1g.append(time.perf_counter() - t0)
 ck.set_device_dispatch(False)
 want = ck.crc64ecma_extend(d[1:1 + (128 << 10)].cpu().numpy().tobytes(), 7)
+ck.extend64_device(d.data_ptr() + 1, n1, out[:1], seed=7, stream=st)
+st.synchronize()
 res["routed_128KiB_us_median"] = round(float(np.median(routed)) * 1e6, 1)
-res["self_check"] = r == want
+res["routed_1GiB_us_median"] = round(float(np.median(routed_1g)) * 1e6, 1)
+res["self_check"] = r == want and r1 == int(out[0].item()) & 0xFFFFFFFFFFFFFFFF
 print(json.dumps(res))

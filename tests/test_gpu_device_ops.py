@@ -219,11 +219,12 @@ def test_device_dispatch_dropin(torch_dev, oracle):
 
 
 def test_device_dispatch_small_buffers_threads(torch_dev, oracle):
-    """Routed crc32c_extend / crc64ecma_extend on small device buffers (the
-    small kernels, their per-workgroup words collected by spinning on tagged
-    slots in the routed stream's pinned area) from 8 threads at once, 1 B ..
-    256 KiB at odd offsets and seeds, back to back: every result equals the
-    oracle's."""
+    """Routed crc32c_extend / crc64ecma_extend on device buffers from 8
+    threads at once, 1 B .. 256 KiB (the small kernels, their per-workgroup
+    words collected by spinning on tagged slots in the routed stream's pinned
+    area) and 300 KB / 700 KB (the long kernels, the last workgroup's tagged
+    result words), at odd offsets and seeds, back to back: every result
+    equals the oracle's."""
     import threading
     torch = torch_dev
     n = 1 << 20
@@ -234,7 +235,7 @@ def test_device_dispatch_small_buffers_threads(torch_dev, oracle):
     rng = random.Random(0x5EED0411)
     cases = []
     for i in range(8 * 60):
-        ln = rng.choice([1, 7, 15, 16, 17, 4095, 4096, 65537, 131072, 200000, 262144])
+        ln = rng.choice([1, 7, 15, 16, 17, 4095, 4096, 65537, 131072, 200000, 262144, 300001, 700000])
         off = rng.randrange(0, n - ln)
         if i % 2:  # CRC-64/ECMA: crc64_small_kernel, two tagged words per workgroup
             seed = rng.getrandbits(64)
