@@ -542,10 +542,14 @@ __device__ __forceinline__ uint2 lag_run64(const uint32_t* lds, const uint4 (&w)
 // ABL != 0 only in bench-only ablation builds (probes.hip); results are then
 // NOT CRCs: 1 = no S (row-shift) lookups, 2 = one D step on lo ^ hi per
 // block (no data chain), 4 = no table lookups at all.
+// V = B = 1 (one partial per lane, single blocks): the batch kernel's finish
+// (finish tables A_dl / B_dh, finish_xor16 at 16 lanes: 17 lookups per lane)
+// instead of a D step plus log2(G) R64 levels (8 + 16 log2(G) lookups).
 template <int G, int U, int D, int V = 1, int B = 1, int ABL = 0>
 __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[k64LdsBytes / 4];
-    build_tables64(lds, kc);
+    constexpr bool kFin = V == 1 && B == 1 && ABL == 0;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kFin ? k64FLdsBytes : k64LdsBytes) / 4];
+    build_tables64<kFin ? G : 0>(lds, kc);
 
     constexpr uint64_t GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
@@ -629,15 +633,25 @@ __global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args arg
             }
             if (++step == spb) {
                 uint64_t acc = 0;
+                if constexpr (kFin) {  // Q * x^(64 + 128 d), d = G - 1 - gl, XOR over the group
+                    const uint32_t d = G - 1 - gl;
+                    if constexpr (G == 16 && PCRC64_FIN16) {
+                        acc = finish_xor16(pc[0], d, lds, gl, lane);
+                    } else {
+                        const uint64_t f = finish64<G>(pc[0], d, lds, lane);
+                        acc = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+                    }
+                } else {
 #pragma unroll
-                for (int j = 0; j < V; ++j)  // Q -> P (dstep), then the lane shift
-                    acc ^= shift64<LOG2VG>(u64of(ABL ? pc[j] : dstep64(lds, pc[j], la)),
-                                           (uint32_t)((G * V - 1 - (j * G + gl)) * B), lds);
+                    for (int j = 0; j < V; ++j)  // Q -> P (dstep), then the lane shift
+                        acc ^= shift64<LOG2VG>(u64of(ABL ? pc[j] : dstep64(lds, pc[j], la)),
+                                               (uint32_t)((G * V - 1 - (j * G + gl)) * B), lds);
 #pragma unroll
-                for (int o = G / 2; o > 0; o >>= 1) {
-                    const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);
-                    const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), o, 64);
-                    acc ^= ((uint64_t)hi32 << 32) | lo32;
+                    for (int o = G / 2; o > 0; o >>= 1) {
+                        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);
+                        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), o, 64);
+                        acc ^= ((uint64_t)hi32 << 32) | lo32;
+                    }
                 }
                 const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
                 if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = ~(acc ^ args.init_shift);

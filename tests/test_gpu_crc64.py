@@ -102,7 +102,7 @@ STREAM64_CASES = [(shape, v) for shape in [(4, 2), (4, 3), (2, 4), (8, 1), (4, 1
 
 
 @pytest.mark.parametrize("shape,v", STREAM64_CASES)
-@pytest.mark.parametrize("g", [8, 32, 64])
+@pytest.mark.parametrize("g", [8, 16, 32, 64])
 def test_streaming_shapes(torch_dev, oracle, shape, g, v):
     # The CRC-64 streaming kernel (uniform batches) in every shape and row
     # interleave, with seed0, per-buffer seeds and no seed; counts that do not
