@@ -27,28 +27,12 @@ int photon_crc_set_lanes_per_buffer(int g);
  * busy CUs at the same HBM rate); 0 = one per CU (default). */
 int photon_crc_set_batch_grid(int workgroups);
 
-/* Streaming-kernel shape for uniform batches (testing / tuning): blocks per
- * lane run B, rows per step U and steps in flight D, one of (1,4,3), (2,2,3),
- * (2,2,4), (1,2,4), (4,1,3), (4,1,4), (1,8,1), (1,6,2), (1,8,2), (1,4,4), (1,4,1),
- * (1,4,2), (1,2,2), (1,2,3); B = 1 uses lagged blocks (16 lookups per 16 B).
- * The streaming kernel is OFF by default (the generic kernel is faster with
- * the current tables); run_blocks = 0 turns it off again. */
-int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight);
-
 /* Batch kernel variant (testing / tuning): -1 (default) = rows per step by
  * lane-group size (2 for 16-lane groups, else 4); 2, 4 or 8 = the generic
- * kernel with that many rows per step; 0 = the fused kernel (four rows per
- * step with the row shifts folded into the tables). */
+ * kernel with that many rows per step. (The fused and streaming kernels of
+ * earlier rounds measured slower and now live only in the bench probes,
+ * photonlibos_amd/csrc/stream_kernels.h.) */
 int photon_crc_set_generic_rows(int rows_per_step);
-
-/* The CRC-64 streaming kernel (uniform batches; off by default, the generic
- * kernel is faster): a shape turns it on -- rows per step U and steps in
- * flight D, one of (4,1..3), (2,2..4), (8,1); U = 0 turns it off again. */
-int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight);
-
-/* Interleaved row partials per lane in the CRC-64 streaming kernel (testing /
- * tuning): 1 (default), 2 or 4 (capped so that partials x lanes <= 64). */
-int photon_crc64_set_interleave(int partials);
 
 /* Message batches (photon_crc32c_batch_msg[_n], the CheckedMessage batch),
  * testing / tuning: 0 = automatic (default: one kernel with a lane group per
@@ -70,11 +54,6 @@ int photon_crc_set_msg_rows(int rows_per_step);
  * round, 64 x 2 from 512 MiB, 32 x 2 from 1 GiB, 64 x 4 from 1.5 GiB, 64 x 2
  * from 3 GiB. */
 int photon_crc_set_long_shape(int lanes, int rounds);
-
-/* CRC-64 streaming kernel: blocks per lane run (tuning): 1 (default) or 2 =
- * each lane reads two consecutive 16-byte blocks per row, one row shift per
- * 32 bytes (lanes per buffer <= 32; overrides the interleave). */
-int photon_crc64_set_run_blocks(int blocks);
 
 /* Lanes per buffer the engine picks for buffers of typical length n (the
  * lane-group table of DESIGN.md §4, or the override when one is set). */

@@ -64,12 +64,8 @@ def _declare(L):
     fn("photon_crc64ecma_extend_device", ctypes.c_int, vp, u64, u64, vp, vp)
     fn("photon_crc_util_fill_splitmix", ctypes.c_int, vp, u64, u64, u64, u64, vp)
     fn("photon_crc_util_read_stream", ctypes.c_int, vp, u64, vp, u64, vp)
-    fn("photon_crc_set_stream_config", ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int)
-    fn("photon_crc64_set_stream_config", ctypes.c_int, ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_generic_rows", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_long_shape", ctypes.c_int, ctypes.c_int, ctypes.c_int)
-    fn("photon_crc64_set_interleave", ctypes.c_int, ctypes.c_int)
-    fn("photon_crc64_set_run_blocks", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_msg_mode", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_host_register", ctypes.c_int, vp, u64)
     fn("photon_crc_stream_create", ctypes.c_int, ctypes.POINTER(vp))

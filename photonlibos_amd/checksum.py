@@ -28,7 +28,7 @@ __all__ = [
     "Shard", "batch_strided", "batch_strided_sync", "batch_iov", "batch_msg",
     "crc64ecma", "crc64ecma_extend", "crc64ecma_sw", "crc64ecma_hw", "crc64ecma_combine", "crc64ecma_series",
     "crc64ecma_combine_series", "crc64ecma_trim",
-    "batch64_strided", "batch64_iov", "combine64_batch", "trim64_batch", "batch64_msg_n", "host_batch64_strided", "extend64_device", "extend_spans", "extend64_spans", "Span", "combine_batch", "fill_splitmix", "read_stream", "set_stream_config", "IOVEC_DTYPE",
+    "batch64_strided", "batch64_iov", "combine64_batch", "trim64_batch", "batch64_msg_n", "host_batch64_strided", "extend64_device", "extend_spans", "extend64_spans", "Span", "combine_batch", "fill_splitmix", "read_stream", "IOVEC_DTYPE",
 ]
 
 _CRC_FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32)
@@ -498,14 +498,9 @@ def file_strided(fd, offset, stride, nbytes, count, seed=0):
     return list(out)[:count]
 
 
-def set_stream_config(run_blocks, rows_per_step=0, steps_in_flight=0):
-    """Streaming-kernel shape (B, U, D) for uniform batches; B = 0 disables it."""
-    _check(lib().photon_crc_set_stream_config(run_blocks, rows_per_step, steps_in_flight))
-
-
 def set_generic_rows(u):
     """Batch kernel variant: -1 (default) = by lane-group size; 2, 4, 8 = rows
-    per step of the generic kernel; 0 = the fused 4-row kernel."""
+    per step of the generic kernel."""
     _check(lib().photon_crc_set_generic_rows(u))
 
 
@@ -523,21 +518,6 @@ def set_long_shape(lanes=0, rounds=0):
 def set_msg_rows(u):
     """Rows per step of the one-kernel message form (2 or 4; tuning)."""
     _check(lib().photon_crc_set_msg_rows(u))
-
-
-def set_stream64_run_blocks(b):
-    """CRC-64 streaming kernel: 16-byte blocks per lane run (1, 2)."""
-    _check(lib().photon_crc64_set_run_blocks(b))
-
-
-def set_stream64_interleave(v):
-    """CRC-64 streaming kernel: interleaved row partials per lane (1, 2, 4)."""
-    _check(lib().photon_crc64_set_interleave(v))
-
-
-def set_stream64_config(rows_per_step, steps_in_flight):
-    """CRC-64 streaming-kernel shape (U, D)."""
-    _check(lib().photon_crc64_set_stream_config(rows_per_step, steps_in_flight))
 
 
 def read_stream(base, nbytes, sink, sink_words, stream=None):

@@ -28,9 +28,8 @@
 // bytes of the first aligned block are masked to 0 and the seed is XORed into
 // the first four data bytes (init-value linearity), so every load is an
 // aligned 16-byte load. Ragged tails (<16 B) are finished byte-serially.
-// Options (tuning, parity-tested, off by default because they measured
-// slower): a streaming kernel whose load ring runs continuously across buffer
-// boundaries, and a fused kernel with the row shifts folded into the tables.
+// (The streaming and fused variants that measured slower live in
+// stream_kernels.h, built only into the bench probes.)
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -69,48 +68,21 @@ thread_local std::string g_err;
 // Tuning knobs (include/photon_crc/tuning.h). Photon calls the checksum from
 // many vCPU threads at once and the reference promises reentrant calls
 // (crc.cpp:126-137: pointers written once, pure functions), so every knob is
-// an atomic word that a launch reads ONCE; a multi-field shape is packed into
-// one word so a launch never sees half of a concurrent setter's update.
+// an atomic word that a launch reads ONCE; a multi-field shape (the long
+// kernel's lanes and rounds) is packed into one word so a launch never sees
+// half of a concurrent setter's update.
 std::atomic<int> g_lanes_override{0};
 // Workgroups of the persistent batch grids (photon_crc_set_batch_grid,
 // tuning): 0 = one per CU (the default).
 std::atomic<int> g_grid_cap{0};
-// Batch kernel: rows per step of the generic kernel (2, 4, 8), or 0 = the
-// fused 4-row kernel (17 instead of 20 lookups per 16 B, measured 1-4 % slower:
-// the batch is HBM-bound, profiles/tune_r01_fused.jsonl).
 // Rows per step of the generic batch kernel: -1 = by lane-group size
-// (batch_rows), else 2, 4, 8, or 0 = the fused kernel.
+// (batch_rows), else 2, 4 or 8.
 std::atomic<int> g_generic_u{-1};
 // Rows per step of the one-kernel message form: 2 measured better than 4 on
 // C5 (64 Ki messages x 8 x 8 KiB: +0.35 points per-segment, +0.8 chained)
 // while strided batches keep 4 (C2 -6, C3 -1.2, C4 -0.9 with 2).
 std::atomic<int> g_msg_u{2};
 std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
-// Streaming kernel shape, 0 = off (the default: with the conflict-free rotated
-// tables the generic kernel measures faster on every config,
-// profiles/tune_r01_generic_rows.jsonl), else run blocks | rows/step << 8 |
-// steps in flight << 16.
-std::atomic<uint32_t> g_stream_cfg{0};
-// CRC-64 streaming kernel: bit 31 = on (off by default: the generic kernel is
-// faster with lagged blocks), rows/step (bits 0-7), steps in
-// flight (8-15), interleave (16-23), run blocks (24-30).
-std::atomic<uint32_t> g_stream64_cfg{4u | 3u << 8 | 1u << 16 | 1u << 24};
-std::mutex g_knob_mu;  // serialises read-modify-write setters of packed words
-
-struct Stream64Cfg {
-    bool on;
-    int u, d, v, b;
-};
-Stream64Cfg stream64_cfg() {
-    const uint32_t w = g_stream64_cfg.load(std::memory_order_relaxed);
-    return {(w >> 31) != 0, (int)(w & 0xff), (int)((w >> 8) & 0xff), (int)((w >> 16) & 0xff),
-            (int)((w >> 24) & 0x7f)};
-}
-void set_stream64_cfg(const Stream64Cfg& c) {
-    g_stream64_cfg.store((c.on ? 1u << 31 : 0u) | (uint32_t)c.u | (uint32_t)c.d << 8 | (uint32_t)c.v << 16 |
-                             (uint32_t)c.b << 24,
-                         std::memory_order_relaxed);
-}
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -383,22 +355,6 @@ int choose_lanes(uint64_t typical_len) {
     return 4;
 }
 
-FusedConsts make_fused_consts(int g) {
-    FusedConsts c;
-    for (int j = 0; j <= 4; ++j) c.xrow[j] = xpow(8ull * 16ull * (uint64_t)g * (uint64_t)j);
-    for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), c.basis[k]);
-    return c;
-}
-
-const FusedConsts& fused_consts(int g) {
-    static FusedConsts tab[7];
-    static std::once_flag once;
-    std::call_once(once, [] {
-        for (int lg = 2; lg <= 6; ++lg) tab[lg] = make_fused_consts(1 << lg);
-    });
-    return tab[g == 64 ? 6 : g == 32 ? 5 : g == 16 ? 4 : g == 8 ? 3 : 2];
-}
-
 // Lane-group size of the CRC32C generic batch kernel: as choose_lanes, but
 // 4-8 KiB buffers take 16 lanes (with 2 rows per step, batch_rows): C3 (1 Mi x
 // 4 KiB) 85.5 % vs 83.7 % for 8 lanes x 4 rows (profiles/r02_tune_lanes_rows.jsonl).
@@ -426,21 +382,6 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
     if (grid > (uint64_t)cus) grid = cus;
     if (const int cap = g_grid_cap.load(std::memory_order_relaxed)) grid = grid > (uint64_t)cap ? (uint64_t)cap : grid;
     const int rows_per_step = batch_rows(g);
-    if (rows_per_step == 0) {
-        const FusedConsts& fc = fused_consts(g);
-#define LF(GG) hipLaunchKernelGGL((crc32c_fused_kernel<GG>), dim3(grid), dim3(kBlock), 0, stream, a, fc)
-        switch (g) {
-            case 64: LF(64); break;
-            case 32: LF(32); break;
-            case 16: LF(16); break;
-            case 8: LF(8); break;
-            default: LF(4); break;
-        }
-#undef LF
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(e, "crc32c_fused_kernel launch");
-        return 0;
-    }
     const LaneConsts& kc = lane_consts(g);
 #define LB(GG, UU) \
     hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc, pow_table())
@@ -510,164 +451,6 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     return 0;
 }
 
-template <int G, int U, int D>
-void launch_uniform64_v(const Uniform64Args& a, dim3 grid, hipStream_t st, const Stream64Cfg& c) {
-    if constexpr (G <= 32) {
-        if (c.b == 2) {
-            hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, 1, 2>), grid, dim3(kBlock), 0, st, a,
-                               lane_consts64(2 * G));
-            return;
-        }
-    }
-    constexpr int V2 = (G <= 32 && U % 2 == 0) ? 2 : 1;
-    constexpr int V4 = (G <= 16 && U % 4 == 0) ? 4 : V2;
-    if (c.v >= 4)
-        hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, V4>), grid, dim3(kBlock), 0, st, a, lane_consts64(G * V4));
-    else if (c.v >= 2)
-        hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, V2>), grid, dim3(kBlock), 0, st, a, lane_consts64(G * V2));
-    else
-        hipLaunchKernelGGL((crc64_uniform_kernel<G, U, D, 1>), grid, dim3(kBlock), 0, st, a, lane_consts64(G));
-}
-
-template <int G>
-bool launch_uniform64_g(const Uniform64Args& a, dim3 grid, hipStream_t st, const Stream64Cfg& c) {
-    const int u = c.u, d = c.d;
-    if (u == 4 && d == 2) launch_uniform64_v<G, 4, 2>(a, grid, st, c);
-    else if (u == 4 && d == 3) launch_uniform64_v<G, 4, 3>(a, grid, st, c);
-    else if (u == 2 && d == 4) launch_uniform64_v<G, 2, 4>(a, grid, st, c);
-    else if (u == 8 && d == 1) launch_uniform64_v<G, 8, 1>(a, grid, st, c);
-    else if (u == 2 && d == 2) launch_uniform64_v<G, 2, 2>(a, grid, st, c);
-    else if (u == 2 && d == 3) launch_uniform64_v<G, 2, 3>(a, grid, st, c);
-    else if (u == 4 && d == 1) launch_uniform64_v<G, 4, 1>(a, grid, st, c);
-    else return false;
-    return true;
-}
-
-int try_launch_uniform64(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint64_t seed0,
-                         const uint64_t* seeds, uint64_t* out, hipStream_t stream) {
-    const Stream64Cfg c = stream64_cfg();
-    if (!c.on || count == 0) return 1;
-    const int g = choose_lanes(nbytes);
-    const int b = (c.b == 2 && g <= 32) ? 2 : 1;
-    const uint64_t row = 16ull * g * b;
-    if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
-    const uint64_t rows = nbytes / row;
-    if (rows % (uint64_t)c.u) return 1;
-    int cus = 0;
-    int dev = current_device(&cus);
-    if (dev < 0) return dev;
-    const uint64_t gpw = 64 / g;
-    const uint64_t waves = (count + gpw - 1) / gpw;
-    uint64_t grid = (waves + kWaves - 1) / kWaves;
-    if (grid > (uint64_t)cus) grid = cus;
-    const uint64_t xn = xpow64(8ull * nbytes);
-    Uniform64Args a{base, stride, rows, count, out, mulmod64(seeds ? ~0ull : ~seed0, xn)};
-    bool ok = false;
-    switch (g) {
-        case 64: ok = launch_uniform64_g<64>(a, dim3(grid), stream, c); break;
-        case 32: ok = launch_uniform64_g<32>(a, dim3(grid), stream, c); break;
-        case 16: ok = launch_uniform64_g<16>(a, dim3(grid), stream, c); break;
-        case 8: ok = launch_uniform64_g<8>(a, dim3(grid), stream, c); break;
-        default: ok = launch_uniform64_g<4>(a, dim3(grid), stream, c); break;
-    }
-    if (!ok) return fail(-EINVAL, "unsupported CRC-64 streaming configuration");
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "crc64_uniform_kernel launch");
-    if (seeds) {
-        SeedConsts64 sc;
-        for (int i = 0; i < 64; ++i) sc.basis[i] = mulmod64(1ull << i, xn);
-        const int bs = 256;
-        hipLaunchKernelGGL(crc64_seed_kernel, dim3((count + bs - 1) / bs), dim3(bs), 0, stream, out, count, seeds, sc);
-        e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(e, "crc64_seed_kernel launch");
-    }
-    return 0;
-}
-
-SeedConsts seed_consts(uint64_t nbytes) {
-    static std::mutex mu;
-    static uint64_t cached_n = ~0ull;
-    static SeedConsts cached;
-    std::lock_guard<std::mutex> lk(mu);
-    if (cached_n != nbytes) {
-        mul_basis(xpow(8ull * nbytes), cached.basis);
-        cached_n = nbytes;
-    }
-    return cached;
-}
-
-template <int G, int B, int U, int D>
-void launch_uniform_t(const UniformArgs& a, dim3 grid, hipStream_t stream) {
-    hipLaunchKernelGGL((crc32c_uniform_kernel<G, B, U, D>), grid, dim3(kBlock), 0, stream, a, lane_consts(G, B));
-}
-
-// The instantiated (B, U, D) shapes: ring registers (D+1)*U*B*4 <= 80 VGPRs.
-template <int G>
-bool launch_uniform_g(const UniformArgs& a, dim3 grid, hipStream_t stream, int b, int u, int d) {
-    if (b == 2 && u == 2 && d == 3) launch_uniform_t<G, 2, 2, 3>(a, grid, stream);
-    else if (b == 1 && u == 4 && d == 3) launch_uniform_t<G, 1, 4, 3>(a, grid, stream);
-    else if (b == 4 && u == 1 && d == 3) launch_uniform_t<G, 4, 1, 3>(a, grid, stream);
-    else if (b == 2 && u == 2 && d == 4) launch_uniform_t<G, 2, 2, 4>(a, grid, stream);
-    else if (b == 4 && u == 1 && d == 4) launch_uniform_t<G, 4, 1, 4>(a, grid, stream);
-    else if (b == 1 && u == 2 && d == 4) launch_uniform_t<G, 1, 2, 4>(a, grid, stream);
-    else if (b == 1 && u == 8 && d == 1) launch_uniform_t<G, 1, 8, 1>(a, grid, stream);
-    else if (b == 1 && u == 6 && d == 2) launch_uniform_t<G, 1, 6, 2>(a, grid, stream);
-    else if (b == 1 && u == 8 && d == 2) launch_uniform_t<G, 1, 8, 2>(a, grid, stream);
-    else if (b == 1 && u == 4 && d == 4) launch_uniform_t<G, 1, 4, 4>(a, grid, stream);
-    else if (b == 1 && u == 4 && d == 1) launch_uniform_t<G, 1, 4, 1>(a, grid, stream);
-    else if (b == 1 && u == 4 && d == 2) launch_uniform_t<G, 1, 4, 2>(a, grid, stream);
-    else if (b == 1 && u == 2 && d == 2) launch_uniform_t<G, 1, 2, 2>(a, grid, stream);
-    else if (b == 1 && u == 2 && d == 3) launch_uniform_t<G, 1, 2, 3>(a, grid, stream);
-    else return false;
-    return true;
-}
-
-bool stream_shape_ok(int b, int u, int d) {
-    return (b == 2 && u == 2 && (d == 3 || d == 4)) ||
-           (b == 1 && ((u == 4 && d >= 1 && d <= 4) || (u == 2 && d >= 2 && d <= 4) || (u == 8 && (d == 1 || d == 2)) ||
-                       (u == 6 && d == 2))) ||
-           (b == 4 && u == 1 && (d == 3 || d == 4));
-}
-
-int try_launch_uniform(const uint8_t* base, uint64_t stride, uint64_t nbytes, uint64_t count, uint32_t seed0,
-                       const uint32_t* seeds, uint32_t* out, hipStream_t stream) {
-    const uint32_t cfg = g_stream_cfg.load(std::memory_order_relaxed);
-    if (!cfg || count == 0) return 1;
-    const int sb = (int)(cfg & 0xff), su = (int)((cfg >> 8) & 0xff), sd = (int)((cfg >> 16) & 0xff);
-    const int g = choose_lanes(nbytes);
-    const uint64_t row = 16ull * g * (uint64_t)sb;
-    if ((reinterpret_cast<uintptr_t>(base) & 15) || (stride & 15) || nbytes < row || nbytes % row) return 1;
-    const uint64_t rows = nbytes / row;
-    if (rows % (uint64_t)su) return 1;
-    int cus = 0;
-    int dev = current_device(&cus);
-    if (dev < 0) return dev;
-    const uint64_t gpw = 64 / g;
-    const uint64_t waves = (count + gpw - 1) / gpw;
-    uint64_t grid = (waves + kWaves - 1) / kWaves;
-    if (grid > (uint64_t)cus) grid = cus;
-    UniformArgs a{base, stride, rows, count, out};
-    bool ok = false;
-    switch (g) {
-        case 64: ok = launch_uniform_g<64>(a, dim3(grid), stream, sb, su, sd); break;
-        case 32: ok = launch_uniform_g<32>(a, dim3(grid), stream, sb, su, sd); break;
-        case 16: ok = launch_uniform_g<16>(a, dim3(grid), stream, sb, su, sd); break;
-        case 8: ok = launch_uniform_g<8>(a, dim3(grid), stream, sb, su, sd); break;
-        default: ok = launch_uniform_g<4>(a, dim3(grid), stream, sb, su, sd); break;
-    }
-    if (!ok) return fail(-EINVAL, "unsupported streaming configuration");
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "crc32c_uniform_kernel launch");
-    if (seeds || seed0) {
-        const int bs = 256;
-        hipLaunchKernelGGL(crc32c_seed_kernel, dim3((count + bs - 1) / bs), dim3(bs), 0, stream, out, count, seeds,
-                           seed0, seed_consts(nbytes));
-        e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(e, "crc32c_seed_kernel launch");
-    }
-    return 0;
-}
-
 // Host-memory pipeline (photon_crc32c_host_batch_strided): per device, a copy
 // stream and a compute stream, kNumStage device staging chunks. Chunk i is
 // copied (H2D, 2-D so any host stride packs densely) while chunk i-1 is
@@ -724,15 +507,96 @@ LongPlan long_plan(const void* data, uint64_t n, int cus, bool crc64) {
     return long_plan_for(data, n, cus, g_long_shape.load(std::memory_order_relaxed), 0, crc64);
 }
 
-// A multi-workgroup long launch may not be captured into a graph (see
-// long_state); one-workgroup launches (<= 256 KiB) hold no state and may.
-int refuse_if_capturing(hipStream_t st) {
+// Run f() with this thread's stream-capture mode relaxed: the library's own
+// one-time setup (hipMalloc, a copy on a private stream and its wait) is then
+// legal even while some stream of the process -- possibly the caller's -- is
+// being captured into a graph (global capture mode refuses such calls and
+// invalidates the capture).
+template <typename F>
+hipError_t relaxed_capture(F f) {
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    const hipError_t ex = hipThreadExchangeStreamCaptureMode(&m);
+    const hipError_t e = f();
+    if (ex == hipSuccess) (void)hipThreadExchangeStreamCaptureMode(&m);
+    return e;
+}
+
+// A multi-workgroup launch captured into a HIP graph cannot use the stream's
+// persistent reduce state (the graph would embed one ticket base and replay
+// it). It gets a state of its own instead, owned by the graph being captured:
+// zeroed, in reset mode (the last workgroup puts the ticket back to 0, so the
+// graph replays any number of times), handed back to a per-device free list
+// by a graph user object when the graph is destroyed. Replays of one graph
+// run in order; two executable graphs instantiated from the SAME captured
+// graph share its states and must not run at the same time (ADVICE r4:
+// multi-workgroup captures used to be refused with -ENOTSUP).
+constexpr uint64_t kStateBytes = 8 + 8 * kLongMaxGrid;
+struct CapState {
+    int dev;
+    void* p;
+};
+std::mutex g_cap_mu;
+std::vector<CapState*> g_cap_free;
+
+void cap_state_release(void* arg) {  // graph user-object destructor: host bookkeeping only
+    std::lock_guard<std::mutex> lk(g_cap_mu);
+    g_cap_free.push_back(static_cast<CapState*>(arg));
+}
+
+int capture_state(hipStream_t st, void** out) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    hipError_t e = hipStreamGetCaptureInfo_v2(st, &cs, &id, &graph, nullptr, nullptr);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamGetCaptureInfo_v2");
+    if (cs != hipStreamCaptureStatusActive || !graph) return fail(-ENOTSUP, "stream capture is not active");
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return hip_fail(e, "hipGetDevice");
+    CapState* c = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_cap_mu);
+        for (size_t i = 0; i < g_cap_free.size(); ++i)
+            if (g_cap_free[i]->dev == dev) {
+                c = g_cap_free[i];
+                g_cap_free.erase(g_cap_free.begin() + (long)i);
+                break;
+            }
+    }
+    if (!c) {
+        c = new CapState{dev, nullptr};
+        e = relaxed_capture([&] {
+            hipStream_t s = nullptr;
+            hipError_t r = hipMalloc(&c->p, kStateBytes);
+            if (r == hipSuccess) r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            if (r == hipSuccess) r = hipMemsetAsync(c->p, 0, kStateBytes, s);
+            if (r == hipSuccess) r = hipStreamSynchronize(s);
+            if (s) (void)hipStreamDestroy(s);
+            return r;
+        });
+        if (e != hipSuccess) {
+            if (c->p) (void)hipFree(c->p);
+            delete c;
+            return hip_fail(e, "capture reduce state");
+        }
+    }
+    hipUserObject_t obj = nullptr;
+    e = hipUserObjectCreate(&obj, c, cap_state_release, 1, hipUserObjectNoDestructorSync);
+    if (e == hipSuccess) e = hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove);
+    if (e != hipSuccess) {
+        if (obj) (void)hipUserObjectRelease(obj, 1);  // runs cap_state_release
+        else cap_state_release(c);
+        return hip_fail(e, "graph user object (capture reduce state)");
+    }
+    *out = c->p;
+    return 0;
+}
+
+// hipStreamCaptureStatus of `st` (None when not capturing), or an error.
+int capture_status(hipStream_t st, bool* capturing) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     const hipError_t e = hipStreamIsCapturing(st, &cs);
     if (e != hipSuccess) return hip_fail(e, "hipStreamIsCapturing");
-    if (cs != hipStreamCaptureStatusNone)
-        return fail(-ENOTSUP, "a long-buffer call over 256 KiB cannot be captured into a HIP graph "
-                              "(its cross-workgroup reduce state is per stream)");
+    *capturing = cs != hipStreamCaptureStatusNone;
     return 0;
 }
 
@@ -747,9 +611,9 @@ int refuse_if_capturing(hipStream_t st) {
 // order as the launches are enqueued. If a destroyed stream's handle (or a
 // recycled thread id's per-thread stream) comes back while the old stream's
 // last launch still runs, the two launches may spoil each other's result,
-// but the count stays exact for every later launch. A stream
-// being captured into a HIP graph is refused by the caller (the graph would
-// embed one `base` and replay it). lease != nullptr: a leased scratch buffer
+// but the count stays exact for every later launch. A launch
+// captured into a HIP graph uses a graph-owned state instead (capture_state:
+// the graph would embed one `base` and replay it). lease != nullptr: a leased scratch buffer
 // instead (more than 4096 streams seen), ticket 0 and put back to 0 by the
 // kernel, to be returned with scratch_free.
 struct LongState {
@@ -775,14 +639,14 @@ int long_state(hipStream_t st, LongState** out, void** lease) {
             *out = it->second;
             return 0;
         }
-        if (g_long_state.size() >= 4096) return scratch_alloc(lease, 8 + 8 * kLongMaxGrid, st, true);
+        if (g_long_state.size() >= 4096) return scratch_alloc(lease, kStateBytes, st, true);
     }
     auto* ls = new LongState;
-    if ((e = hipMalloc(&ls->p, 8 + 8 * kLongMaxGrid)) != hipSuccess) {
+    if ((e = hipMalloc(&ls->p, kStateBytes)) != hipSuccess) {
         delete ls;
         return hip_fail(e, "hipMalloc(long state)");
     }
-    if ((e = hipMemset(ls->p, 0, 8 + 8 * kLongMaxGrid)) != hipSuccess) {
+    if ((e = hipMemset(ls->p, 0, kStateBytes)) != hipSuccess) {
         (void)hipFree(ls->p);
         delete ls;
         return hip_fail(e, "hipMemset(long state)");
@@ -806,7 +670,14 @@ int long_launch(hipStream_t st, uint64_t grid, const char* what, L launch) {
         const hipError_t e = launch(nullptr, 0ull, 0u);
         return e == hipSuccess ? 0 : hip_fail(e, what);
     }
-    if (int rc = refuse_if_capturing(st)) return rc;
+    bool capturing = false;
+    if (int rc = capture_status(st, &capturing)) return rc;
+    if (capturing) {  // a state owned by the graph, in reset mode
+        void* cs = nullptr;
+        if (int rc = capture_state(st, &cs)) return rc;
+        const hipError_t e = launch(cs, 0ull, 1u);
+        return e == hipSuccess ? 0 : hip_fail(e, what);
+    }
     LongState* ls = nullptr;
     void* lease = nullptr;
     if (int rc = long_state(st, &ls, &lease)) return rc;
@@ -852,12 +723,15 @@ int small_image(int dev, const uint32_t** out) {
     if (!g_img[dev]) {
         static const std::vector<uint32_t> host = small_image_host();
         void* d = nullptr;
-        hipStream_t s = nullptr;
-        hipError_t e = hipMalloc(&d, kSmImage);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMemcpyAsync(d, host.data(), kSmImage, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (s) (void)hipStreamDestroy(s);
+        const hipError_t e = relaxed_capture([&] {  // legal during a caller's graph capture
+            hipStream_t s = nullptr;
+            hipError_t r = hipMalloc(&d, kSmImage);
+            if (r == hipSuccess) r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            if (r == hipSuccess) r = hipMemcpyAsync(d, host.data(), kSmImage, hipMemcpyHostToDevice, s);
+            if (r == hipSuccess) r = hipStreamSynchronize(s);
+            if (s) (void)hipStreamDestroy(s);
+            return r;
+        });
         if (e != hipSuccess) {
             if (d) (void)hipFree(d);
             return hip_fail(e, "small-buffer table image");
@@ -900,12 +774,15 @@ int small64_image(int dev, const uint64_t** out) {
     if (!g_img64[dev]) {
         static const std::vector<uint64_t> host = small64_image_host();
         void* d = nullptr;
-        hipStream_t s = nullptr;
-        hipError_t e = hipMalloc(&d, kSm64Image);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMemcpyAsync(d, host.data(), kSm64Image, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (s) (void)hipStreamDestroy(s);
+        const hipError_t e = relaxed_capture([&] {  // legal during a caller's graph capture
+            hipStream_t s = nullptr;
+            hipError_t r = hipMalloc(&d, kSm64Image);
+            if (r == hipSuccess) r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            if (r == hipSuccess) r = hipMemcpyAsync(d, host.data(), kSm64Image, hipMemcpyHostToDevice, s);
+            if (r == hipSuccess) r = hipStreamSynchronize(s);
+            if (s) (void)hipStreamDestroy(s);
+            return r;
+        });
         if (e != hipSuccess) {
             if (d) (void)hipFree(d);
             return hip_fail(e, "CRC-64 small-buffer table image");
@@ -1058,21 +935,9 @@ int photon_crc_test_long_plan(uint64_t addr, uint64_t n, int cus, int lanes, int
 }
 
 int photon_crc_set_generic_rows(int rows_per_step) {
-    if (rows_per_step != -1 && rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
-        return fail(-EINVAL, "rows per step must be -1 (auto), 0 (fused kernel), 2, 4 or 8");
+    if (rows_per_step != -1 && rows_per_step != 2 && rows_per_step != 4 && rows_per_step != 8)
+        return fail(-EINVAL, "rows per step must be -1 (auto), 2, 4 or 8");
     g_generic_u.store(rows_per_step, std::memory_order_relaxed);
-    return 0;
-}
-
-int photon_crc_set_stream_config(int run_blocks, int rows_per_step, int steps_in_flight) {
-    if (run_blocks == 0) {
-        g_stream_cfg.store(0, std::memory_order_relaxed);
-        return 0;
-    }
-    if (!stream_shape_ok(run_blocks, rows_per_step, steps_in_flight))
-        return fail(-EINVAL, "unsupported (run_blocks, rows_per_step, steps_in_flight)");
-    g_stream_cfg.store((uint32_t)run_blocks | (uint32_t)rows_per_step << 8 | (uint32_t)steps_in_flight << 16,
-                       std::memory_order_relaxed);
     return 0;
 }
 
@@ -1095,48 +960,9 @@ int photon_crc_set_msg_rows(int rows_per_step) {
     return 0;
 }
 
-int photon_crc64_set_run_blocks(int blocks) {
-    if (blocks != 1 && blocks != 2) return fail(-EINVAL, "run blocks must be 1 or 2");
-    std::lock_guard<std::mutex> lk(g_knob_mu);
-    Stream64Cfg c = stream64_cfg();
-    c.b = blocks;
-    set_stream64_cfg(c);
-    return 0;
-}
-
-int photon_crc64_set_interleave(int partials) {
-    if (partials != 1 && partials != 2 && partials != 4) return fail(-EINVAL, "interleave must be 1, 2 or 4");
-    std::lock_guard<std::mutex> lk(g_knob_mu);
-    Stream64Cfg c = stream64_cfg();
-    c.v = partials;
-    set_stream64_cfg(c);
-    return 0;
-}
-
-int photon_crc64_set_stream_config(int rows_per_step, int steps_in_flight) {
-    const int u = rows_per_step, d = steps_in_flight;
-    std::lock_guard<std::mutex> lk(g_knob_mu);
-    Stream64Cfg c = stream64_cfg();
-    if (u == 0) {
-        c.on = false;
-        set_stream64_cfg(c);
-        return 0;
-    }
-    if (!((u == 4 && (d >= 1 && d <= 3)) || (u == 2 && (d >= 2 && d <= 4)) || (u == 8 && d == 1)))
-        return fail(-EINVAL, "unsupported CRC-64 (rows_per_step, steps_in_flight)");
-    c.on = true;
-    c.u = u;
-    c.d = d;
-    set_stream64_cfg(c);
-    return 0;
-}
-
 int photon_crc32c_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                 uint32_t seed0, const uint32_t* d_seeds, uint32_t* d_out, void* stream) {
     if (count && (!d_out || (!d_base && nbytes))) return fail(-EINVAL, "null buffer or output");
-    int rc = try_launch_uniform(static_cast<const uint8_t*>(d_base), stride, nbytes, count, seed0, d_seeds, d_out,
-                                static_cast<hipStream_t>(stream));
-    if (rc <= 0) return rc;
     BatchArgs a{};
     a.base = static_cast<const uint8_t*>(d_base);
     a.stride = stride;
@@ -1437,11 +1263,6 @@ int photon_crc32c_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* d_m
 int photon_crc64ecma_batch_strided(const void* d_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                    uint64_t seed0, const uint64_t* d_seeds, uint64_t* d_out, void* stream) {
     if (count && (!d_out || (!d_base && nbytes))) return fail(-EINVAL, "null buffer or output");
-    {
-        const int rc = try_launch_uniform64(static_cast<const uint8_t*>(d_base), stride, nbytes, count, seed0, d_seeds,
-                                            d_out, static_cast<hipStream_t>(stream));
-        if (rc <= 0) return rc;  // launched (0) or failed (< 0); 1 = not a uniform batch
-    }
     Batch64Args a{};
     a.base = static_cast<const uint8_t*>(d_base);
     a.stride = stride;

@@ -70,10 +70,6 @@ struct LaneConsts64 {
     uint64_t sbasis[64];       // basis of kshift (S64 entries by select-XOR)
 };
 
-struct SeedConsts64 {
-    uint64_t basis[64];        // basis of x^(8 * nbytes) mod P64
-};
-
 struct Batch64Args {
     const uint8_t* base;
     uint64_t stride;
@@ -89,15 +85,6 @@ struct Batch64Args {
     // being XORed into every buffer's first words by two lanes per group.
     uint64_t init_shift;
     uint32_t shift_init;
-};
-
-struct Uniform64Args {
-    const uint8_t* base;
-    uint64_t stride;
-    uint64_t rows;             // nbytes / (16*G)
-    uint64_t count;
-    uint64_t* out;
-    uint64_t init_shift;       // (~seed0) * x^(8*nbytes): the inverted init's contribution
 };
 
 __device__ __forceinline__ uint2 lds_u2(const uint32_t* lds, uint32_t byte_addr) {
@@ -514,165 +501,6 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
     crc64_batch_run<G>(args, kc, lds, nullptr);
 }
 
-// Uniform batches (aligned base and stride, nbytes = R*16*G with R % U == 0):
-// the continuous cross-buffer load ring of crc32c_uniform_kernel (B = 1).
-// Register init 0; lane 0 applies the inverted init (~seed0 * x^(8n)) and the
-// final inversion; per-buffer seeds are folded in by crc64_seed_kernel.
-// V interleaved partials per lane: partial j takes rows r = j (mod V), i.e.
-// lane l plays virtual lane j*G + l of a V*G-lane geometry (row shift
-// x^(8*16*G*V), the kc passed is lane_consts64(G*V)); V independent S chains
-// of U/V steps instead of one of U steps.
-// Lagged CRC (x^-64 times the CRC register, init 0) after a run of B
-// consecutive 16-byte blocks (lag16_64 for B = 1).
-template <int B>
-__device__ __forceinline__ uint2 lag_run64(const uint32_t* lds, const uint4 (&w)[B], const LaneAddr64& a) {
-    uint2 c = dstep64(lds, make_uint2(w[0].x, w[0].y), a, make_uint2(w[0].z, w[0].w));
-#pragma unroll
-    for (int b = 1; b < B; ++b) {
-        c = dstep64(lds, c, a, make_uint2(w[b].x, w[b].y));
-        c = dstep64(lds, c, a, make_uint2(w[b].z, w[b].w));
-    }
-    return c;
-}
-
-// B = 2: each lane reads a RUN of two consecutive blocks per row (two
-// dwordx4 loads, lane stride 32 B) and pays the row shift once per 32 bytes
-// (3 D + 1 S steps = 32 lookups per 32 B, as two lagged single blocks). The
-// lane then plays the 2G-lane geometry's blocks 2l, 2l+1 (kc = lane_consts64(2G)).
-// ABL != 0 only in bench-only ablation builds (probes.hip); results are then
-// NOT CRCs: 1 = no S (row-shift) lookups, 2 = one D step on lo ^ hi per
-// block (no data chain), 4 = no table lookups at all.
-// V = B = 1 (one partial per lane, single blocks): the batch kernel's finish
-// (finish tables A_dl / B_dh, finish_xor16 at 16 lanes: 17 lookups per lane)
-// instead of a D step plus log2(G) R64 levels (8 + 16 log2(G) lookups).
-template <int G, int U, int D, int V = 1, int B = 1, int ABL = 0>
-__global__ __launch_bounds__(kBlock) void crc64_uniform_kernel(Uniform64Args args, LaneConsts64 kc) {
-    constexpr bool kFin = V == 1 && B == 1 && ABL == 0;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(kFin ? k64FLdsBytes : k64LdsBytes) / 4];
-    build_tables64<kFin ? G : 0>(lds, kc);
-
-    constexpr uint64_t GPW = 64 / G;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & (G - 1);
-    const uint32_t grp = lane / G;
-    const LaneAddr64 la = lane_addr64(lane);
-
-    const uint64_t ngroups = (args.count + GPW - 1) / GPW;
-    const uint64_t wv0 = (uint64_t)blockIdx.x * kWaves + wave_id();
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-    if (wv0 >= ngroups) return;
-    const uint64_t nslots = (ngroups - 1 - wv0) / nwaves + 1;
-    const uint64_t spb = args.rows / U;
-    const uint64_t nsteps = nslots * spb;
-    constexpr uint64_t kRow = 16ull * G * B;
-
-    auto buffer_of = [&](uint64_t slot) -> uint64_t {
-        const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
-        return bi < args.count ? bi : args.count - 1;
-    };
-    auto slot_base = [&](uint64_t slot) -> const uint8_t* {
-        if (slot >= nslots) slot = nslots - 1;
-        return args.base + buffer_of(slot) * args.stride + 16ull * B * gl;
-    };
-    uint64_t lslot = 0, lstep = 0;
-    const uint8_t* lptr = slot_base(0);
-    auto advance = [&]() {
-        if (++lstep == spb) {
-            lstep = 0;
-            ++lslot;
-            lptr = slot_base(lslot);
-        } else if (lslot < nslots) {
-            lptr += kRow * U;
-        }
-    };
-    constexpr int S = D + 1;
-    uint4 ring[S][U][B];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int b = 0; b < B; ++b) ring[d][u][b] = load16(lptr + u * kRow + 16 * b);
-        advance();
-    }
-    const uint64_t padded = (nsteps + S - 1) / S * S;
-    static_assert(U % V == 0 && G * V * B <= 64 && (V == 1 || B == 1),
-                  "interleave must divide the step; V*B*G virtual lanes <= 64; runs and interleave exclusive");
-    constexpr int VGB = G * V * B;
-    constexpr int LOG2VG = VGB == 64 ? 6 : VGB == 32 ? 5 : VGB == 16 ? 4 : VGB == 8 ? 3 : 2;
-    uint64_t slot = 0, step = 0;
-    uint2 pc[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) pc[j] = make_uint2(0, 0);
-    for (uint64_t s = 0; s < padded; s += S) {
-#pragma unroll
-        for (int d = 0; d < S; ++d) {
-            const int refill = (d + D) % S;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int b = 0; b < B; ++b) ring[refill][u][b] = load16(lptr + u * kRow + 16 * b);
-            advance();
-            uint2 c[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if constexpr (ABL & 4) {
-                    c[u] = make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w);
-                } else if constexpr (ABL & 2) {
-                    c[u] = dstep64(lds, make_uint2(ring[d][u][0].x ^ ring[d][u][0].z, ring[d][u][0].y ^ ring[d][u][0].w),
-                                   la);
-                } else {
-                    c[u] = lag_run64<B>(lds, ring[d][u], la);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if constexpr (ABL & 1) pc[u % V] = make_uint2((pc[u % V].x ^ (pc[u % V].y << 1)) ^ c[u].x,
-                                                              (pc[u % V].y ^ (pc[u % V].x >> 1)) ^ c[u].y);
-                else pc[u % V] = sstep64(lds, pc[u % V], la, c[u]);
-            }
-            if (++step == spb) {
-                uint64_t acc = 0;
-                if constexpr (kFin) {  // Q * x^(64 + 128 d), d = G - 1 - gl, XOR over the group
-                    const uint32_t d = G - 1 - gl;
-                    if constexpr (G == 16 && PCRC64_FIN16) {
-                        acc = finish_xor16(pc[0], d, lds, gl, lane);
-                    } else {
-                        const uint64_t f = finish64<G>(pc[0], d, lds, lane);
-                        acc = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < V; ++j)  // Q -> P (dstep), then the lane shift
-                        acc ^= shift64<LOG2VG>(u64of(ABL ? pc[j] : dstep64(lds, pc[j], la)),
-                                               (uint32_t)((G * V - 1 - (j * G + gl)) * B), lds);
-#pragma unroll
-                    for (int o = G / 2; o > 0; o >>= 1) {
-                        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, o, 64);
-                        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), o, 64);
-                        acc ^= ((uint64_t)hi32 << 32) | lo32;
-                    }
-                }
-                const uint64_t bi = (wv0 + slot * nwaves) * GPW + grp;
-                if (gl == 0 && slot < nslots && bi < args.count) args.out[bi] = ~(acc ^ args.init_shift);
-#pragma unroll
-                for (int j = 0; j < V; ++j) pc[j] = make_uint2(0, 0);
-                step = 0;
-                ++slot;
-            }
-        }
-    }
-}
-
-// out[i] ^= seed_i * x^(8*nbytes) (the uniform kernel used seed0 = 0:
-// ~(F ^ ~s*X) = ~(F ^ ~0*X) ^ s*X).
-__global__ void crc64_seed_kernel(uint64_t* out, uint64_t count, const uint64_t* seeds, SeedConsts64 sc) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    out[i] ^= mul_basis64(seeds[i], sc.basis);
-}
-
-
 // ---------------------------------------------- CRC-64 combine / fold / extend
 // crc64ecma_combine(c1, c2, len2) = c1 ? c2 ^ c1 * x^(8*len2) : c2
 // (crc.cpp crc64ecma_combine_sw: the inverted-CRC combine is linear). A
@@ -983,7 +811,8 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
 #pragma unroll
     for (int r = 0; r < (int)kSmallRows; ++r) {
         const int b = first + r * (int)kSmallLanes;
-        w[r] = ((uint32_t)r < rows && b >= 0) ? load16(a.a0 + 16 * (uint32_t)b) : make_uint4(0, 0, 0, 0);
+        w[r] = ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) ? load16(a.a0 + 16 * (uint32_t)b)
+                                                                           : make_uint4(0, 0, 0, 0);  // as crc32c_small_kernel
     }
     const uint64_t bw_wave = a.image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
     const uint64_t bw_tail = a.image[kSm64Tail / 8 + a.k * 64u + lane];

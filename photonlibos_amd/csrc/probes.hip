@@ -11,6 +11,7 @@
 #include "crc32c_kernels.h"
 #include "crc64_kernels.h"
 #include "long_plan.h"
+#include "stream_kernels.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;

@@ -33,9 +33,8 @@ for v in args.variants.split(",") * args.repeat:
     if v == "read":
         fn = lambda: ck.read_stream(buf, total, sink, sink.numel(), stream=st)  # noqa: E731
     else:
-        _, g, b, u, d = v.split(":")
+        _, g = v.split(":")[:2]
         ck.set_lanes_per_buffer(int(g))
-        ck.set_stream_config(int(b), int(u), int(d))
         fn = lambda: ck.batch_strided(buf, nbytes, nbytes, count, out, stream=st)  # noqa: E731
     time.sleep(args.rest)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.n)]
@@ -49,4 +48,3 @@ for v in args.variants.split(",") * args.repeat:
                       "median_ms": round(float(np.median(ms)), 4),
                       "median_GBps": round(total / float(np.median(ms)) / 1e6, 1)}), flush=True)
 ck.set_lanes_per_buffer(0)
-ck.set_stream_config(0, 0, 0)

@@ -18,7 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--variants", default="stream:2:2:3,stream:1:4:3,stream:4:1:3,stream:2:2:4,stream:4:1:4,stream:1:2:4,generic")
+ap.add_argument("--variants", default="generic,generic:2,generic:4,generic:8,g64")
 ap.add_argument("--lanes", default="0")
 ap.add_argument("--count", type=int, default=0, help="override buffer count")
 args = ap.parse_args()
@@ -50,30 +50,15 @@ def timed(fn):
 def make(v, lanes):
     if v == "read":
         return lambda: ck.read_stream(buf, total, sink, sink.numel(), stream=stream)
-    if v.startswith("s64") or v == "g64":
+    if v == "g64":
         def f64():
             ck.set_lanes_per_buffer(lanes)
-            if v == "g64":
-                ck.set_stream64_config(0, 0)
-            elif v.startswith("s64b2"):
-                parts = v.split(":")
-                ck.set_stream64_config(int(parts[1]), int(parts[2]))
-                ck.set_stream64_run_blocks(2)
-            else:
-                ck.set_stream64_run_blocks(1)
-                parts = v.split(":")
-                ck.set_stream64_config(int(parts[1]), int(parts[2]))
-                ck.set_stream64_interleave(int(parts[3]) if len(parts) > 3 else 2)
             ck.batch64_strided(buf, nbytes, nbytes, count, out64, stream=stream)
         return f64
+
     def f():
         ck.set_lanes_per_buffer(lanes)
-        if v.startswith("generic"):
-            ck.set_generic_rows(int(v.split(":")[1]) if ":" in v else -1)
-            ck.set_stream_config(0)
-        else:
-            _, b, u, d = v.split(":")
-            ck.set_stream_config(int(b), int(u), int(d))
+        ck.set_generic_rows(int(v.split(":")[1]) if ":" in v else -1)
         ck.batch_strided(buf, nbytes, nbytes, count, out, stream=stream)
     return f
 
@@ -89,16 +74,12 @@ for r in range(args.rounds):
         res[f"{v}/G{l}"].append(ms)
         if v != "read":
             torch.cuda.synchronize()
-            is64 = v.startswith("s64") or v == "g64"
+            is64 = v == "g64"
             o = (out64 if is64 else out).cpu().numpy().copy()
             key = "64" if is64 else "32"
             if key not in refs:
                 refs[key] = o
             assert np.array_equal(o, refs[key]), f"variant {v}/G{l} disagrees"
-ck.set_stream_config(0, 0, 0)
-ck.set_stream64_config(0, 0)
-ck.set_stream64_interleave(1)
-ck.set_stream64_run_blocks(1)
 ck.set_generic_rows(-1)
 ck.set_lanes_per_buffer(0)
 rows = []

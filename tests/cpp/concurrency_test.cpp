@@ -59,14 +59,14 @@ std::atomic<long> g_checked{0}, g_bad{0}, g_err{0};
     } while (0)
 
 // Knob state as set by the flipper (for the mismatch report only).
-std::atomic<int> g_k_lanes{0}, g_k_rows{-1}, g_k_stream{0}, g_k_msg{0}, g_k_s64{0}, g_k_il{1};
+std::atomic<int> g_k_lanes{0}, g_k_rows{-1}, g_k_msg{0}, g_k_long{0}, g_k_grid{0};
 
 void check_at(bool ok, const char* what, uint64_t a, uint64_t b, uint64_t c) {
     g_checked.fetch_add(1);
     if (!ok && g_bad.fetch_add(1) < 30)
-        fprintf(stderr, "MISMATCH %s (%llu, %llu, %llu) knobs now: lanes %d rows %d stream %d msg %d s64 %d il %d\n",
+        fprintf(stderr, "MISMATCH %s (%llu, %llu, %llu) knobs now: lanes %d rows %d msg %d long %#x grid %d\n",
                 what, (unsigned long long)a, (unsigned long long)b, (unsigned long long)c, g_k_lanes.load(),
-                g_k_rows.load(), g_k_stream.load(), g_k_msg.load(), g_k_s64.load(), g_k_il.load());
+                g_k_rows.load(), g_k_msg.load(), g_k_long.load(), g_k_grid.load());
 }
 #define check(ok) check_at((ok), kind_name, p0, p1, p2)
 
@@ -257,28 +257,27 @@ void submitter(int t) {
 void knob_flipper() {
     std::mt19937 rng(7);
     const int lanes[] = {0, 4, 8, 16, 32, 64};
-    const int rows[] = {-1, 0, 2, 4, 8};
+    const int rows[] = {-1, 2, 4, 8};
+    const int long_lanes[] = {0, 32, 64};
     long flips = 0;
     while (!g_stop.load()) {
-        switch (rng() % 6) {
+        switch (rng() % 5) {
             case 0: { int v = lanes[rng() % 6]; photon_crc_set_lanes_per_buffer(v); g_k_lanes = v; break; }
-            case 1: { int v = rows[rng() % 5]; photon_crc_set_generic_rows(v); g_k_rows = v; break; }
-            case 2:
-                if (rng() & 1) { photon_crc_set_stream_config(0, 0, 0); g_k_stream = 0; }
-                else { photon_crc_set_stream_config(1, 4, 3); g_k_stream = 1; }
-                break;
-            case 3: {
+            case 1: { int v = rows[rng() % 4]; photon_crc_set_generic_rows(v); g_k_rows = v; break; }
+            case 2: {
                 int v = (int)(rng() % 3);
                 photon_crc_set_msg_mode(v);
                 photon_crc_set_msg_rows(rng() & 1 ? 2 : 4);
                 g_k_msg = v;
                 break;
             }
-            case 4:
-                if (rng() & 1) { photon_crc64_set_stream_config(0, 0); g_k_s64 = 0; }
-                else { photon_crc64_set_stream_config(4, 3); g_k_s64 = 1; }
+            case 3: {
+                int l = long_lanes[rng() % 3], r = l ? (int)(rng() % 4) : 0;
+                photon_crc_set_long_shape(l, r);
+                g_k_long = l << 8 | r;
                 break;
-            default: { int v = rng() & 1 ? 1 : 2; photon_crc64_set_interleave(v); g_k_il = v; break; }
+            }
+            default: { int v = rng() & 1 ? 0 : 64 + (int)(rng() % 192); photon_crc_set_batch_grid(v); g_k_grid = v; break; }
         }
         ++flips;
         std::this_thread::yield();
@@ -286,11 +285,10 @@ void knob_flipper() {
     // back to the defaults
     photon_crc_set_lanes_per_buffer(0);
     photon_crc_set_generic_rows(-1);
-    photon_crc_set_stream_config(0, 0, 0);
     photon_crc_set_msg_mode(0);
     photon_crc_set_msg_rows(2);
-    photon_crc64_set_stream_config(0, 0);
-    photon_crc64_set_interleave(1);
+    photon_crc_set_long_shape(0, 0);
+    photon_crc_set_batch_grid(0);
     printf("knob flips: %ld\n", flips);
 }
 
@@ -311,9 +309,9 @@ int main() {
         for (int t = 0; t < kThreads; ++t)
             fprintf(stderr, "WATCHDOG thread %d: iteration %d kind %d phase %s\n", t, g_where[t].it.load(),
                     g_where[t].kind.load(), kPhase[g_where[t].phase.load()]);
-        fprintf(stderr, "WATCHDOG knobs: lanes %d rows %d stream %d msg %d s64 %d il %d; checked %ld\n",
-                g_k_lanes.load(), g_k_rows.load(), g_k_stream.load(), g_k_msg.load(), g_k_s64.load(),
-                g_k_il.load(), g_checked.load());
+        fprintf(stderr, "WATCHDOG knobs: lanes %d rows %d msg %d long %#x grid %d; checked %ld\n",
+                g_k_lanes.load(), g_k_rows.load(), g_k_msg.load(), g_k_long.load(), g_k_grid.load(),
+                g_checked.load());
         fflush(stderr);
         _exit(3);
     }).detach();

@@ -95,26 +95,11 @@ def test_strided(torch_dev, oracle, g):
             assert int(got[i]) == oracle.crc64ecma(datagen.stream_bytes(0x640 + nbytes + i, nbytes), 0x1234), i
 
 
-# (shape, v) cases: every streaming shape with every row interleave and with
-# runs of two blocks ("b2"); None = the generic kernel, which has neither.
-STREAM64_CASES = [(shape, v) for shape in [(4, 2), (4, 3), (2, 4), (8, 1), (4, 1), (2, 2), (2, 3)]
-                  for v in [1, 2, 4, "b2"]] + [(None, 1)]
-
-
-@pytest.mark.parametrize("shape,v", STREAM64_CASES)
-@pytest.mark.parametrize("g", [8, 16, 32, 64])
-def test_streaming_shapes(torch_dev, oracle, shape, g, v):
-    # The CRC-64 streaming kernel (uniform batches) in every shape and row
-    # interleave, with seed0, per-buffer seeds and no seed; counts that do not
-    # fill whole wave tuples. v = "b2": runs of two blocks per lane.
-    if shape is None:
-        ck.set_stream64_config(0, 0)  # generic kernel only
-    else:
-        ck.set_stream64_config(*shape)
-        if v == "b2":
-            ck.set_stream64_run_blocks(2)
-        else:
-            ck.set_stream64_interleave(v)
+@pytest.mark.parametrize("g", [4, 8, 16, 32, 64])
+def test_lane_groups_uniform_batches(torch_dev, oracle, g):
+    # The batch kernel at every lane-group size on uniform batches (the shapes
+    # the retired streaming kernel used to take), with seed0, per-buffer seeds
+    # and no seed; counts that do not fill whole wave tuples.
     ck.set_lanes_per_buffer(g)
     try:
         for nbytes, count in ((16 * 64 * 8, 37), (65536, 301), (4096, 1001)):
@@ -130,27 +115,25 @@ def test_streaming_shapes(torch_dev, oracle, shape, g, v):
                 got = out.cpu().numpy().view(np.uint64)
                 for i in list(range(0, count, max(1, count // 25))) + [count - 1]:
                     want = oracle.crc64ecma(datagen.stream_bytes(0x6400 + nbytes + i, nbytes), sd(i))
-                    assert int(got[i]) == want, (shape, g, nbytes, i)
+                    assert int(got[i]) == want, (g, nbytes, i)
     finally:
-        ck.set_stream64_config(0, 0)
-        ck.set_stream64_interleave(1)
-        ck.set_stream64_run_blocks(1)
+        ck.set_lanes_per_buffer(0)
 
 
 def test_full_c2_crc64(torch_dev, oracle):
-    # C2 shape at full size: streaming vs generic kernel agree on all 65,536
-    # CRCs; a sample is checked against the oracle.
+    # C2 shape at full size: two lane-group sizes agree on all 65,536 CRCs; a
+    # sample is checked against the oracle.
     n, cnt = 65536, 65536
     d = torch_dev.empty(n * cnt, dtype=torch_dev.uint8, device="cuda")
     ck.fill_splitmix(d, n, n, cnt, 0x5EED0001)
     a = torch_dev.zeros(cnt, dtype=torch_dev.int64, device="cuda")
     b = torch_dev.zeros(cnt, dtype=torch_dev.int64, device="cuda")
-    ck.batch64_strided(d, n, n, cnt, a)  # default: generic kernel
-    ck.set_stream64_config(4, 3)
+    ck.batch64_strided(d, n, n, cnt, a)  # default: 32 lanes per buffer
+    ck.set_lanes_per_buffer(64)
     try:
         ck.batch64_strided(d, n, n, cnt, b)
     finally:
-        ck.set_stream64_config(0, 0)
+        ck.set_lanes_per_buffer(0)
     torch_dev.cuda.synchronize()
     assert torch_dev.equal(a, b)
     got = a.cpu().numpy().view(np.uint64)

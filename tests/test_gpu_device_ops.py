@@ -167,6 +167,51 @@ def test_extend_device(torch_dev, oracle, nbytes, off):
         assert int(u32(out)[0]) == oracle.crc32c(host, seed), (nbytes, off, seed)
 
 
+def _hip():
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so")
+    h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    h.hipFree.argtypes = [ctypes.c_void_p]
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return h
+
+
+def test_extend_device_null_and_allocation_end(torch_dev, oracle):
+    # the small-buffer kernels used to read a whole 16-byte
+    # block past the data when the block grid was stretched to cover the
+    # seed's 4 (8) bytes: (NULL, 0, seed) loaded address 0, and 0-7 byte
+    # buffers at the very end of an allocation read past it. Now only blocks
+    # that overlap the data are loaded.
+    import ctypes
+    torch = torch_dev
+    out = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out64 = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for seed in (0, 0x9E3779B9):
+        ck.extend_device(0, 0, seed, out)
+        ck.extend64_device(0, 0, out64, seed=seed | (seed << 32))
+        torch.cuda.synchronize()
+        assert int(u32(out)[0]) == seed
+        assert int(out64.cpu().numpy().view(np.uint64)[0]) == seed | (seed << 32)
+    # Buffers ending exactly at the end of a page-multiple hipMalloc block.
+    hip = _hip()
+    size = 1 << 16
+    p = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(p), size) == 0
+    try:
+        host = np.frombuffer(datagen.stream_bytes(0x5EED0E00, size), np.uint8).copy()
+        assert hip.hipMemcpy(p, host.ctypes.data, size, 1) == 0  # hipMemcpyHostToDevice
+        end = p.value + size
+        for n in range(0, 9):
+            for seed in (0, 0xDEADBEEF):
+                ck.extend_device(end - n, n, seed, out)
+                ck.extend64_device(end - n, n, out64, seed=seed)
+                torch.cuda.synchronize()
+                assert int(u32(out)[0]) == oracle.crc32c(host[size - n:], seed), (n, seed)
+                assert int(out64.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(host[size - n:], seed), (n, seed)
+    finally:
+        hip.hipFree(p)
+
+
 def test_extend_device_1gib(torch_dev):
     # Size-independent check at scale: one 1 GiB buffer == combine of its
     # 64 KiB series (both on the device, different kernels and splits).

@@ -13,10 +13,14 @@ count the held-back segment stores are built around); C4 shard: 1 per task,
 
 Reference shapes: common/checksum/test/test_checksum.cpp:231-266 (properties),
 rpc/serialize.h:244-251 (Crc32Hasher: chained crc32c_extend per message)."""
+import os
+
 import numpy as np
 import pytest
 
 from photonlibos_amd import checksum as ck
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -73,17 +77,25 @@ def test_full_strided_every_crc(torch_dev, oracle, cfg):
 
 
 def test_full_c3_crc64_every_crc(torch_dev, oracle):
-    # CRC-64/ECMA (row f2) on the C3 shape at full size (crc64<8> kernel).
+    # CRC-64/ECMA (row f2) on the C3 shape at full size: the product's
+    # 16-lane path (crc64_batch_kernel<16>, 4-8 KiB buffers) and the 8-lane
+    # one (lanes override), every CRC of both against the oracle.
     torch = torch_dev
     nbytes, count = 4096, 1 << 20
     d = torch.empty(nbytes * count, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, nbytes, nbytes, count, SEED_BASE)
-    out = torch.zeros(count, dtype=torch.int64, device="cuda")
-    ck.batch64_strided(d, nbytes, nbytes, count, out)
-    torch.cuda.synchronize()
-    got = out.cpu().numpy().view(np.uint64)
     want = oracle.crc64ecma_strided(d.cpu().numpy(), nbytes, nbytes, count)
-    assert _first_mismatch(got, want) is None, _first_mismatch(got, want)
+    assert ck.lanes_for(nbytes) in (8, 16)
+    for lanes in (0, 8):
+        ck.set_lanes_per_buffer(lanes)
+        try:
+            out = torch.zeros(count, dtype=torch.int64, device="cuda")
+            ck.batch64_strided(d, nbytes, nbytes, count, out)
+            torch.cuda.synchronize()
+        finally:
+            ck.set_lanes_per_buffer(0)
+        got = out.cpu().numpy().view(np.uint64)
+        assert _first_mismatch(got, want) is None, (lanes, _first_mismatch(got, want))
 
 
 def test_full_c5_every_segment_and_message(torch_dev, oracle):
@@ -345,55 +357,90 @@ def test_extend_device_thousand_back_to_back_launches(torch_dev, oracle):
 
 
 def test_extend_device_graph_capture(torch_dev, oracle):
-    """a call launching more than one workgroup (a block span over
-    4 KiB) is refused (-ENOTSUP) while its stream is captured into a HIP graph
-    (its reduce state is per stream); a one-workgroup call captures and
-    replays exactly; the stream runs long calls again after the capture."""
+    """every extend_device call captures into a HIP graph -- a
+    one-workgroup call, a multi-workgroup small-kernel call (128 KiB) and a
+    full-grid long-kernel call (1 MiB) -- each multi-workgroup launch with a
+    reduce state owned by the graph (reset mode), so the graph replays exactly
+    any number of times over new data; the stream runs long calls on its own
+    state again after the capture, and destroying the graph hands the states
+    back for the next capture."""
     torch = torch_dev
     d = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0C00)
-    out = torch.zeros(3, dtype=torch.int32, device="cuda")
-    ck.extend_device(d.data_ptr() + 3, 3000, 9, out[0:1])  # the device's table image exists before capture
+    spans = ((3, 3000), (3, 128 << 10), (3, (1 << 20) - 64))
+    for rep in range(2):  # the second capture reuses the states the first graph handed back
+        out = torch.zeros(3, dtype=torch.int32, device="cuda")
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            st = torch.cuda.current_stream()
+            for k, (off, n) in enumerate(spans):
+                ck.extend_device(d.data_ptr() + off, n, 9 + k, out[k:k + 1], stream=st)
+        for seed_fill in (0x5EED0C01, 0x5EED0C02, 0x5EED0C01):  # new data, same graph, replayed thrice
+            ck.fill_splitmix(d, d.numel(), d.numel(), 1, seed_fill + rep)
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            host = d.cpu().numpy()
+            for k, (off, n) in enumerate(spans):
+                assert int(_u32(out)[k]) == oracle.crc32c(host[off:off + n], 9 + k), (rep, k)
+        del g
+    out = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    refused = []
-    with torch.cuda.graph(g):
-        st = torch.cuda.current_stream()
-        ck.extend_device(d.data_ptr() + 3, 3000, 9, out[0:1], stream=st)
-        for k, n in ((1, 128 << 10), (2, (1 << 20) - 64)):
-            try:
-                ck.extend_device(d.data_ptr() + 3, n, 9, out[k:k + 1], stream=st)
-            except ck.CrcError as e:
-                refused.append(e.code)
-    assert refused == [-95, -95]  # ENOTSUP
-    for seed_fill in (0x5EED0C01, 0x5EED0C02):  # new data, same graph
-        ck.fill_splitmix(d, d.numel(), d.numel(), 1, seed_fill)
-        torch.cuda.synchronize()
-        g.replay()
-        torch.cuda.synchronize()
-        assert int(_u32(out)[0]) == oracle.crc32c(d.cpu().numpy()[3:3 + 3000], 9)
-    ck.extend_device(d.data_ptr() + 3, (1 << 20) - 64, 9, out[2:3])
-    torch.cuda.synchronize()
-    assert int(_u32(out)[2]) == oracle.crc32c(d.cpu().numpy()[3:3 + (1 << 20) - 64], 9)
-    # CRC-64 (crc64_small_kernel): the same rule
-    out64 = torch.zeros(2, dtype=torch.int64, device="cuda")
-    ck.extend64_device(d.data_ptr() + 5, 4000, out64[0:1], seed=11)  # its table image exists before capture
-    torch.cuda.synchronize()
+    assert int(_u32(out)[0]) == oracle.crc32c(d.cpu().numpy()[3:3 + (1 << 20) - 64], 9)
+    # CRC-64 (crc64_small_kernel and crc64_long_kernel): the same rule
+    out64 = torch.zeros(3, dtype=torch.int64, device="cuda")
     g64 = torch.cuda.CUDAGraph()
-    refused = []
     with torch.cuda.graph(g64):
         st = torch.cuda.current_stream()
-        ck.extend64_device(d.data_ptr() + 5, 4000, out64[0:1], seed=11, stream=st)
-        try:
-            ck.extend64_device(d.data_ptr() + 5, 64 << 10, out64[1:2], seed=11, stream=st)
-        except ck.CrcError as e:
-            refused.append(e.code)
-    assert refused == [-95]
-    ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0C03)
-    torch.cuda.synchronize()
-    g64.replay()
-    torch.cuda.synchronize()
-    assert int(out64.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(d.cpu().numpy()[5:5 + 4000], 11)
+        for k, (off, n) in enumerate(spans):
+            ck.extend64_device(d.data_ptr() + off + 2, n, out64[k:k + 1], seed=11 + k, stream=st)
+    for seed_fill in (0x5EED0C03, 0x5EED0C04):
+        ck.fill_splitmix(d, d.numel(), d.numel(), 1, seed_fill)
+        torch.cuda.synchronize()
+        g64.replay()
+        torch.cuda.synchronize()
+        host = d.cpu().numpy()
+        got = out64.cpu().numpy().view(np.uint64)
+        for k, (off, n) in enumerate(spans):
+            assert int(got[k]) == oracle.crc64ecma(host[off + 2:off + 2 + n], 11 + k), k
+
+
+def test_first_small_call_inside_capture(torch_dev):
+    """the small kernels' table images are built lazily on
+    a device's first small call; when that first call is made while the
+    caller's stream is being captured, the build runs in relaxed capture mode
+    and the capture stays valid. Needs a fresh process (the images are per
+    process)."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %r)
+from photonlibos_amd import checksum as ck
+from tests import _oracle as oracle
+d = torch.empty(1 << 18, dtype=torch.uint8, device="cuda")
+ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0D00)
+out = torch.zeros(2, dtype=torch.int32, device="cuda")
+out64 = torch.zeros(1, dtype=torch.int64, device="cuda")
+torch.cuda.synchronize()
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    st = torch.cuda.current_stream()
+    ck.extend_device(d.data_ptr() + 1, 5000, 3, out[0:1], stream=st)
+    ck.extend_device(d.data_ptr() + 1, 100000, 4, out[1:2], stream=st)
+    ck.extend64_device(d.data_ptr() + 1, 5000, out64, seed=5, stream=st)
+g.replay()
+torch.cuda.synchronize()
+h = d.cpu().numpy()
+got = out.cpu().numpy().view(np.uint32)
+assert int(got[0]) == oracle.crc32c(h[1:5001], 3)
+assert int(got[1]) == oracle.crc32c(h[1:100001], 4)
+assert int(out64.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(h[1:5001], 5)
+print("ok")
+""" % (REPO,)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout[-2000:], r.stderr[-4000:])
 
 
 @pytest.mark.parametrize("shape", [(0, 0), (64, 1), (64, 2), (32, 1), (32, 2), (32, 3)])

@@ -30,18 +30,12 @@ def _reset():
     yield
     ck.set_lanes_per_buffer(0)
     ck.set_generic_rows(-1)
-    ck.set_stream_config(0, 0, 0)
     ck.set_msg_mode(0)
     ck.set_msg_rows(2)
-    ck.set_stream64_run_blocks(1)
-    ck.set_stream64_interleave(1)
-    ck.set_stream64_config(0, 0)
 
 
-ENGINES = [  # (lanes, generic rows, streaming shape)
-    (0, 4, None), (4, 4, None), (8, 2, None), (16, 8, None), (32, 4, None), (64, 4, None),
-    (0, 0, None), (8, 0, None), (64, 0, None),           # fused kernel
-    (8, 4, (1, 4, 3)), (32, 4, (2, 2, 3)),               # streaming kernel (uniform batches only)
+ENGINES = [  # (lanes, generic rows): every lane-group size, every rows-per-step shape
+    (0, -1), (0, 4), (4, 4), (8, 2), (16, 8), (16, 2), (32, 4), (64, 4), (64, 8),
 ]
 
 
@@ -58,10 +52,9 @@ def _lengths(rnd, k):
 def test_fuzz_iov_batches(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(1000 + round_)
-    for lanes, rows, stream in ENGINES:
+    for lanes, rows in ENGINES:
         ck.set_lanes_per_buffer(lanes)
         ck.set_generic_rows(rows)
-        ck.set_stream_config(*(stream or (0, 0, 0)))
         lens = _lengths(rnd, 120)
         offs = [rnd.randrange(0, POOL - n) for n in lens]
         seeds = [rnd.getrandbits(32) if rnd.random() < 0.7 else 0 for _ in lens]
@@ -75,17 +68,16 @@ def test_fuzz_iov_batches(dev_pool, oracle, round_):
         torch.cuda.synchronize()
         got = out.cpu().numpy().view(np.uint32)
         for k, (o, n, s) in enumerate(zip(offs, lens, seeds)):
-            assert got[k] == oracle.crc32c(host[o:o + n], s), (lanes, rows, stream, o, n, s)
+            assert got[k] == oracle.crc32c(host[o:o + n], s), (lanes, rows, o, n, s)
 
 
 @pytest.mark.parametrize("round_", range(3 * SOAK))
 def test_fuzz_strided_batches(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(2000 + round_)
-    for lanes, rows, stream in ENGINES:
+    for lanes, rows in ENGINES:
         ck.set_lanes_per_buffer(lanes)
         ck.set_generic_rows(rows)
-        ck.set_stream_config(*(stream or (0, 0, 0)))
         aligned = rnd.random() < 0.5
         nbytes = rnd.choice([4096, 8192, 65536, 16 * 64 * 4]) if aligned else rnd.randrange(1, 70000)
         stride = nbytes if aligned else nbytes + rnd.randrange(0, 64)
@@ -98,7 +90,7 @@ def test_fuzz_strided_batches(dev_pool, oracle, round_):
         got = out.cpu().numpy().view(np.uint32)
         for i in range(count):
             o = base + i * stride
-            assert got[i] == oracle.crc32c(host[o:o + nbytes], seed0), (lanes, rows, stream, nbytes, stride, i)
+            assert got[i] == oracle.crc32c(host[o:o + nbytes], seed0), (lanes, rows, nbytes, stride, i)
 
 
 @pytest.mark.parametrize("round_", range(3 * SOAK))
@@ -200,21 +192,15 @@ def test_fuzz_crc64(dev_pool, oracle, round_):
             assert int(got[k]) == oracle.crc64ecma(host[o:o + n], s), (lanes, o, n)
 
 
-SHAPES64 = [  # (lanes, run blocks, interleave, (U, D)); (0, 0) = streaming kernel off
-    (0, 1, 1, (4, 3)), (8, 1, 1, (4, 1)), (16, 2, 1, (4, 3)), (32, 2, 1, (2, 2)), (32, 1, 2, (4, 3)),
-    (16, 1, 4, (4, 2)), (64, 1, 1, (8, 1)), (8, 1, 1, (0, 0)), (64, 1, 1, (0, 0)),
-]
+LANES64 = [0, 4, 8, 16, 32, 64]  # lanes per buffer of the CRC-64 batch kernel (0 = automatic)
 
 
 @pytest.mark.parametrize("round_", range(3 * SOAK))
 def test_fuzz_crc64_strided(dev_pool, oracle, round_):
     torch, host, d = dev_pool
     rnd = random.Random(5000 + round_)
-    for lanes, b, v, (u, dd) in SHAPES64:
+    for lanes in LANES64:
         ck.set_lanes_per_buffer(lanes)
-        ck.set_stream64_run_blocks(b)
-        ck.set_stream64_interleave(v)
-        ck.set_stream64_config(u, dd)
         aligned = rnd.random() < 0.6
         nbytes = rnd.choice([4096, 8192, 65536, 16 * 64 * 8]) if aligned else rnd.randrange(1, 70000)
         stride = nbytes if aligned else nbytes + rnd.randrange(0, 64)
@@ -230,7 +216,7 @@ def test_fuzz_crc64_strided(dev_pool, oracle, round_):
         for i in range(count):
             o = base + i * stride
             want = oracle.crc64ecma(host[o:o + nbytes], seeds[i] if seeds else seed0)
-            assert int(got[i]) == want, (lanes, b, v, u, dd, nbytes, stride, i)
+            assert int(got[i]) == want, (lanes, nbytes, stride, i)
 
 
 def _chain64(oracle, parts, seed):

@@ -29,7 +29,6 @@ def torch_dev():
 def _reset_lanes():
     yield
     ck.set_lanes_per_buffer(0)
-    ck.set_stream_config(0, 0, 0)
     ck.set_generic_rows(-1)
     ck.set_msg_mode(0)
 
@@ -39,13 +38,10 @@ def _reset_lanes():
 MSG_MODES = [0, 1, 2]
 
 
-# Batch kernel variants: 4 = the generic kernel (default), 0 = the fused
-# 4-row kernel (a tuning option).
-VARIANTS = [-1, 2, 4, 0]  # rows per step: auto (the product default), 2, 4, fused kernel
-
-
-STREAM_SHAPES = [(2, 2, 3), (1, 4, 3), (4, 1, 3), (2, 2, 4), (4, 1, 4), (1, 2, 4), (1, 4, 1), (1, 4, 2), (1, 2, 2),
-                 (1, 2, 3), (1, 8, 1), (1, 8, 2), (1, 6, 2), (1, 4, 4), (0, 0, 0)]
+# Batch kernel variants: rows per step of the generic kernel (-1 = by
+# lane-group size, the product default). The fused and streaming kernels of
+# earlier rounds are bench-only probes now (stream_kernels.h).
+VARIANTS = [-1, 2, 4, 8]
 
 
 def to_dev(torch, arr):
@@ -150,22 +146,6 @@ def test_strided_all_lane_groups(torch_dev, oracle, g, nbytes, stride, variant):
         assert list(got) == want, (g, nbytes, stride, base_off)
 
 
-@pytest.mark.parametrize("shape", STREAM_SHAPES)
-@pytest.mark.parametrize("g", [8, 16, 32, 64])
-def test_stream_shapes(torch_dev, oracle, shape, g):
-    # Every streaming-kernel shape (and the generic kernel, shape 0) on uniform
-    # batches whose buffer count does not fill whole tuples or ring turns.
-    ck.set_stream_config(*shape)
-    ck.set_lanes_per_buffer(g)
-    for nbytes, count in ((16 * 4 * 64 * 4, 37), (65536, 300), (4096, 1001)):
-        d = torch_dev.empty(nbytes * count, dtype=torch_dev.uint8, device="cuda")
-        ck.fill_splitmix(d, nbytes, nbytes, count, 0x77 + nbytes)
-        got = run_strided(torch_dev, d, nbytes, nbytes, count, seeds=[(7 * i) & 0xFFFFFFFF for i in range(count)])
-        for i in list(range(0, count, max(1, count // 40))) + [count - 1]:
-            want = oracle.crc32c(datagen.stream_bytes(0x77 + nbytes + i, nbytes), (7 * i) & 0xFFFFFFFF)
-            assert got[i] == want, (shape, g, nbytes, i)
-
-
 def test_device_fill_matches_datagen(torch_dev):
     d = torch_dev.zeros(5 * 1000 + 3, dtype=torch_dev.uint8, device="cuda")
     ck.fill_splitmix(d, 1000, 997, 5, 0xABC)
@@ -197,10 +177,9 @@ def test_full_c2_4gib(torch_dev, oracle):
     ck.set_lanes_per_buffer(16)
     b = run_strided(torch_dev, d, nbytes, nbytes, count)
     ck.set_lanes_per_buffer(0)
-    ck.set_stream_config(1, 4, 3)  # the streaming kernel
+    ck.set_generic_rows(2)  # another rows-per-step shape
     c = run_strided(torch_dev, d, nbytes, nbytes, count)
-    ck.set_stream_config(0, 0, 0)
-    ck.set_generic_rows(0)  # the fused kernel
+    ck.set_generic_rows(8)
     e = run_strided(torch_dev, d, nbytes, nbytes, count)
     ck.set_generic_rows(-1)
     assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, e)
