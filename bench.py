@@ -9,7 +9,10 @@ One "step" = one pass of the hot path over one batch (BASELINE.json configs):
       device-resident, per GPU (weak scaling: N GPUs checksum N such batches,
       so the driver's 1/2/4/8-GPU lines compare like with like)
   c4 (configs[3]): 32,768 x 1 MiB per GPU = the 256 Ki x 1 MiB batch sharded
-      over 8 GPUs (`--config c4 --gpus 8`)
+      over 8 GPUs (`--config c4 --gpus 8`); with --gpus N > 1 the C2 line
+      also carries a `config_c4` sub-record: the same ranks time the C4 shard
+      right after the C2 leg (so the driver's one 8-GPU run measures
+      configs[3] too; `value` stays C2's)
   c3: 1,048,576 x 4 KiB        c5: 65,536 messages x 8 non-contiguous 8 KiB
       segments, per-segment CRC + crc32c_combine fold (BASELINE.json configs[4])
   c5_chain: the C5 shape, one CRC per message chained through the seed
@@ -99,6 +102,8 @@ def parse(argv=None):
     ap.add_argument("--no-live-pmc", action="store_true",
                     help="do not run the rocprofv3 FETCH_SIZE child pass; read profiles/pmc_<config>.json instead")
     ap.add_argument("--no-shape64", action="store_true", help="skip the one-wavefront-per-buffer (G=64) side line")
+    ap.add_argument("--no-c4-leg", action="store_true",
+                    help="with --gpus N > 1: skip the C4 (BASELINE configs[3]) leg timed after the C2 line")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (profiles/*.json) giving HBM bytes per launch (fallback when no live pass)")
@@ -689,6 +694,51 @@ def run_file_records(args):
                       "config": {"workload": "1 GiB file, 262144 x 4 KiB records"}}))
 
 
+def event_marks(stream):
+    """timed_region's on_step: one HIP event per launch boundary on the launch
+    stream (see main)."""
+    bounds = {}
+
+    def on_step(s, step):
+        if s == 0:
+            bounds.clear()
+        if s not in bounds:
+            bounds[s] = torch.cuda.Event(enable_timing=True)
+            bounds[s].record(stream)
+        step()
+        bounds[s + 1] = torch.cuda.Event(enable_timing=True)
+        bounds[s + 1].record(stream)
+        a, b = bounds[s], bounds[s + 1]
+        return lambda: a.elapsed_time(b)
+    return on_step
+
+
+def c4_leg(args, rank, world, device, stream, dist):
+    """BASELINE configs[3] in the same ranks after the C2 leg:
+    every rank checksums its 32 Ki x 1 MiB shard of the 256 Ki x 1 MiB batch
+    (global ids r*32768.., no collective), timed like the C2 leg (barrier +
+    sync both sides, max over ranks). At N = 8 this is the whole configs[3]
+    batch; at N < 8, N/8 of it."""
+    cfg = CONFIGS["c4"]
+    wl = Workload(cfg, rank, stream)
+    elapsed, kernel_ms, local_el, local_ms = timed_region(wl.step, args.steps, args.warmup, torch.cuda.synchronize,
+                                                          dist, event_marks(stream))
+    ok = wl.self_check()
+    ranks = gather_ranks(dist, {"rank": rank, "device": device, "wall_s": round(local_el, 6),
+                                "launch_ms": launch_summary(local_ms), "self_check": ok})
+    per_launch = wl.bytes_per_step / (kernel_ms * 1e-3) / 1e9
+    rec = {"workload": cfg["workload"], "config": "c4", "buffers_total": cfg["count"] * world,
+           "buffer_bytes": cfg["nbytes"],
+           "value": round(aggregate_gibps(wl.bytes_per_step, args.steps, world, elapsed), 3), "unit": "GiB/s",
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+           "frac": round(per_launch / HBM_PEAK_GBPS, 4),
+           "frac_wall": round(wl.bytes_per_step * args.steps * world / elapsed / 1e9 / (HBM_PEAK_GBPS * world), 4),
+           "per_rank": ranks, "self_check": all(r["self_check"] for r in ranks)}
+    del wl
+    torch.cuda.empty_cache()
+    return rec
+
+
 # ------------------------------------------------------------- CPU rehearsal
 
 def run_cpu_rehearsal(args, rank, world, dist):
@@ -715,6 +765,24 @@ def run_cpu_rehearsal(args, rank, world, dist):
     elapsed, _, local_el, local_ms = timed_region(step, args.steps, args.warmup, lambda: None, dist, on_step)
     ranks = gather_ranks(dist, {"rank": rank, "wall_s": round(local_el, 6), "first_crc": int(out[0]),
                                 "launch_ms": launch_summary(local_ms)})
+    c4 = None
+    if world > 1 and args.config == "c2" and not args.no_c4_leg:
+        # the C4 leg's host stand-in: 4 x 1 MiB per rank (global ids as the C4 shard's)
+        n4, cnt4 = 1 << 20, 4
+        bufs4 = [datagen.stream_bytes(shard_seed_base(rank, CONFIGS["c4"]["count"]) + i, n4).tobytes()
+                 for i in range(cnt4)]
+        out4 = [0] * cnt4
+
+        def step4():
+            for i, b in enumerate(bufs4):
+                out4[i] = ck.crc32c(b)
+        el4, _, lel4, lms4 = timed_region(step4, args.steps, args.warmup, lambda: None, dist, on_step)
+        r4 = gather_ranks(dist, {"rank": rank, "wall_s": round(lel4, 6), "first_crc": int(out4[0]),
+                                 "launch_ms": launch_summary(lms4)})
+        c4 = {"workload": CONFIGS["c4"]["workload"], "config": "c4", "buffers_total": CONFIGS["c4"]["count"] * world,
+              "value": round(aggregate_gibps(n4 * cnt4, args.steps, world, el4), 3), "unit": "GiB/s",
+              "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el4 / args.steps * 1e3, 4),
+              "per_rank": r4, "rehearsal_step": f"{cnt4} x {n4} B host buffers per rank, crc32c() drop-in"}
     if rank == 0:
         print(json.dumps({"metric": "GiB/s CRC32C host rehearsal of the N-rank bench path (no GPU)",
                           "value": round(aggregate_gibps(n * cnt, args.steps, world, elapsed), 3), "unit": "GiB/s",
@@ -723,7 +791,8 @@ def run_cpu_rehearsal(args, rank, world, dist):
                           "rehearsal": "cpu", "per_rank": ranks,
                           "rehearsal_step": f"{cnt} x {n} B host buffers per rank, crc32c() drop-in",
                           "config": {"workload": CONFIGS[args.config]["workload"], "config": args.config,
-                                     "parallelism": f"shard-per-gpu x{world}"}}), flush=True)
+                                     "parallelism": f"shard-per-gpu x{world}"},
+                          **({"config_c4": c4} if c4 else {})}), flush=True)
 
 
 # ----------------------------------------------------------------------- main
@@ -782,19 +851,7 @@ def main(argv=None):
     # wall clock ~1.3 % over the kernels' own time (r04a: 0.6441 ms per step
     # against a 0.636 ms mean launch). A launch's time is boundary to
     # boundary, so it includes the gap before the next launch.
-    bounds = {}
-
-    def on_step(s, step):
-        if s == 0:
-            bounds.clear()
-        if s not in bounds:
-            bounds[s] = torch.cuda.Event(enable_timing=True)
-            bounds[s].record(stream)
-        step()
-        bounds[s + 1] = torch.cuda.Event(enable_timing=True)
-        bounds[s + 1].record(stream)
-        a, b = bounds[s], bounds[s + 1]
-        return lambda: a.elapsed_time(b)
+    on_step = event_marks(stream)
 
     if args.pmc_child:  # the workload's launches under rocprofv3 --pmc (live_traffic)
         for _ in range(args.warmup + args.steps):
@@ -804,6 +861,7 @@ def main(argv=None):
     elapsed, kernel_ms, local_el, local_ms = timed_region(wl.step, args.steps, args.warmup, torch.cuda.synchronize,
                                                           dist, on_step)
     ok = wl.self_check()  # the last timed step's results, checked after the timed region
+    bytes_step = wl.bytes_per_step
     value = aggregate_gibps(wl.bytes_per_step, args.steps, world, elapsed)
     per_launch_gbps = wl.bytes_per_step / (kernel_ms * 1e-3) / 1e9
     ls = launch_summary(local_ms)
@@ -822,6 +880,13 @@ def main(argv=None):
                    "kernel_ms_median": round(float(np.median(l64)), 4),
                    "frac": round(wl.bytes_per_step / (ms64 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
+    c4 = None
+    if world > 1 and args.config == "c2" and not args.no_c4_leg:
+        del wl
+        torch.cuda.empty_cache()
+        c4 = c4_leg(args, rank, world, device, stream, dist)
+        all_ok = all_ok and c4["self_check"]
+
     traffic, traffic_src = None, None
     if rank == 0 and world == 1 and not args.no_live_pmc:
         lt = live_traffic(args.config)
@@ -833,7 +898,7 @@ def main(argv=None):
                        "FETCH_SIZE pass of this config on one GPU)") if traffic else None
 
     if rank == 0:
-        steady = wl.bytes_per_step / (float(np.median([r["launch_ms"]["median"] for r in ranks])) * 1e-3) / 1e9
+        steady = bytes_step / (float(np.median([r["launch_ms"]["median"] for r in ranks])) * 1e-3) / 1e9
         res = {
             "metric": METRIC.replace("CRC32C", "CRC-64/ECMA") if cfg["kind"] == "strided64" else METRIC,
             "value": round(value, 3),
@@ -849,14 +914,14 @@ def main(argv=None):
             "data": "synthetic (splitmix64 random bytes generated on device)",
             "config": {"workload": cfg["workload"], "config": args.config, "buffers": cfg["count"],
                        "buffer_bytes": cfg["nbytes"],
-                       "bytes_per_gpu_per_step": wl.bytes_per_step, "parallelism": f"shard-per-gpu x{world}",
+                       "bytes_per_gpu_per_step": bytes_step, "parallelism": f"shard-per-gpu x{world}",
                        "lanes_per_buffer": args.lanes or "auto"},
             "roofline": {"bound": "hbm", "achieved": round(per_launch_gbps, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(per_launch_gbps / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes": wl.bytes_per_step,
+                         "algorithmic_bytes": bytes_step,
                          "frac_kernel": round(per_launch_gbps / HBM_PEAK_GBPS, 4),
-                         "frac_wall": round(wl.bytes_per_step * args.steps * world / elapsed / 1e9
+                         "frac_wall": round(bytes_step * args.steps * world / elapsed / 1e9
                                             / (HBM_PEAK_GBPS * world), 4),
                          "frac_steady_median_launch": round(steady / HBM_PEAK_GBPS, 4),
                          "clock_note": "frac/frac_kernel: mean launch time between HIP events at the launch "
@@ -870,6 +935,8 @@ def main(argv=None):
             res["rehearsal"] = f"{world} ranks sharing {visible} visible GPU(s): not a scaling measurement"
         if shape64:
             res["north_star_shape_g64"] = shape64
+        if c4:
+            res["config_c4"] = c4
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             res["cpu_reference_c1"] = cpu_reference_c1(min(2.0, args.cpu_seconds))

@@ -99,9 +99,10 @@ typedef struct photon_crc_msg_batch photon_crc_msg_batch;
 #define PHOTON_CRC_BATCH_DETACHED_BODY 4u /* bodies are separate buffers: hash payload, then body */
 
 /* A batch on the current device with room for max_messages messages and
- * max_segments segments in total (a DETACHED_BODY body counts as one
- * segment, a message-object body as two: the zero word standing for
- * m_checksum and the rest of the object). NULL on error. */
+ * max_segments segments in total: every iovec entry and every body counts
+ * as one (a message-object body is hashed internally as two pieces, the zero
+ * word standing for m_checksum and the rest of the object; the batch
+ * reserves the extra piece itself). NULL on error. */
 photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_t max_segments, uint32_t flags);
 void photon_crc_msg_batch_destroy(photon_crc_msg_batch* b);
 

@@ -55,6 +55,15 @@ int photon_crc_set_msg_rows(int rows_per_step);
  * from 3 GiB. */
 int photon_crc_set_long_shape(int lanes, int rounds);
 
+/* Routed drop-in calls (photon_crc_set_device_dispatch) collect their result
+ * by polling tagged words in pinned memory for at most `spin_us` microseconds
+ * (default 30, with a pause between reads), then sleep in the driver until
+ * the kernel has finished (a blocking-sync event); with sleep_ahead != 0 (the
+ * default) a call whose bytes at a nominal 6 GB/ms would take longer than
+ * the window first sleeps through all but the window. spin_us = 0: no
+ * polling at all. */
+int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
+
 /* Lanes per buffer the engine picks for buffers of typical length n (the
  * lane-group table of DESIGN.md §4, or the override when one is set). */
 int photon_crc_lanes_for(uint64_t nbytes);

@@ -176,6 +176,7 @@ struct photon_crc_msg_batch {
     uint32_t* d_zero = nullptr;
     hipEvent_t done_ev = nullptr;
     uint64_t nmsg = 0, nseg = 0;
+    uint64_t nseg_caller = 0;  // segments as the caller counts them (a body = one), against max_seg
     uint64_t host_bytes = 0, total_bytes = 0;  // payload in host memory / all (lane choice)
     bool submitted = false;
     std::atomic<bool> completed{false};    // results on the host and counted
@@ -333,7 +334,10 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
     b->max_msg = max_messages;
     b->max_seg = max_segments;
     hipError_t e = hipGetDevice(&b->dev);
-    const uint64_t M = max_messages, S = max_segments;
+    // Descriptor slots: the caller's segments plus, per message, the zero word
+    // an object body is hashed with (max_segments keeps its
+    // meaning, one segment per body).
+    const uint64_t M = max_messages, S = (uint64_t)max_segments + max_messages;
     b->zero_copy = !(flags & PHOTON_CRC_BATCH_STAGED);
     auto hm = [&](void** p, uint64_t n) {
         if (e == hipSuccess) e = hipHostMalloc(p, n, hipHostMallocMapped | hipHostMallocPortable);
@@ -391,8 +395,11 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
     // the word masked again on every resubmit of refilled bodies.
     const bool object_body = has_body && !(b->flags & PHOTON_CRC_BATCH_DETACHED_BODY);
     if (object_body && body_length < 4) return report_error(-EINVAL, "message body shorter than its m_checksum");
-    const uint32_t nput = object_body ? (body_length > 4 ? 2u : 1u) : iovcnt + (has_body ? 1 : 0);
-    if (b->nmsg >= b->max_msg || b->nseg + nput > b->max_seg) return report_error(-ENOSPC, "batch is full");
+    // The caller's count: one segment for an object body (its payload does
+    // not enter the CRC), else the iovector plus the body; the zero word of an
+    // object body takes one of the max_messages extra descriptor slots.
+    const uint64_t nput = object_body ? 1u : (uint64_t)iovcnt + (has_body ? 1u : 0u);
+    if (b->nmsg >= b->max_msg || b->nseg_caller + nput > b->max_seg) return report_error(-ENOSPC, "batch is full");
     const bool trusted = b->flags & PHOTON_CRC_BATCH_TRUSTED;
     uint64_t s = b->nseg;
     uint64_t host = 0, total = 0;
@@ -426,6 +433,7 @@ int64_t photon_crc_msg_batch_add(photon_crc_msg_batch* b, const photon_crc_iovec
         }
     }
     b->nseg = s;
+    b->nseg_caller += nput;
     b->host_bytes += host;
     b->total_bytes += total;
     b->h_expect[b->nmsg] = expected;
@@ -510,7 +518,7 @@ int photon_crc_msg_batch_reset(photon_crc_msg_batch* b) {
         int64_t rc = finish(b);
         if (rc < 0) return (int)rc;
     }
-    b->nmsg = b->nseg = 0;
+    b->nmsg = b->nseg = b->nseg_caller = 0;
     b->host_bytes = b->total_bytes = 0;
     b->submitted = false;
     b->completed.store(false, std::memory_order_relaxed);

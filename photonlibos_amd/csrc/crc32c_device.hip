@@ -54,6 +54,7 @@
 #include "crc32c_kernels.h"
 #include "crc64_kernels.h"
 #include "long_plan.h"
+#include "multi_device.h"
 #include "gf2.h"
 #include "internal.h"
 
@@ -83,6 +84,8 @@ std::atomic<int> g_generic_u{-1};
 // while strided batches keep 4 (C2 -6, C3 -1.2, C4 -0.9 with 2).
 std::atomic<int> g_msg_u{2};
 std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
+// Routed drop-in calls: spin window in µs | sleep-ahead << 16 (wait_tagged).
+std::atomic<uint32_t> g_routed_wait{30u | 1u << 16};
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -92,6 +95,18 @@ int fail(int code, const std::string& what) {
 int hip_fail(hipError_t e, const char* what) {
     return fail(-EIO, std::string(what) + ": " + hipGetErrorString(e));
 }
+
+// The device runtime of multi_device.h.
+struct HipRT {
+    int get(int* dev) {
+        const hipError_t e = hipGetDevice(dev);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipGetDevice");
+    }
+    int set(int dev) {
+        const hipError_t e = hipSetDevice(dev);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipSetDevice");
+    }
+};
 
 struct DeviceInfo {
     bool probed = false;
@@ -698,8 +713,7 @@ int long_launch(hipStream_t st, uint64_t grid, const char* what, L launch) {
 // buffer"): its LDS tables and basis words, computed on the host with gf2.h
 // and copied to each device once, on that device's first small call (a
 // private non-blocking stream, so no other stream is synchronised).
-std::mutex g_img_mu;
-std::vector<uint32_t*> g_img;
+PerDevice<uint32_t*> g_img;
 
 std::vector<uint32_t> small_image_host() {
     std::vector<uint32_t> img(kSmImage / 4, 0u);
@@ -717,29 +731,39 @@ std::vector<uint32_t> small_image_host() {
     return img;
 }
 
-int small_image(int dev, const uint32_t** out) {
-    std::lock_guard<std::mutex> lk(g_img_mu);
-    if ((int)g_img.size() <= dev) g_img.resize(dev + 1, nullptr);
-    if (!g_img[dev]) {
-        static const std::vector<uint32_t> host = small_image_host();
-        void* d = nullptr;
-        const hipError_t e = relaxed_capture([&] {  // legal during a caller's graph capture
-            hipStream_t s = nullptr;
-            hipError_t r = hipMalloc(&d, kSmImage);
-            if (r == hipSuccess) r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-            if (r == hipSuccess) r = hipMemcpyAsync(d, host.data(), kSmImage, hipMemcpyHostToDevice, s);
-            if (r == hipSuccess) r = hipStreamSynchronize(s);
-            if (s) (void)hipStreamDestroy(s);
-            return r;
-        });
-        if (e != hipSuccess) {
-            if (d) (void)hipFree(d);
-            return hip_fail(e, "small-buffer table image");
-        }
-        g_img[dev] = static_cast<uint32_t*>(d);
+
+
+// Copy `bytes` of host words to a new device buffer of the current device.
+template <typename T>
+int upload_image(const std::vector<T>& host, uint64_t bytes, T** out, const char* what) {
+    void* d = nullptr;
+    const hipError_t e = relaxed_capture([&] {  // legal during a caller's graph capture
+        hipStream_t s = nullptr;
+        hipError_t r = hipMalloc(&d, bytes);
+        if (r == hipSuccess) r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (r == hipSuccess) r = hipMemcpyAsync(d, host.data(), bytes, hipMemcpyHostToDevice, s);
+        if (r == hipSuccess) r = hipStreamSynchronize(s);
+        if (s) (void)hipStreamDestroy(s);
+        return r;
+    });
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        return hip_fail(e, what);
     }
-    *out = g_img[dev];
+    *out = static_cast<T*>(d);
     return 0;
+}
+
+// The image of device `dev` (the caller's current device: multi-device paths
+// set it first, multi_device.h).
+int small_image(int dev, const uint32_t** out) {
+    uint32_t* p = nullptr;
+    const int rc = g_img.get(dev, &p, [](int, uint32_t*& slot) {
+        static const std::vector<uint32_t> host = small_image_host();
+        return upload_image(host, kSmImage, &slot, "small-buffer table image");
+    });
+    *out = p;
+    return rc;
 }
 
 // The CRC-64 small kernel's image (crc64_kernels.h crc64_small_kernel), as
@@ -766,31 +790,16 @@ std::vector<uint64_t> small64_image_host() {
     return img;
 }
 
-std::vector<uint64_t*> g_img64;
+PerDevice<uint64_t*> g_img64;
 
 int small64_image(int dev, const uint64_t** out) {
-    std::lock_guard<std::mutex> lk(g_img_mu);
-    if ((int)g_img64.size() <= dev) g_img64.resize(dev + 1, nullptr);
-    if (!g_img64[dev]) {
+    uint64_t* p = nullptr;
+    const int rc = g_img64.get(dev, &p, [](int, uint64_t*& slot) {
         static const std::vector<uint64_t> host = small64_image_host();
-        void* d = nullptr;
-        const hipError_t e = relaxed_capture([&] {  // legal during a caller's graph capture
-            hipStream_t s = nullptr;
-            hipError_t r = hipMalloc(&d, kSm64Image);
-            if (r == hipSuccess) r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-            if (r == hipSuccess) r = hipMemcpyAsync(d, host.data(), kSm64Image, hipMemcpyHostToDevice, s);
-            if (r == hipSuccess) r = hipStreamSynchronize(s);
-            if (s) (void)hipStreamDestroy(s);
-            return r;
-        });
-        if (e != hipSuccess) {
-            if (d) (void)hipFree(d);
-            return hip_fail(e, "CRC-64 small-buffer table image");
-        }
-        g_img64[dev] = static_cast<uint64_t*>(d);
-    }
-    *out = g_img64[dev];
-    return 0;
+        return upload_image(host, kSm64Image, &slot, "CRC-64 small-buffer table image");
+    });
+    *out = p;
+    return rc;
 }
 
 // The CRC-64 small kernel's geometry (as small_args; the grid covers the
@@ -954,6 +963,12 @@ int photon_crc_set_long_shape(int lanes, int rounds) {
     return 0;
 }
 
+int photon_crc_set_routed_wait(int spin_us, int sleep_ahead) {
+    if (spin_us < 0 || spin_us > 65535) return fail(-EINVAL, "spin window must be 0..65535 us");
+    g_routed_wait.store((uint32_t)spin_us | (sleep_ahead ? 1u << 16 : 0u), std::memory_order_relaxed);
+    return 0;
+}
+
 int photon_crc_set_msg_rows(int rows_per_step) {
     if (rows_per_step != 2 && rows_per_step != 4) return fail(-EINVAL, "message rows per step must be 2 or 4");
     g_msg_u.store(rows_per_step, std::memory_order_relaxed);
@@ -1082,61 +1097,54 @@ int photon_crc64ecma_host_batch_strided(const void* h_base, uint64_t stride, uin
                                      &photon_crc64ecma_batch_strided);
 }
 
+// The gfx950 devices of this process, in id order (at most kMaxDevices).
+static int usable_devices(std::vector<int>* devs) {
+    int total = 0;
+    hipError_t e = hipGetDeviceCount(&total);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    devs->clear();
+    for (int d = 0; d < total && d < kMaxDevices; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+            devs->push_back(d);
+    }
+    return devs->empty() ? fail(-ENODEV, "photon_crc: no gfx950 device") : 0;
+}
+
 int photon_crc32c_host_batch_strided_multi(const void* h_base, uint64_t stride, uint64_t nbytes, uint64_t count,
                                            uint32_t seed0, const uint32_t* h_seeds, uint32_t* h_out, int ndev) {
     if (!count) return 0;
     if (!h_out || (!h_base && nbytes) || stride < nbytes) return fail(-EINVAL, "bad arguments");
-    int total = 0;
-    hipError_t e = hipGetDeviceCount(&total);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
-    std::vector<int> devs;
-    for (int d = 0; d < total && d < kMaxDevices; ++d) {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0)
-            devs.push_back(d);
-    }
-    if (devs.empty()) return fail(-ENODEV, "photon_crc: no gfx950 device");
-    if (ndev > 0 && ndev < (int)devs.size()) devs.resize(ndev);
-    const uint64_t nd = devs.size() < count ? devs.size() : count;
-    // Contiguous slices of the buffer indices, one host thread per device, each
-    // driving that device's pipeline over its own host link.
-    std::vector<int> rcs(nd, 0);
-    std::vector<std::string> errs(nd);
-    std::vector<std::thread> th;
+    std::vector<int> usable;
+    if (int rc = usable_devices(&usable)) return rc;
+    // Contiguous slices of the buffer indices (multi_device.h shard_plan), one
+    // host thread per device, each driving that device's pipeline over its own
+    // host link.
+    const std::vector<Slice> plan = shard_plan(count, first_devices(usable, ndev));
     const uint8_t* src = static_cast<const uint8_t*>(h_base);
-    for (uint64_t k = 0; k < nd; ++k) {
-        const uint64_t lo = count * k / nd, hi = count * (k + 1) / nd;
-        th.emplace_back([&, k, lo, hi] {
-            hipError_t se = hipSetDevice(devs[k]);
-            rcs[k] = se != hipSuccess ? hip_fail(se, "hipSetDevice")
-                                      : photon_crc32c_host_batch_strided(src + lo * stride, stride, nbytes, hi - lo,
-                                                                         seed0, h_seeds ? h_seeds + lo : nullptr,
-                                                                         h_out + lo);
-            if (rcs[k]) errs[k] = g_err;
-        });
-    }
-    for (auto& t : th) t.join();
-    for (uint64_t k = 0; k < nd; ++k)
-        if (rcs[k]) return fail(rcs[k], "device " + std::to_string(devs[k]) + ": " + errs[k]);
-    return 0;
+    HipRT rt;
+    std::string err;
+    const int rc = run_slices_threaded(
+        rt, plan,
+        [&](const Slice& sl) {
+            return photon_crc32c_host_batch_strided(src + sl.lo * stride, stride, nbytes, sl.hi - sl.lo, seed0,
+                                                    h_seeds ? h_seeds + sl.lo : nullptr, h_out + sl.lo);
+        },
+        [] { return g_err; }, &err);
+    return rc ? fail(rc, err) : 0;
 }
 
 int photon_crc32c_batch_strided_shards(const photon_crc_shard* shards, int nshards) {
     if (nshards < 0 || (nshards && !shards)) return fail(-EINVAL, "bad shard list");
-    int prev = -1;
-    hipError_t e = hipGetDevice(&prev);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-    int rc = 0;
-    for (int i = 0; i < nshards && !rc; ++i) {
-        const photon_crc_shard& s = shards[i];
-        if ((e = hipSetDevice(s.device)) != hipSuccess) {
-            rc = hip_fail(e, "hipSetDevice");
-            break;
-        }
-        rc = photon_crc32c_batch_strided(s.d_base, s.stride, s.nbytes, s.count, s.seed0, s.d_seeds, s.d_out, s.stream);
-    }
-    (void)hipSetDevice(prev);
-    return rc;
+    HipRT rt;
+    return run_on_devices(
+        rt, nshards, [&](int i) { return shards[i].device; },
+        [&](int i) {
+            const photon_crc_shard& s = shards[i];
+            return photon_crc32c_batch_strided(s.d_base, s.stride, s.nbytes, s.count, s.seed0, s.d_seeds, s.d_out,
+                                               s.stream);
+        },
+        nullptr);
 }
 
 int photon_crc32c_batch_iov(const photon_crc_iovec* d_iov, uint64_t count, uint32_t seed0,
@@ -1525,39 +1533,36 @@ int extend_spans(const photon_crc_span* spans, int nspans, T seed, T* h_result, 
         *h_result = seed;
         return 0;
     }
-    int prev = -1;
-    hipError_t e = hipGetDevice(&prev);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
     std::vector<void*> outs(nspans, nullptr);
     std::vector<T> crcs(nspans, 0);
-    int rc = 0;
+    HipRT rt;
+    // Every span's kernel enqueued on its own device before any wait...
     int issued = 0;
-    for (int i = 0; i < nspans && !rc; ++i, ++issued) {
-        const photon_crc_span& sp = spans[i];
-        if (!sp.d_data && sp.nbytes) {
-            rc = fail(-EINVAL, "null span with bytes");
-            break;
-        }
-        if ((e = hipSetDevice(sp.device)) != hipSuccess) {
-            rc = hip_fail(e, "hipSetDevice");
-            break;
-        }
-        if ((rc = scratch_alloc(&outs[i], sizeof(T), nullptr))) break;
-        rc = launch(sp.d_data, sp.nbytes, static_cast<T*>(outs[i]));
-    }
-    // Collect (and return every lease) even after a failure, each on its device.
-    for (int i = 0; i < issued; ++i) {
-        if (!outs[i]) continue;
-        if ((e = hipSetDevice(spans[i].device)) == hipSuccess) {
-            if (!rc && (e = hipMemcpy(&crcs[i], outs[i], sizeof(T), hipMemcpyDeviceToHost)) != hipSuccess)
-                rc = hip_fail(e, "hipMemcpy(span CRC)");
+    int rc = run_on_devices(
+        rt, nspans, [&](int i) { return spans[i].device; },
+        [&](int i) {
+            const photon_crc_span& sp = spans[i];
+            if (!sp.d_data && sp.nbytes) return fail(-EINVAL, "null span with bytes");
+            if (int r = scratch_alloc(&outs[i], sizeof(T), nullptr)) return r;
+            return launch(sp.d_data, sp.nbytes, static_cast<T*>(outs[i]));
+        },
+        &issued);
+    // ...then collected (and every lease returned, even after a failure), each on its device.
+    int first = 0;  // the first collection error; the loop goes on so that every lease is returned
+    const int set_rc = run_on_devices(
+        rt, issued, [&](int i) { return spans[i].device; },
+        [&](int i) {
+            if (!outs[i]) return 0;
+            if (!rc && !first) {
+                const hipError_t e = hipMemcpy(&crcs[i], outs[i], sizeof(T), hipMemcpyDeviceToHost);
+                if (e != hipSuccess) first = hip_fail(e, "hipMemcpy(span CRC)");
+            }
             const int frc = scratch_free(outs[i], nullptr);
-            if (!rc) rc = frc;
-        } else if (!rc) {
-            rc = hip_fail(e, "hipSetDevice");
-        }
-    }
-    (void)hipSetDevice(prev);
+            if (!first) first = frc;
+            return 0;
+        },
+        nullptr);
+    if (!rc) rc = first ? first : set_rc;
     if (rc) return rc;
     T acc = seed;
     for (int i = 0; i < nspans; ++i) acc = shift(acc, spans[i].nbytes) ^ crcs[i];
@@ -1723,6 +1728,7 @@ struct RoutedStream {
     void* h;  // host address of the result area
     void* d;  // its device address
     uint32_t tag;  // last tag of a spin-waited call (crc32c_small_kernel slots)
+    hipEvent_t done;  // blocking-sync event: the wait after the spin window sleeps in the driver
 };
 std::mutex g_rs_mu;
 std::vector<RoutedStream*> g_rs_free;
@@ -1737,8 +1743,9 @@ int routed_lease(int dev, RoutedStream** out) {
                 return 0;
             }
     }
-    auto* r = new RoutedStream{dev, nullptr, nullptr, nullptr, 0};
+    auto* r = new RoutedStream{dev, nullptr, nullptr, nullptr, 0, nullptr};
     hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->done, hipEventBlockingSync | hipEventDisableTiming);
     // coherent: the small kernel's system-scope tag stores reach the host directly
     if (e == hipSuccess)
         e = hipHostMalloc(&r->h, 512, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
@@ -1746,6 +1753,7 @@ int routed_lease(int dev, RoutedStream** out) {
     if (e == hipSuccess) e = hipHostGetDevicePointer(&r->d, r->h, 0);
     if (e != hipSuccess) {
         if (r->h) (void)hipHostFree(r->h);
+        if (r->done) (void)hipEventDestroy(r->done);
         if (r->st) (void)hipStreamDestroy(r->st);
         delete r;
         return hip_fail(e, "routed stream");
@@ -1797,44 +1805,62 @@ int with_scratch(int dev, uint64_t bytes, void* h_out, uint64_t out_bytes, F f) 
     return rc;
 }
 
-// The small kernel on a leased routed stream, its result collected by
-// spinning on the workgroups' tagged slots in the pinned result area (no
-// stream wait: the completion signal adds microseconds to a 5 µs kernel).
-// Bounded: every 64 µs of spinning the stream is queried, and an error or a
-// stream that finished without all tags falls back to hipStreamSynchronize's
-// verdict. The stream's later work is ordered behind this kernel, so the
-// area is not rewritten before the kernel has ended.
-// Spin until the `per` tagged words of each of `n` workgroups (slots w[per
-// b + h]) carry `tag`; x[h] = XOR of their low words. Bounded: every 64 µs
-// the stream is queried, and a stream that finished (or failed) without all
-// tags returns its error.
-int spin_tagged(RoutedStream* r, uint32_t tag, uint32_t n, uint32_t* x, uint32_t per, const char* what) {
+// Collecting a routed call's result (crc32c.h:30-33 is synchronous). The
+// kernels store their result words tagged, at system scope, into the routed
+// stream's pinned area, and the caller polls the tags: a completion signal
+// would add microseconds to a 5 µs kernel. The poll is bounded so that a
+// routed call does not hold a Photon vCPU (rpc.cpp:379: coroutines share the
+// thread, thread/thread.h:511-520) for the whole of a long kernel:
+//   1. a call whose kernel is expected to run longer than the spin window
+//      (its bytes at the nominal rate below) first sleeps through all but
+//      the window (nanosleep; the CPU is free for other threads);
+//   2. then polls the tags with a pause between reads for at most the spin
+//      window (g_routed_wait, default 30 µs);
+//   3. then sleeps in the driver until the stream's work has finished
+//      (an event with hipEventBlockingSync recorded behind the kernel) and
+//      reads the tags once more; a stream that finished (or failed) without
+//      every tag returns its error.
+// photon_crc_set_routed_wait (tuning.h) changes the window and step 1.
+constexpr double kNominalBytesPerUs = 6.0e6;           // ~75 % of 8 TB/s: a long kernel's expected rate
+
+inline void cpu_relax() {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+    __builtin_ia32_pause();
+#endif
+}
+
+// Wait until the `per` tagged words of each of `n` workgroups (slots w[per
+// b + h]) carry `tag`; x[h] = XOR of their low words. `bytes`: the call's
+// payload (the sleep-ahead estimate).
+int wait_tagged(RoutedStream* r, uint32_t tag, uint32_t n, uint32_t* x, uint32_t per, uint64_t bytes,
+                const char* what) {
+    using clk = std::chrono::steady_clock;
     const volatile uint64_t* w = static_cast<const volatile uint64_t*>(r->h);
     const uint32_t total = n * per;
-    auto t0 = std::chrono::steady_clock::now();
     uint32_t done = 0;
-    for (;;) {
+    auto scan = [&] {
         while (done < total && (uint32_t)(w[done] >> 32) == tag) {
             x[done % per] ^= (uint32_t)w[done];
             ++done;
         }
-        if (done == total) return 0;
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(64)) {
-            const hipError_t q = hipStreamQuery(r->st);
-            if (q == hipErrorNotReady) {
-                t0 = std::chrono::steady_clock::now();
-                continue;
-            }
-            // finished (or failed) without every tag seen yet: a last look, then its verdict
-            while (done < total && (uint32_t)(w[done] >> 32) == tag) {
-                x[done % per] ^= (uint32_t)w[done];
-                ++done;
-            }
-            if (done == total) return 0;
-            const hipError_t e = hipStreamSynchronize(r->st);
-            return hip_fail(e != hipSuccess ? e : hipErrorUnknown, what);
-        }
+        return done == total;
+    };
+    const uint32_t pol = g_routed_wait.load(std::memory_order_relaxed);
+    const auto spin = std::chrono::microseconds(pol & 0xffffu);
+    const double expect_us = (double)bytes / kNominalBytesPerUs;
+    if ((pol >> 16) && expect_us > (double)(pol & 0xffffu) + 20.0)
+        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(expect_us - (double)(pol & 0xffffu))));
+    const auto t0 = clk::now();
+    while (!scan()) {
+        if (clk::now() - t0 > spin) break;
+        for (int k = 0; k < 8; ++k) cpu_relax();
     }
+    if (done == total) return 0;
+    hipError_t e = hipEventRecord(r->done, r->st);
+    if (e == hipSuccess) e = hipEventSynchronize(r->done);
+    if (e != hipSuccess) (void)hipStreamSynchronize(r->st);  // nothing left running on a returned stream
+    if (scan()) return 0;
+    return hip_fail(e != hipSuccess ? e : hipErrorUnknown, what);
 }
 
 int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_out) {
@@ -1855,7 +1881,7 @@ int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_ou
     }
     if (!rc) {
         uint32_t x = 0;
-        rc = spin_tagged(r, sa.tag, sgrid, &x, 1, "crc32c_small_kernel (routed)");
+        rc = wait_tagged(r, sa.tag, sgrid, &x, 1, sa.eoff, "crc32c_small_kernel (routed)");
         if (!rc) *crc_out = x;
     } else {
         (void)hipStreamSynchronize(r->st);  // nothing left running on a returned stream
@@ -1880,7 +1906,7 @@ int routed_long(int dev, const uint8_t* p, uint64_t n, uint32_t crc, uint32_t* c
     }
     if (!rc) {
         uint32_t x = 0;
-        rc = spin_tagged(r, tag, 1, &x, 1, "crc32c_long_kernel (routed)");
+        rc = wait_tagged(r, tag, 1, &x, 1, n, "crc32c_long_kernel (routed)");
         if (!rc) *crc_out = x;
     } else {
         (void)hipStreamSynchronize(r->st);
@@ -1904,7 +1930,7 @@ int routed_long64(int dev, const uint8_t* p, uint64_t n, uint64_t crc, uint64_t*
     }
     if (!rc) {
         uint32_t x[2] = {0, 0};
-        rc = spin_tagged(r, tag, 1, x, 2, "crc64_long_kernel (routed)");
+        rc = wait_tagged(r, tag, 1, x, 2, n, "crc64_long_kernel (routed)");
         if (!rc) *crc_out = ((uint64_t)x[1] << 32) | x[0];  // long_reduce already inverted it
     } else {
         (void)hipStreamSynchronize(r->st);
@@ -1931,7 +1957,7 @@ int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* cr
     }
     if (!rc) {
         uint32_t x[2] = {0, 0};
-        rc = spin_tagged(r, sa.tag, sgrid, x, 2, "crc64_small_kernel (routed)");
+        rc = wait_tagged(r, sa.tag, sgrid, x, 2, sa.eoff, "crc64_small_kernel (routed)");
         if (!rc) *crc_out = ~(((uint64_t)x[1] << 32) | x[0]);
     } else {
         (void)hipStreamSynchronize(r->st);

@@ -89,3 +89,17 @@ def test_cpp_concurrent_submitters():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 mismatches, 0 errors" in r.stdout
+
+
+def test_multi_device_plumbing_simulated_8_devices():
+    """the shard plan and per-device switching behind
+    photon_crc32c_host_batch_strided_multi / _batch_strided_shards /
+    _extend_spans, and the per-device table images, run against a simulated
+    runtime of 8 devices (tests/cpp/multi_device_test.cpp, CPU only): slices
+    contiguous, disjoint, complete and balanced for 1-8 devices; every slice's
+    work runs with its own device current and reads its own device's image;
+    failures name their device; the caller's device is restored."""
+    exe = os.path.join(BIN, "multi_device_test")
+    assert os.path.exists(exe), "build with make -C photonlibos_amd/csrc"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -144,7 +144,34 @@ def test_capacity_and_empty(torch_dev):
     b.wait()
     assert b.result(1) == (True, 0)
     b.close()
+    # a message-object body counts as ONE of max_segments (the
+    # zero word standing for its m_checksum takes a slot the batch reserves
+    # itself), as before the zero-word change: two bodies fit max_segments 2.
+    b = MessageBatch(3, 2)
+    bodies = []
+    for k in range(2):
+        body = alloc.alloc(64)
+        v = PinnedAlloc.view(body, 64)
+        v[:] = np.arange(64, dtype=np.uint8) + k
+        bodies.append(body)
+        z = v.copy()
+        z[:4] = 0  # validate_checksum hashes the object with m_checksum = 0
+        b.add([(a, 8)], (body, 64), oracle_crc32c(z))
+    with pytest.raises(CrcError) as e:
+        b.add([], (bodies[0], 64), 0)
+    assert e.value.code == -28  # ENOSPC: the caller's two segments are used
+    b.submit()
+    assert b.wait() == 0
+    assert b.result(0)[0] and b.result(1)[0]
+    b.close()
+    for body in bodies:
+        alloc.dealloc(body)
     alloc.dealloc(a)
+
+
+def oracle_crc32c(data):
+    from tests import _oracle
+    return _oracle.crc32c(data)
 
 
 def test_resubmit_after_completion_without_wait(torch_dev, oracle):

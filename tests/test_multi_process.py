@@ -133,3 +133,33 @@ def test_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, os.path.join(bench.REPO, "bench.py"), *env_args], capture_output=True,
                        text=True, timeout=120, env=env, cwd=bench.REPO)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_two_rank_line_carries_c4_leg():
+    """with --gpus N > 1 the C2 line (value, config.workload =
+    C2) also carries a `config_c4` sub-record for BASELINE configs[3] timed in
+    the same ranks after the C2 leg; each rank checksummed ITS part of the C4
+    batch (global ids r*32768..)."""
+    from photonlibos_amd import datagen
+    r = _run_bench("--gpus", "2", "--cpu-rehearsal", "--steps", "2", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["config"]["workload"] == bench.CONFIGS["c2"]["workload"]
+    c4 = res["config_c4"]
+    assert c4["workload"] == bench.CONFIGS["c4"]["workload"] and c4["config"] == "c4"
+    assert c4["buffers_total"] == 2 * 32768 and c4["steps"] == 2 and c4["warmup"] == 1
+    assert [p["rank"] for p in c4["per_rank"]] == [0, 1]
+    for p in c4["per_rank"]:
+        want = oracle_crc(datagen.stream_bytes(bench.shard_seed_base(p["rank"], 32768), 1 << 20))
+        assert p["first_crc"] == want
+    # the C4 leg's value is its own bytes over its own slowest-rank time
+    slow = max(p["wall_s"] for p in c4["per_rank"])
+    assert c4["value"] == pytest.approx(2 * 2 * 4 * (1 << 20) / slow / (1 << 30), rel=0.05)
+    # and the one-GPU line has none (the driver's N = 1 run stays C2 only)
+    r1 = _run_bench("--gpus", "1", "--cpu-rehearsal", "--steps", "1", "--warmup", "0")
+    assert "config_c4" not in json.loads([ln for ln in r1.stdout.splitlines() if ln.startswith("{")][0])
+
+
+def oracle_crc(data):
+    from tests import _oracle
+    return _oracle.crc32c(data)
