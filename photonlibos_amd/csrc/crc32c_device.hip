@@ -84,6 +84,10 @@ std::atomic<int> g_generic_u{-1};
 // while strided batches keep 4 (C2 -6, C3 -1.2, C4 -0.9 with 2).
 std::atomic<int> g_msg_u{2};
 std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
+// CRC-64 whole-step uniform batches: rows per step << 4 | mode (0 = the
+// generic kernel, 1 = crc64_full_kernel, 2 = with the next buffer's first
+// step prefetched across the finish).
+std::atomic<uint32_t> g_full64{2u << 4 | 0u};
 // Routed drop-in calls: spin window in µs | sleep-ahead << 16 (wait_tagged).
 std::atomic<uint32_t> g_routed_wait{30u | 1u << 16};
 
@@ -454,6 +458,35 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     uint64_t grid = (waves + kWaves - 1) / kWaves;
     if (grid > (uint64_t)cus) grid = cus;
     const LaneConsts64& kc = lane_consts64(g);
+    // Whole-step uniform batches: the full-row kernel (crc64_kernels.h).
+    const uint32_t full = g_full64.load(std::memory_order_relaxed);
+    const int fu = (int)(full >> 4), fx = (int)(full & 15u);
+    if (fx && !a.iov && a.shift_init && a.nbytes % (2ull * 16ull * (uint64_t)g * (uint64_t)fu) == 0) {
+#define LF64(GG, UU)                                                                                          \
+    do {                                                                                                      \
+        if (fx == 2)                                                                                          \
+            hipLaunchKernelGGL((crc64_full_kernel<GG, UU, true>), dim3(grid), dim3(kBlock), 0, stream, a, kc);  \
+        else                                                                                                  \
+            hipLaunchKernelGGL((crc64_full_kernel<GG, UU, false>), dim3(grid), dim3(kBlock), 0, stream, a, kc); \
+    } while (0)
+#define LF64G(UU)                     \
+    switch (g) {                      \
+        case 64: LF64(64, UU); break; \
+        case 32: LF64(32, UU); break; \
+        case 16: LF64(16, UU); break; \
+        case 8: LF64(8, UU); break;   \
+        default: LF64(4, UU); break;  \
+    }
+        if (fu == 4) {
+            LF64G(4)
+        } else {
+            LF64G(2)
+        }
+#undef LF64G
+#undef LF64
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "crc64_full_kernel launch");
+    }
     switch (g) {
         case 64: hipLaunchKernelGGL(crc64_batch_kernel<64>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
         case 32: hipLaunchKernelGGL(crc64_batch_kernel<32>, dim3(grid), dim3(kBlock), 0, stream, a, kc); break;
@@ -960,6 +993,13 @@ int photon_crc_set_long_shape(int lanes, int rounds) {
     if ((lanes != 0 && lanes != 32 && lanes != 64) || rounds < 0 || rounds > 64)
         return fail(-EINVAL, "long-buffer lanes must be 0, 32 or 64 and rounds 0..64");
     g_long_shape.store((uint32_t)lanes | (uint32_t)rounds << 8, std::memory_order_relaxed);
+    return 0;
+}
+
+int photon_crc64_set_full_rows(int mode, int rows_per_step) {
+    if (mode < 0 || mode > 2 || (rows_per_step != 2 && rows_per_step != 4))
+        return fail(-EINVAL, "full-row mode must be 0, 1 or 2 and rows per step 2 or 4");
+    g_full64.store((uint32_t)rows_per_step << 4 | (uint32_t)mode, std::memory_order_relaxed);
     return 0;
 }
 

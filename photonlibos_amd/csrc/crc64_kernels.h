@@ -501,6 +501,111 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
     crc64_batch_run<G>(args, kc, lds, nullptr);
 }
 
+// ------------------------------------------------ full-row uniform batches
+// Strided batches whose buffers are made of whole steps: base and stride
+// 16-byte aligned, nbytes a multiple of 2 * 16 G U (an even number of U-row
+// steps), one seed for all (its inverted init enters at the end, shift_init).
+// Every lane has a block in every row, so nothing in the loop depends on the
+// lane: the trip counts are wave-uniform (scalar loop control, no exec-mask
+// loops), every load is unconditional and the compiler counts vmcnt exactly.
+// Two register sets in turn (no copies on the loop edge, round 4's body
+// copied U rows every step): the next step's U rows are issued before the
+// current step's lookups, one step in flight as in the generic kernel.
+// XB: the next buffer's first step is issued before this buffer's last step
+// and finish (the lane-group finish runs with loads in flight instead of none).
+// The first step of a buffer starts from Q = 0, so its first row needs no
+// row shift (the generic kernel shifted 0 through the S tables). Lane gl's
+// last block is G - 1 - gl blocks before the end of every buffer: its finish
+// factor x^(64 + 128 (G - 1 - gl)) is fixed per lane.
+// Reference semantics: crc64ecma_sw (crc.cpp:119-122, 511-669).
+template <int G, int U, bool FIRST>
+__device__ __forceinline__ uint2 column_step64(const uint32_t* lds, uint2 pc, const uint4 (&w)[U],
+                                               const LaneAddr64& la) {
+    uint2 c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = lag16_64(lds, w[u], la);
+    if constexpr (FIRST) {
+        pc = c[0];
+#pragma unroll
+        for (int u = 1; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+    }
+    return pc;
+}
+
+template <int G, int U>
+__device__ __forceinline__ void load_step64(uint4 (&w)[U], const uint8_t* p) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = load16(p + u * (16 * G));
+}
+
+template <int G, int U, bool XB>
+__global__ __launch_bounds__(kBlock) void crc64_full_kernel(Batch64Args args, LaneConsts64 kc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+    build_tables64<G>(lds, kc);
+    constexpr int GPW = 64 / G;
+    constexpr uint32_t kStep = 16u * G * U;  // bytes of one step of a lane group
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gl = lane & (G - 1);
+    const uint32_t grp = lane / G;
+    const LaneAddr64 la = lane_addr64(lane);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    const uint32_t steps = __builtin_amdgcn_readfirstlane((uint32_t)(args.nbytes / kStep));  // even, >= 2
+    const uint32_t d = G - 1 - gl;
+    uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave_id();
+    if (wv * GPW >= args.count) return;
+    // This lane's first block of wave-iteration w's buffer (a group past the
+    // end of the batch re-reads the last buffer; its result is not stored).
+    auto lane_ptr = [&](uint64_t w) {
+        const uint64_t bi = w * GPW + grp;
+        return args.base + (bi < args.count ? bi : args.count - 1) * args.stride + 16u * gl;
+    };
+    uint4 a[U], b[U];
+    const uint8_t* p = lane_ptr(wv);
+    load_step64<G, U>(a, p);
+    for (;;) {
+        const uint64_t next = wv + nwaves;
+        const bool more = next * GPW < args.count;  // wave-uniform
+        const uint8_t* pn = more ? lane_ptr(next) : p;
+        uint2 pc;
+        // steps 0 and 1 (peeled: step 0 starts from Q = 0)
+        load_step64<G, U>(b, p + kStep);
+        pc = column_step64<G, U, true>(lds, make_uint2(0, 0), a, la);
+        if (steps > 2) {
+            load_step64<G, U>(a, p + 2 * kStep);
+        } else if (XB && more) {
+            load_step64<G, U>(a, pn);
+        }
+        pc = column_step64<G, U, false>(lds, pc, b, la);
+        for (uint32_t s = 2; s < steps; s += 2) {
+            load_step64<G, U>(b, p + (uint64_t)(s + 1) * kStep);
+            pc = column_step64<G, U, false>(lds, pc, a, la);
+            if (s + 2 < steps) {
+                load_step64<G, U>(a, p + (uint64_t)(s + 2) * kStep);
+            } else if (XB && more) {
+                load_step64<G, U>(a, pn);
+            }
+            pc = column_step64<G, U, false>(lds, pc, b, la);
+        }
+        // Q * x^(64 + 128 d) (Q -> P and the lane's shift to the end), XOR over the group.
+        uint64_t reg;
+        if constexpr (G == 16 && PCRC64_FIN16) {
+            reg = finish_xor16(pc, d, lds, gl, lane);
+        } else {
+            const uint64_t f = finish64<G>(pc, d, lds, lane);
+            reg = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+        }
+        const uint64_t bi = wv * GPW + grp;
+        if (gl == 0 && bi < args.count) args.out[bi] = ~(reg ^ args.init_shift);  // crc.cpp:119-122
+        if (!more) break;
+        if (!XB) load_step64<G, U>(a, pn);
+        wv = next;
+        p = pn;
+    }
+}
+
 // ---------------------------------------------- CRC-64 combine / fold / extend
 // crc64ecma_combine(c1, c2, len2) = c1 ? c2 ^ c1 * x^(8*len2) : c2
 // (crc.cpp crc64ecma_combine_sw: the inverted-CRC combine is linear). A

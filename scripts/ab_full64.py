@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""A/B of the CRC-64 batch kernels on whole-step uniform batches, in ONE
+process with interleaved rounds: the generic batch kernel (mode 0) against
+crc64_full_kernel (mode 1) and its cross-buffer-prefetch form (mode 2), 2 or
+4 rows per step. Every variant's 65,536 / 1,048,576 CRCs must equal the
+generic kernel's (which the GPU parity suite pins to the oracle). One JSON
+line per variant: mean / median launch time (HIP events on the launch
+stream) and the fraction of 8 TB/s."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from photonlibos_amd import checksum as ck  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c3", choices=["c2", "c3"])
+ap.add_argument("--rounds", type=int, default=4)
+ap.add_argument("--reps", type=int, default=30)
+ap.add_argument("--variants", default="0:2,1:2,2:2,1:4,2:4")
+ap.add_argument("--lanes", type=int, default=0)
+args = ap.parse_args()
+
+nbytes, count = {"c2": (65536, 65536), "c3": (4096, 1 << 20)}[args.config]
+st = torch.cuda.current_stream()
+buf = torch.empty(nbytes * count, dtype=torch.uint8, device="cuda")
+ck.fill_splitmix(buf, nbytes, nbytes, count, 0x5EED0001)
+out = torch.zeros(count, dtype=torch.int64, device="cuda")
+ck.set_lanes_per_buffer(args.lanes)
+variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
+ref = None
+times = {v: [] for v in variants}
+for r in range(args.rounds):
+    for v in (variants if r % 2 == 0 else variants[::-1]):
+        ck.set_full_rows64(*v)
+        ck.batch64_strided(buf, nbytes, nbytes, count, out, stream=st)  # warm this shape
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
+        ev[0].record(st)
+        for k in range(args.reps):
+            ck.batch64_strided(buf, nbytes, nbytes, count, out, stream=st)
+            ev[k + 1].record(st)
+        torch.cuda.synchronize()
+        times[v] += [ev[k].elapsed_time(ev[k + 1]) for k in range(args.reps)]
+        o = out.cpu().numpy().copy()
+        if ref is None:
+            ref = o
+        assert np.array_equal(o, ref), f"variant {v} disagrees with the first variant"
+ck.set_full_rows64(0, 2)
+ck.set_lanes_per_buffer(0)
+for v in variants:
+    ms = np.asarray(times[v])
+    print(json.dumps({"config": args.config + "_crc64", "mode": v[0], "rows": v[1], "lanes": args.lanes or "auto",
+                      "launches": int(ms.size), "ms_mean": round(float(ms.mean()), 5),
+                      "ms_median": round(float(np.median(ms)), 5),
+                      "frac_mean": round(nbytes * count / (ms.mean() * 1e-3) / 8e12, 4),
+                      "frac_median": round(nbytes * count / (np.median(ms) * 1e-3) / 8e12, 4)}), flush=True)

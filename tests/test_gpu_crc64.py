@@ -241,3 +241,35 @@ def test_trim64_batch_reference_vectors(torch_dev, ref_vectors, oracle):
     torch_dev.cuda.synchronize()
     assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == want
     assert int(nerr.item()) == 1
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("rows", [2, 4])
+@pytest.mark.parametrize("g", [4, 8, 16, 32, 64])
+def test_full_row_kernel(torch_dev, oracle, mode, rows, g):
+    # crc64_full_kernel (whole-step uniform batches): one and several step
+    # pairs per buffer, counts that leave the last wave's groups partly idle
+    # (they re-read the last buffer, nothing stored), seed0 entering at the
+    # end; every CRC against the oracle. Batches it does not take (seeds per
+    # buffer, a ragged length) fall back to the generic kernel.
+    ck.set_full_rows64(mode, rows)
+    ck.set_lanes_per_buffer(g)
+    try:
+        for k, count in ((1, 1), (1, 37), (3, 301), (2, 1001)):
+            nbytes = 2 * 16 * g * rows * k
+            if nbytes * count > (64 << 20):
+                count = max(1, (64 << 20) // nbytes)
+            d = torch_dev.empty(nbytes * count + 64, dtype=torch_dev.uint8, device="cuda")
+            ck.fill_splitmix(d, nbytes, nbytes, count, 0x6500 + nbytes + g)
+            host = d.cpu().numpy()
+            for seed in (0, 0xFEDCBA9876543210):
+                out = torch_dev.full((count + 1,), -1, dtype=torch_dev.int64, device="cuda")
+                ck.batch64_strided(d, nbytes, nbytes, count, out, seed=seed)
+                torch_dev.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint64)
+                want = oracle.crc64ecma_strided(host, nbytes, nbytes, count, seed)
+                assert np.array_equal(got[:count], np.asarray(want, np.uint64)), (mode, rows, g, nbytes, count, seed)
+                assert int(got[count]) == 0xFFFFFFFFFFFFFFFF  # nothing written past the batch
+    finally:
+        ck.set_full_rows64(0, 2)
+        ck.set_lanes_per_buffer(0)
