@@ -113,9 +113,11 @@ int photon_crc_util_fill_splitmix(void* d_base, uint64_t stride, uint64_t nbytes
                                   uint64_t seed_base, void* stream);
 
 /* Bench utility (not on the checksum path): read nbytes (16-byte aligned
- * base) once with the CRC kernels' load instructions and fold them into
- * d_sink (>= 256 words; grid = min(8*CUs, sink_words/256) blocks of 256):
- * the achievable HBM-read rate the roofline is compared against. */
+ * base) once with the CRC kernels' loads and access pattern (one persistent
+ * 1024-thread workgroup per CU, waves sweeping 64 KiB pieces in 1 KiB rows,
+ * 4 rows in flight) and fold them into d_sink (>= 1024 words; grid =
+ * min(CUs, sink_words/1024)): the achievable HBM-read rate the roofline is
+ * compared against. */
 int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d_sink, uint64_t sink_words,
                                 void* stream);
 

@@ -1640,11 +1640,11 @@ int photon_crc_util_read_stream(const void* d_base, uint64_t nbytes, uint32_t* d
     int cus = 0;
     int dev = current_device(&cus);
     if (dev < 0) return dev;
-    uint64_t grid = (uint64_t)cus * 8;
-    if (grid * 256 > sink_words) grid = sink_words / 256;
-    if (!grid) return fail(-EINVAL, "sink too small (need >= 256 words)");
-    hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                       static_cast<const uint8_t*>(d_base), nbytes / 16, d_sink);
+    uint64_t grid = (uint64_t)cus;  // one persistent 16-wave workgroup per CU, as the batch kernels
+    if (grid * kBlock > sink_words) grid = sink_words / kBlock;
+    if (!grid) return fail(-EINVAL, "sink too small (need >= 1024 words)");
+    hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t*>(d_base), nbytes, d_sink);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "read_stream_kernel launch");
     return 0;

@@ -1448,23 +1448,42 @@ __global__ void fill_splitmix_kernel(uint8_t* base, uint64_t stride, uint64_t nb
 }
 
 // Read-only HBM stream (bench reference for the achievable read roofline):
-// every 16-byte word read once with the same nontemporal dwordx4 loads as the
-// CRC kernels, XOR-folded so nothing is dead code.
-__global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t* p, uint64_t nvec, uint32_t* sink) {
-    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+// the CRC kernels' own access pattern with the CRC replaced by an XOR --
+// persistent 1024-thread workgroups, each wave sweeping contiguous 64 KiB
+// pieces in rows of 1 KiB (one 16-byte nontemporal load per lane), 4 rows
+// per step with the next 4 in flight. (Round 1-4's grid-stride form, 8 loads
+// per thread 8 MiB apart, read at only ~69 % of 8 TB/s, below the CRC
+// kernels themselves) Every byte is read once; the XOR keeps the
+// loads live.
+constexpr uint64_t kStreamPiece = 64u << 10;
+__global__ __launch_bounds__(kBlock) void read_stream_kernel(const uint8_t* p, uint64_t nbytes, uint32_t* sink) {
+    constexpr int U = 4;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+    const uint64_t pieces = nbytes / kStreamPiece;
     uint32_t acc = 0;
-    uint64_t i = tid;
-    for (; i + 7 * nth < nvec; i += 8 * nth) {
-        uint4 v[8];
+    for (uint64_t w = (uint64_t)blockIdx.x * kWaves + wave_id(); w < pieces; w += nwaves) {
+        const uint8_t* q = p + w * kStreamPiece + 16u * lane;
+        uint4 cur[U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = load16(p + 16 * (i + k * nth));
+        for (int u = 0; u < U; ++u) cur[u] = load16(q + u * 1024u);
+        for (uint32_t r = U; r < kStreamPiece / 1024u; r += U) {
+            uint4 nxt[U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+            for (int u = 0; u < U; ++u) nxt[u] = load16(q + (r + u) * 1024u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc ^= xor3(cur[u].x, cur[u].y, cur[u].z) ^ cur[u].w;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= xor3(cur[u].x, cur[u].y, cur[u].z) ^ cur[u].w;
     }
-    for (; i < nvec; i += nth) {
+    // the bytes past the last whole piece: 16-byte words, grid-stride
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    for (uint64_t i = pieces * kStreamPiece / 16 + tid; i < nbytes / 16; i += (uint64_t)gridDim.x * kBlock) {
         const uint4 v = load16(p + 16 * i);
-        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        acc ^= xor3(v.x, v.y, v.z) ^ v.w;
     }
     sink[tid] = acc;
 }
