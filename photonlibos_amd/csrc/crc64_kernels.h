@@ -512,6 +512,8 @@ __global__ __launch_bounds__(kBlock) void crc64_batch_kernel(Batch64Args args, L
 // copied U rows every step): the next step's U rows are issued before the
 // current step's lookups, one step in flight as in the generic kernel.
 // XB: the next buffer's first step is issued before this buffer's last step
+// (the last buffer of a wave re-reads its own first step there: one step of
+// extra reads per wave and launch, so that no load sits behind a branch)
 // and finish (the lane-group finish runs with loads in flight instead of none).
 // The first step of a buffer starts from Q = 0, so its first row needs no
 // row shift (the generic kernel shifted 0 through the S tables). Lane gl's
@@ -573,19 +575,19 @@ __global__ __launch_bounds__(kBlock) void crc64_full_kernel(Batch64Args args, La
         // steps 0 and 1 (peeled: step 0 starts from Q = 0)
         load_step64<G, U>(b, p + kStep);
         pc = column_step64<G, U, true>(lds, make_uint2(0, 0), a, la);
-        if (steps > 2) {
+        if constexpr (XB) {  // unconditional (a select of the address): vmcnt stays exact
+            load_step64<G, U>(a, steps > 2 ? p + 2 * kStep : pn);
+        } else if (steps > 2) {
             load_step64<G, U>(a, p + 2 * kStep);
-        } else if (XB && more) {
-            load_step64<G, U>(a, pn);
         }
         pc = column_step64<G, U, false>(lds, pc, b, la);
         for (uint32_t s = 2; s < steps; s += 2) {
             load_step64<G, U>(b, p + (uint64_t)(s + 1) * kStep);
             pc = column_step64<G, U, false>(lds, pc, a, la);
-            if (s + 2 < steps) {
+            if constexpr (XB) {
+                load_step64<G, U>(a, s + 2 < steps ? p + (uint64_t)(s + 2) * kStep : pn);
+            } else if (s + 2 < steps) {
                 load_step64<G, U>(a, p + (uint64_t)(s + 2) * kStep);
-            } else if (XB && more) {
-                load_step64<G, U>(a, pn);
             }
             pc = column_step64<G, U, false>(lds, pc, b, la);
         }
