@@ -613,18 +613,27 @@ def run_extend(args, stream):
     # Routed drop-in: crc32c_extend through crc32c_auto on a device pointer
     # (default stream, synchronous), and the routing probe's price on host
     # pointers (C1: 1024 x 4 KiB).
+    import resource
+
+    def thread_cpu():
+        r = resource.getrusage(resource.RUSAGE_THREAD)
+        return r.ru_utime + r.ru_stime
     ck.set_device_dispatch(True)
     routed = []
+    c0, w0 = thread_cpu(), time.perf_counter()
     for _ in range(50):
         t0 = time.perf_counter()
         r = ck.crc32c_extend_at(d.data_ptr() + 1, 128 << 10, 0)
         routed.append(time.perf_counter() - t0)
+    cpu_128k = (thread_cpu() - c0) / (time.perf_counter() - w0)
     ok = ok and r == want
     routed_1g = []
+    c0, w0 = thread_cpu(), time.perf_counter()
     for _ in range(10):  # the same drop-in on the 1 GiB buffer (the long kernel, tagged result word)
         t0 = time.perf_counter()
         ck.crc32c_extend_at(d.data_ptr() + 1, n, 0)
         routed_1g.append(time.perf_counter() - t0)
+    cpu_1g = (thread_cpu() - c0) / (time.perf_counter() - w0)
     ck.set_device_dispatch(False)
     hbuf = np.frombuffer(d[:1024 * 4096].cpu().numpy().tobytes(), np.uint8)
     base = hbuf.ctypes.data
@@ -644,6 +653,8 @@ def run_extend(args, stream):
     off_us, on_us = per_call_us(False), per_call_us(True)
     res["routed_crc32c_extend_128KiB_device_us_median"] = round(float(np.median(routed)) * 1e6, 1)
     res["routed_crc32c_extend_1GiB_device_us_median"] = round(float(np.median(routed_1g)) * 1e6, 1)
+    res["routed_calling_thread_cpu_frac"] = {"128KiB": round(cpu_128k, 3), "1GiB": round(cpu_1g, 3),
+                                             "note": "getrusage(RUSAGE_THREAD) over the routed calls / wall time"}
     res["host_pointer_call_us"] = {"dispatch_off": round(off_us, 3), "dispatch_on": round(on_us, 3),
                                    "note": "C1 (1024 x 4 KiB host buffers) through crc32c_auto from Python "
                                            "ctypes; the difference is the per-call hipPointerGetAttributes probe"}

@@ -156,10 +156,15 @@ int photon_crc32c_combine_batch(const uint32_t* d_crc1, const uint32_t* d_crc2, 
  *                    one workgroup share, per stream, the reduce's state (a
  *                    ticket counting every workgroup of the stream's
  *                    launches, a slot per workgroup): the calls are safe
- *                    from any number of streams and threads, but such a call
- *                    cannot be captured into a HIP graph (-ENOTSUP while
- *                    `stream` is capturing; one-workgroup calls, block spans
- *                    up to 4 KiB, may be captured).
+ *                    from any number of streams and threads. Every call may
+ *                    be captured into a HIP graph (even a process's first:
+ *                    the per-device setup runs in relaxed capture mode); a
+ *                    captured launch of more than one workgroup uses a
+ *                    reduce state owned by the graph, reset by the launch
+ *                    itself, so the graph replays any number of times, one
+ *                    replay at a time: two executable graphs instantiated
+ *                    from the same captured graph share those states and
+ *                    must not run concurrently.
  * Asynchronous on `stream` like the batches. */
 int photon_crc32c_series_device(const void* d_buffer, uint32_t part_size, uint32_t n_parts, uint32_t* d_crc_parts,
                                 void* stream);
@@ -193,8 +198,13 @@ int photon_crc32c_extend_spans(const photon_crc_span* spans, int nspans, uint32_
  * routed call runs on a non-blocking stream leased from a per-device pool
  * (never the legacy default stream, so it does not serialise against the
  * process's other streams; concurrent routed calls get streams of their
- * own) and its result is written by the kernel into pinned host memory. Off (the default, also at load time) restores the host
- * engines. The reference signatures have no error channel and the reference
+ * own) and its result is written by the kernel into pinned host memory. The
+ * calling thread (a photon vCPU: its coroutines wait with it) does not spin
+ * through a long kernel: a call whose bytes would take longer than the poll
+ * window first sleeps through its expected time, then polls the result words
+ * with a pause between reads for at most 30 us, then sleeps in the driver
+ * until the kernel ends (photon_crc_set_routed_wait, tuning.h). Off (the
+ * default, also at load time) restores the host engines. The reference signatures have no error channel and the reference
  * always computes (crc.cpp:114-117), so a routed call whose device work
  * fails NEVER returns a made-up value: it is reported on stderr, counted,
  * errno is set to EIO, and the bytes are copied to the host and checksummed
@@ -252,8 +262,7 @@ int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* 
 /* photon_crc32c_extend_device for CRC-64/ECMA (crc64ecma_extend, crc.cpp:
  * 119-122): the same latency path for spans up to 256 KiB (a small kernel of
  * up to 32 workgroups), one launch over the chip above, the same per-stream
- * state and capture rule (-ENOTSUP on a capturing stream for more than one
- * workgroup; spans up to 4 KiB are capturable). */
+ * state and capture rules. */
 int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,
                                    void* stream);
 /* photon_crc32c_extend_spans for CRC-64/ECMA (crc64ecma_combine's identity:

@@ -25,6 +25,7 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--variants", default="0:2,1:2,2:2,1:4,2:4")
 ap.add_argument("--lanes", type=int, default=0)
+ap.add_argument("--no-check", action="store_true", help="ablation builds (PHOTON_CRC_LIB): results are not CRCs")
 args = ap.parse_args()
 
 nbytes, count = {"c2": (65536, 65536), "c3": (4096, 1 << 20), "c4": (1 << 20, 4096)}[args.config]
@@ -52,7 +53,7 @@ for r in range(args.rounds):
         o = out.cpu().numpy().copy()
         if ref is None:
             ref = o
-        assert np.array_equal(o, ref), f"variant {v} disagrees with the first variant"
+        assert args.no_check or np.array_equal(o, ref), f"variant {v} disagrees with the first variant"
 setk(0, 2 if args.crc == 64 else 0)
 ck.set_lanes_per_buffer(0)
 for v in variants:

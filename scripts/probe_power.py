@@ -19,7 +19,10 @@ without amdsmi the power sampler's mean power x time is used instead.
 Phases are separated by IDLE_S seconds of idle GPU. One JSON line per phase.
 
   KERNELS=crc,rows,read,crc  STEADY_S=3  IDLE_S=2  python scripts/probe_power.py [--stamps]
-  (crc@W: the product kernel on a grid capped at W workgroups, photon_crc_set_batch_grid)
+  (crc@W: the product kernel on a grid capped at W workgroups, photon_crc_set_batch_grid;
+   c3: CRC-32C on the same 4 GiB as 1 Mi x 4 KiB buffers; c3_64 / c2_64: CRC-64/ECMA on
+   4 KiB / 64 KiB buffers with the generic batch kernel, c3_64full / c2_64full: with the
+   full-row kernel, cross-buffer prefetch, 2 rows per step)
 """
 import ctypes
 import json
@@ -125,6 +128,8 @@ n, cnt = 65536, 65536
 nbytes = n * cnt
 buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
 out = torch.zeros(cnt, dtype=torch.int32, device="cuda")
+out3 = torch.zeros(nbytes // 4096, dtype=torch.int32, device="cuda")
+out64 = torch.zeros(nbytes // 4096, dtype=torch.int64, device="cuda")
 ticket = torch.zeros(256, dtype=torch.int32, device="cuda")
 sink = torch.zeros(max(cus * 8 * 256, cus * 1024), dtype=torch.int32, device="cuda")
 ts = [torch.zeros(6 * cus * 32, dtype=torch.int64, device="cuda") for _ in range(WINDOW)]
@@ -139,6 +144,14 @@ def launch(kernel, k):
     elif STAMPS:
         rc = P.probe_crc_wave_times(buf.data_ptr(), n, cnt, out.data_ptr(), t, ticket.data_ptr(), 32, 0, 0, cus,
                                     st.cuda_stream)
+    elif kernel == "c3":
+        ck.batch_strided(buf, 4096, 4096, nbytes // 4096, out3, stream=st)
+        rc = 0
+    elif kernel.startswith("c3_64") or kernel.startswith("c2_64"):
+        ck.set_full_rows64(2 if kernel.endswith("full") else 0, 2)
+        b = 4096 if kernel.startswith("c3") else 65536
+        ck.batch64_strided(buf, b, b, nbytes // b, out64, stream=st)
+        rc = 0
     else:  # crc or crc@<workgroups>: the product kernel (on a capped grid)
         ck.batch_strided(buf, n, n, cnt, out, stream=st)
         rc = 0
@@ -179,7 +192,7 @@ def phase(kernel, label):
     torch.cuda.synchronize()
     e1, t1 = board.energy_uj(), time.perf_counter()
     ms = [round(a.elapsed_time(b), 4) for a, b in ev]
-    clk = clocks(WINDOW) if (kernel != "crc" or STAMPS) else None
+    clk = clocks(WINDOW) if (kernel in ("read", "rows") or STAMPS) else None
     # steady state
     e2, t2 = board.energy_uj(), time.perf_counter()
     launches = 0
