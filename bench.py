@@ -613,27 +613,37 @@ def run_extend(args, stream):
     # Routed drop-in: crc32c_extend through crc32c_auto on a device pointer
     # (default stream, synchronous), and the routing probe's price on host
     # pointers (C1: 1024 x 4 KiB).
-    import resource
-
-    def thread_cpu():
-        r = resource.getrusage(resource.RUSAGE_THREAD)
-        return r.ru_utime + r.ru_stime
     ck.set_device_dispatch(True)
     routed = []
-    c0, w0 = thread_cpu(), time.perf_counter()
     for _ in range(50):
         t0 = time.perf_counter()
         r = ck.crc32c_extend_at(d.data_ptr() + 1, 128 << 10, 0)
         routed.append(time.perf_counter() - t0)
-    cpu_128k = (thread_cpu() - c0) / (time.perf_counter() - w0)
     ok = ok and r == want
     routed_1g = []
-    c0, w0 = thread_cpu(), time.perf_counter()
     for _ in range(10):  # the same drop-in on the 1 GiB buffer (the long kernel, tagged result word)
         t0 = time.perf_counter()
         ck.crc32c_extend_at(d.data_ptr() + 1, n, 0)
         routed_1g.append(time.perf_counter() - t0)
-    cpu_1g = (thread_cpu() - c0) / (time.perf_counter() - w0)
+    # The routed calls' wait policy (photon_crc_set_routed_wait): latency and
+    # the calling thread's CPU time (CLOCK_THREAD_CPUTIME_ID) over >= 0.3 s of
+    # back-to-back calls each, for spin windows / sleep-ahead on and off.
+    policies = {}
+    for spin_us, ahead in ((30, True), (30, False), (0, False), (100, True), (1000, False)):
+        ck.set_routed_wait(spin_us, ahead)
+        row = {}
+        for label, nb in (("128KiB", 128 << 10), ("1GiB", n)):
+            lat = []
+            c0, w0 = time.thread_time(), time.perf_counter()
+            while time.perf_counter() - w0 < 0.3 or len(lat) < 20:
+                t0 = time.perf_counter()
+                ck.crc32c_extend_at(d.data_ptr() + 1, nb, 0)
+                lat.append(time.perf_counter() - t0)
+            row[label] = {"us_median": round(float(np.median(lat)) * 1e6, 1),
+                          "thread_cpu_frac": round((time.thread_time() - c0) / (time.perf_counter() - w0), 3),
+                          "calls": len(lat)}
+        policies[f"spin{spin_us}{'_sleep_ahead' if ahead else ''}"] = row
+    ck.set_routed_wait(30, True)
     ck.set_device_dispatch(False)
     hbuf = np.frombuffer(d[:1024 * 4096].cpu().numpy().tobytes(), np.uint8)
     base = hbuf.ctypes.data
@@ -651,10 +661,27 @@ def run_extend(args, stream):
         ck.set_device_dispatch(False)
         return best / 1024 * 1e6
     off_us, on_us = per_call_us(False), per_call_us(True)
+    # The CPU alternative for DEVICE-resident bytes: copy the 128 KiB at
+    # buf+1 to pinned host memory (one stream-ordered copy + wait), then the
+    # host engine (crc32c_auto = crc32c_hw, Photon's own choice on x86).
+    from photonlibos_amd._native import lib as _lib
+    L = _lib()
+    hpin = torch.empty(128 << 10, dtype=torch.uint8).pin_memory()
+    crc_fn = ck._auto("crc32c_auto", ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                                                       ctypes.c_uint32))
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    d2h = []
+    for _ in range(50):
+        t0 = time.perf_counter()
+        L.photon_crc_memcpy_async(hpin.data_ptr(), d.data_ptr() + 1, 128 << 10, sptr)
+        L.photon_crc_stream_sync(sptr)
+        r2 = crc_fn(hpin.data_ptr(), 128 << 10, 0)
+        d2h.append(time.perf_counter() - t0)
+    ok = ok and r2 == want
+    res["d2h_copy_then_host_crc32c_128KiB_us_median"] = round(float(np.median(d2h)) * 1e6, 1)
     res["routed_crc32c_extend_128KiB_device_us_median"] = round(float(np.median(routed)) * 1e6, 1)
     res["routed_crc32c_extend_1GiB_device_us_median"] = round(float(np.median(routed_1g)) * 1e6, 1)
-    res["routed_calling_thread_cpu_frac"] = {"128KiB": round(cpu_128k, 3), "1GiB": round(cpu_1g, 3),
-                                             "note": "getrusage(RUSAGE_THREAD) over the routed calls / wall time"}
+    res["routed_wait_policies"] = policies
     res["host_pointer_call_us"] = {"dispatch_off": round(off_us, 3), "dispatch_on": round(on_us, 3),
                                    "note": "C1 (1024 x 4 KiB host buffers) through crc32c_auto from Python "
                                            "ctypes; the difference is the per-call hipPointerGetAttributes probe"}

@@ -55,18 +55,13 @@ int photon_crc_set_msg_rows(int rows_per_step);
  * from 3 GiB. */
 int photon_crc_set_long_shape(int lanes, int rounds);
 
-/* CRC32C batches of whole steps (aligned strided, one seed, nbytes a
- * multiple of 32 * lanes * rows_per_step): 0 = the generic batch kernel,
- * 1 = the full-row kernel, 2 = the same with the next buffer's first rows
- * issued before the finish; rows_per_step 0 (as the batch kernel: 2 for
- * 16-lane groups, else 4), 2 or 4. Default: see DESIGN.md §4. */
-int photon_crc_set_full_rows(int mode, int rows_per_step);
-
 /* CRC-64 batches of whole steps (aligned strided, one seed, nbytes a
  * multiple of 32 * lanes * rows_per_step): 0 = the generic batch kernel,
  * 1 = the full-row kernel (wave-uniform loop, two register sets), 2 = the
- * same with the next buffer's first rows issued before the finish;
- * rows_per_step 2 or 4. Default: see DESIGN.md §4.1. */
+ * same with the next buffer's first rows issued before the finish, 3 = the
+ * default: mode 2 for buffers that take lane groups of up to 16 lanes (up to
+ * 8 KiB), the generic kernel above; rows_per_step 2 or 4 (default 2).
+ * DESIGN.md §4.1 has the measurements. */
 int photon_crc64_set_full_rows(int mode, int rows_per_step);
 
 /* Routed drop-in calls (photon_crc_set_device_dispatch) collect their result

@@ -521,15 +521,10 @@ def set_routed_wait(spin_us=30, sleep_ahead=True):
     _check(lib().photon_crc_set_routed_wait(spin_us, 1 if sleep_ahead else 0))
 
 
-def set_full_rows(mode, rows_per_step=0):
-    """CRC32C whole-step uniform batches: 0 generic kernel, 1 full-row kernel,
-    2 full-row kernel with cross-buffer prefetch; rows 0 = as the batch kernel (tuning)."""
-    _check(lib().photon_crc_set_full_rows(mode, rows_per_step))
-
-
 def set_full_rows64(mode, rows_per_step=2):
     """CRC-64 whole-step uniform batches: 0 generic kernel, 1 full-row kernel,
-    2 full-row kernel with cross-buffer prefetch (tuning)."""
+    2 full-row kernel with cross-buffer prefetch, 3 automatic (the default:
+    2 for buffers up to 8 KiB) (tuning)."""
     _check(lib().photon_crc64_set_full_rows(mode, rows_per_step))
 
 

@@ -84,14 +84,12 @@ std::atomic<int> g_generic_u{-1};
 // while strided batches keep 4 (C2 -6, C3 -1.2, C4 -0.9 with 2).
 std::atomic<int> g_msg_u{2};
 std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2 segment kernel + fold kernel
-// CRC32C whole-step uniform batches: rows per step << 4 (0 = as the batch
-// kernel) | mode (0 = the generic kernel, 1 = crc32c_full_kernel, 2 = with
-// the next buffer's first step prefetched across the finish).
-std::atomic<uint32_t> g_full32{0u};
 // CRC-64 whole-step uniform batches: rows per step << 4 | mode (0 = the
 // generic kernel, 1 = crc64_full_kernel, 2 = with the next buffer's first
-// step prefetched across the finish).
-std::atomic<uint32_t> g_full64{2u << 4 | 0u};
+// step prefetched across the finish, 3 = automatic: mode 2 for lane groups
+// of up to 16 lanes, i.e. buffers up to 8 KiB, else the generic kernel;
+// DESIGN.md §4.1).
+std::atomic<uint32_t> g_full64{2u << 4 | 3u};
 // Routed drop-in calls: spin window in µs | sleep-ahead << 16 (wait_tagged).
 std::atomic<uint32_t> g_routed_wait{30u | 1u << 16};
 
@@ -406,35 +404,6 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
     if (const int cap = g_grid_cap.load(std::memory_order_relaxed)) grid = grid > (uint64_t)cap ? (uint64_t)cap : grid;
     const int rows_per_step = batch_rows(g);
     const LaneConsts& kc = lane_consts(g);
-    // Whole-step uniform batches: the full-row kernel (crc32c_kernels.h).
-    const uint32_t full = g_full32.load(std::memory_order_relaxed);
-    const int fx = (int)(full & 15u), fu = (full >> 4) ? (int)(full >> 4) : (rows_per_step == 2 ? 2 : 4);
-    if (fx && !a.iov && a.shift_init && a.nbytes % (2ull * 16ull * (uint64_t)g * (uint64_t)fu) == 0) {
-#define LF32(GG, UU)                                                                                          \
-    do {                                                                                                      \
-        if (fx == 2)                                                                                          \
-            hipLaunchKernelGGL((crc32c_full_kernel<GG, UU, true>), dim3(grid), dim3(kBlock), 0, stream, a, kc);  \
-        else                                                                                                  \
-            hipLaunchKernelGGL((crc32c_full_kernel<GG, UU, false>), dim3(grid), dim3(kBlock), 0, stream, a, kc); \
-    } while (0)
-#define LF32G(UU)                     \
-    switch (g) {                      \
-        case 64: LF32(64, UU); break; \
-        case 32: LF32(32, UU); break; \
-        case 16: LF32(16, UU); break; \
-        case 8: LF32(8, UU); break;   \
-        default: LF32(4, UU); break;  \
-    }
-        if (fu == 2) {
-            LF32G(2)
-        } else {
-            LF32G(4)
-        }
-#undef LF32G
-#undef LF32
-        const hipError_t e = hipGetLastError();
-        return e == hipSuccess ? 0 : hip_fail(e, "crc32c_full_kernel launch");
-    }
 #define LB(GG, UU) \
     hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc, pow_table())
 #define LBG(UU)                    \
@@ -493,7 +462,8 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     const LaneConsts64& kc = lane_consts64(g);
     // Whole-step uniform batches: the full-row kernel (crc64_kernels.h).
     const uint32_t full = g_full64.load(std::memory_order_relaxed);
-    const int fu = (int)(full >> 4), fx = (int)(full & 15u);
+    const int fu = (int)(full >> 4);
+    const int fx = (full & 15u) == 3u ? (g <= 16 ? 2 : 0) : (int)(full & 15u);
     if (fx && !a.iov && a.shift_init && a.nbytes % (2ull * 16ull * (uint64_t)g * (uint64_t)fu) == 0) {
 #define LF64(GG, UU)                                                                                          \
     do {                                                                                                      \
@@ -1029,16 +999,9 @@ int photon_crc_set_long_shape(int lanes, int rounds) {
     return 0;
 }
 
-int photon_crc_set_full_rows(int mode, int rows_per_step) {
-    if (mode < 0 || mode > 2 || (rows_per_step != 0 && rows_per_step != 2 && rows_per_step != 4))
-        return fail(-EINVAL, "full-row mode must be 0, 1 or 2 and rows per step 0 (auto), 2 or 4");
-    g_full32.store((uint32_t)rows_per_step << 4 | (uint32_t)mode, std::memory_order_relaxed);
-    return 0;
-}
-
 int photon_crc64_set_full_rows(int mode, int rows_per_step) {
-    if (mode < 0 || mode > 2 || (rows_per_step != 2 && rows_per_step != 4))
-        return fail(-EINVAL, "full-row mode must be 0, 1 or 2 and rows per step 2 or 4");
+    if (mode < 0 || mode > 3 || (rows_per_step != 2 && rows_per_step != 4))
+        return fail(-EINVAL, "full-row mode must be 0..3 and rows per step 2 or 4");
     g_full64.store((uint32_t)rows_per_step << 4 | (uint32_t)mode, std::memory_order_relaxed);
     return 0;
 }

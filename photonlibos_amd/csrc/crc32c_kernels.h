@@ -951,99 +951,6 @@ __global__ void crc32c_trim_kernel(const photon_crc_component* all, const photon
     out[i] = crc;
 }
 
-// ------------------------------------------------ full-row uniform batches
-// Strided batches whose buffers are made of whole step pairs: base and
-// stride 16-byte aligned, nbytes a multiple of 2 * 16 G U, one seed for all
-// (entering at the end, shift_init). Every lane has a block in every row, so
-// nothing in the loop depends on the lane: wave-uniform trip counts (scalar
-// loop control instead of exec-mask loops), unconditional loads (exact
-// vmcnt waits), two register sets in turn instead of a copy of U rows on
-// every loop edge, and the first row of a buffer taken without its (zero)
-// row shift. XB: the next buffer's first step is issued before this
-// buffer's last step and finish (through a select of the address, so no load
-// sits behind a branch; a wave's last buffer re-reads its own first step
-// there: one step of extra reads per wave and launch). Lane gl's last block lies G - 1 - gl blocks
-// before every buffer's end: a fixed finish factor per lane.
-// (crc64_kernels.h crc64_full_kernel is the CRC-64 form.)
-template <int U, bool FIRST>
-__device__ __forceinline__ uint32_t column_step32(const uint32_t* lds, uint32_t q, const uint4 (&w)[U],
-                                                  const LaneAddr& la) {
-    uint32_t c[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = lag16(lds, w[u], la);
-    if constexpr (FIRST) {
-        q = c[0];
-#pragma unroll
-        for (int u = 1; u < U; ++u) q = sstep(lds, q, la, c[u]);
-    } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) q = sstep(lds, q, la, c[u]);
-    }
-    return q;
-}
-
-template <int G, int U>
-__device__ __forceinline__ void load_step32(uint4 (&w)[U], const uint8_t* p) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) w[u] = load16(p + u * (16 * G));
-}
-
-template <int G, int U, bool XB>
-__global__ __launch_bounds__(kBlock) void crc32c_full_kernel(BatchArgs args, LaneConsts kc) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
-    build_tables<G>(lds, kc);
-    constexpr int GPW = 64 / G;
-    constexpr uint32_t kStep = 16u * G * U;  // bytes of one step of a lane group
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gl = lane & (G - 1);
-    const uint32_t grp = lane / G;
-    const LaneAddr la = lane_addr(lane);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-    const uint32_t steps = __builtin_amdgcn_readfirstlane((uint32_t)(args.nbytes / kStep));  // even, >= 2
-    const uint32_t d = G - 1 - gl;
-    uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave_id();
-    if (wv * GPW >= args.count) return;
-    // This lane's first block of wave-iteration w's buffer (a group past the
-    // end of the batch re-reads the last buffer; its result is not stored).
-    auto lane_ptr = [&](uint64_t w) {
-        const uint64_t bi = w * GPW + grp;
-        return args.base + (bi < args.count ? bi : args.count - 1) * args.stride + 16u * gl;
-    };
-    uint4 a[U], b[U];
-    const uint8_t* p = lane_ptr(wv);
-    load_step32<G, U>(a, p);
-    for (;;) {
-        const uint64_t next = wv + nwaves;
-        const bool more = next * GPW < args.count;  // wave-uniform
-        const uint8_t* pn = more ? lane_ptr(next) : p;
-        load_step32<G, U>(b, p + kStep);
-        uint32_t q = column_step32<U, true>(lds, 0u, a, la);
-        if constexpr (XB) {  // unconditional (a select of the address): vmcnt stays exact
-            load_step32<G, U>(a, steps > 2 ? p + 2 * kStep : pn);
-        } else if (steps > 2) {
-            load_step32<G, U>(a, p + 2 * kStep);
-        }
-        q = column_step32<U, false>(lds, q, b, la);
-        for (uint32_t s = 2; s < steps; s += 2) {
-            load_step32<G, U>(b, p + (uint64_t)(s + 1) * kStep);
-            q = column_step32<U, false>(lds, q, a, la);
-            if constexpr (XB) {
-                load_step32<G, U>(a, s + 2 < steps ? p + (uint64_t)(s + 2) * kStep : pn);
-            } else if (s + 2 < steps) {
-                load_step32<G, U>(a, p + (uint64_t)(s + 2) * kStep);
-            }
-            q = column_step32<U, false>(lds, q, b, la);
-        }
-        const uint32_t crc = finish_group<G>(lds, q, d, la);
-        const uint64_t bi = wv * GPW + grp;
-        if (gl == 0 && bi < args.count) args.out[bi] = crc ^ args.init_shift;  // the seed's share, crc.cpp:393-405
-        if (!more) break;
-        if (!XB) load_step32<G, U>(a, pn);
-        wv = next;
-        p = pn;
-    }
-}
-
 // ------------------------------------------------------- one long buffer
 // photon_crc32c_extend_device (crc32c_extend, crc32c.h:30-33, over ONE
 // device buffer of more than 256 KiB) in ONE launch that fills the chip. The

@@ -271,5 +271,5 @@ def test_full_row_kernel(torch_dev, oracle, mode, rows, g):
                 assert np.array_equal(got[:count], np.asarray(want, np.uint64)), (mode, rows, g, nbytes, count, seed)
                 assert int(got[count]) == 0xFFFFFFFFFFFFFFFF  # nothing written past the batch
     finally:
-        ck.set_full_rows64(0, 2)
+        ck.set_full_rows64(3, 2)
         ck.set_lanes_per_buffer(0)

@@ -418,35 +418,3 @@ def test_msg_many_messages_fused_vs_two_kernels(torch_dev, oracle):
     for m in list(range(0, nmsg, 97)) + [nmsg - 1]:
         parts = [host[o:o + n] for o, n in msgs[m]]
         assert res[1][0][m] == oracle.extend_chain(parts, int(seeds[m])), m
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("rows", [0, 2, 4])
-@pytest.mark.parametrize("g", [4, 8, 16, 32, 64])
-def test_full_row_kernel(torch_dev, oracle, mode, rows, g):
-    # crc32c_full_kernel (whole-step uniform batches): one and several step
-    # pairs per buffer, counts that leave the last wave's groups partly idle
-    # (they re-read the last buffer, nothing stored), seed0 entering at the
-    # end; every CRC against the oracle. Batches it does not take (seeds per
-    # buffer, unaligned, ragged lengths) keep the generic kernel.
-    ck.set_full_rows(mode, rows)
-    ck.set_lanes_per_buffer(g)
-    u = rows or (2 if g == 16 else 4)
-    try:
-        for k, count in ((1, 1), (1, 37), (3, 301), (2, 1001)):
-            nbytes = 2 * 16 * g * u * k
-            count = max(1, min(count, (64 << 20) // nbytes))
-            d = torch_dev.empty(nbytes * count + 64, dtype=torch_dev.uint8, device="cuda")
-            ck.fill_splitmix(d, nbytes, nbytes, count, 0x3200 + nbytes + g)
-            host = d.cpu().numpy()
-            for seed in (0, 0x9E3779B9):
-                out = torch_dev.full((count + 1,), -1, dtype=torch_dev.int32, device="cuda")
-                ck.batch_strided(d, nbytes, nbytes, count, out, seed=seed)
-                torch_dev.cuda.synchronize()
-                got = out.cpu().numpy().view(np.uint32)
-                want = oracle.crc32c_strided(host, nbytes, nbytes, count, seed)
-                assert np.array_equal(got[:count], np.asarray(want, np.uint32)), (mode, rows, g, nbytes, count, seed)
-                assert int(got[count]) == 0xFFFFFFFF  # nothing written past the batch
-    finally:
-        ck.set_full_rows(0, 0)
-        ck.set_lanes_per_buffer(0)
