@@ -14,7 +14,9 @@ Bench-only.
             strided batch kernel over the same bytes as 64 KiB pieces from an
             aligned base) and "read" (the read-only grid-stride stream)
   SIZES_MIB buffer sizes (at base+1, test_checksum.cpp:125-168)
-  LAUNCHES  back-to-back launches per variant per round, ROUNDS rounds
+  LAUNCHES  back-to-back launches per variant per round, ROUNDS rounds (after
+            WARM untimed interleaved rounds: under rocprofv3 every kernel then
+            starts past the fill's DVFS dip, so the kernels' stats compare)
 Prints one JSON line per (size, variant): mean / median ms over all launches,
 frac of 8 TB/s; every variant's CRC must equal the first's."""
 import ctypes
@@ -141,8 +143,14 @@ def make(v, n):
     return f
 
 
+WARM = int(os.environ.get("WARM", "0"))  # untimed interleaved rounds first (past the fill's DVFS dip)
 for n in SIZES:
     fns = {v: make(v, n) for v in VARIANTS}
+    for r in range(WARM):
+        for v in (VARIANTS if r % 2 == 0 else VARIANTS[::-1]):
+            for k in range(N):
+                fns[v](k)
+        torch.cuda.synchronize()
     times = {v: [] for v in VARIANTS}
     crcs = {}
     c64 = {}
