@@ -9,10 +9,11 @@ One "step" = one pass of the hot path over one batch (BASELINE.json configs):
       device-resident, per GPU (weak scaling: N GPUs checksum N such batches,
       so the driver's 1/2/4/8-GPU lines compare like with like)
   c4 (configs[3]): 32,768 x 1 MiB per GPU = the 256 Ki x 1 MiB batch sharded
-      over 8 GPUs (`--config c4 --gpus 8`); with --gpus N > 1 the C2 line
-      also carries a `config_c4` sub-record: the same ranks time the C4 shard
-      right after the C2 leg (so the driver's one 8-GPU run measures
-      configs[3] too; `value` stays C2's)
+      over 8 GPUs (`--config c4 --gpus 8`); at every --gpus N the C2 line
+      also carries a `config_c4` sub-record: the same ranks time their C4
+      shard right after the C2 leg (so the driver's 1/2/4/8-GPU sweep also
+      measures configs[3], weak-scaling, as SURVEY §8(d) asks; `value` stays
+      C2's)
   c3: 1,048,576 x 4 KiB        c5: 65,536 messages x 8 non-contiguous 8 KiB
       segments, per-segment CRC + crc32c_combine fold (BASELINE.json configs[4])
   c5_chain: the C5 shape, one CRC per message chained through the seed
@@ -103,7 +104,7 @@ def parse(argv=None):
                     help="do not run the rocprofv3 FETCH_SIZE child pass; read profiles/pmc_<config>.json instead")
     ap.add_argument("--no-shape64", action="store_true", help="skip the one-wavefront-per-buffer (G=64) side line")
     ap.add_argument("--no-c4-leg", action="store_true",
-                    help="with --gpus N > 1: skip the C4 (BASELINE configs[3]) leg timed after the C2 line")
+                    help="skip the C4 (BASELINE configs[3]) shard leg timed after the C2 leg")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (profiles/*.json) giving HBM bytes per launch (fallback when no live pass)")
@@ -752,7 +753,8 @@ def event_marks(stream):
 
 
 def c4_leg(args, rank, world, device, stream, dist):
-    """BASELINE configs[3] in the same ranks after the C2 leg:
+    """BASELINE configs[3] in the same ranks after the C2 leg,
+    at every N (the same per-GPU shard at 1/2/4/8 GPUs):
     every rank checksums its 32 Ki x 1 MiB shard of the 256 Ki x 1 MiB batch
     (global ids r*32768.., no collective), timed like the C2 leg (barrier +
     sync both sides, max over ranks). At N = 8 this is the whole configs[3]
@@ -804,7 +806,7 @@ def run_cpu_rehearsal(args, rank, world, dist):
     ranks = gather_ranks(dist, {"rank": rank, "wall_s": round(local_el, 6), "first_crc": int(out[0]),
                                 "launch_ms": launch_summary(local_ms)})
     c4 = None
-    if world > 1 and args.config == "c2" and not args.no_c4_leg:
+    if args.config == "c2" and not args.no_c4_leg:
         # the C4 leg's host stand-in: 4 x 1 MiB per rank (global ids as the C4 shard's)
         n4, cnt4 = 1 << 20, 4
         bufs4 = [datagen.stream_bytes(shard_seed_base(rank, CONFIGS["c4"]["count"]) + i, n4).tobytes()
@@ -919,7 +921,7 @@ def main(argv=None):
                    "frac": round(wl.bytes_per_step / (ms64 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
     c4 = None
-    if world > 1 and args.config == "c2" and not args.no_c4_leg:
+    if args.config == "c2" and not args.no_c4_leg:
         del wl
         torch.cuda.empty_cache()
         c4 = c4_leg(args, rank, world, device, stream, dist)

@@ -136,8 +136,8 @@ def test_world_size_must_match_gpus():
 
 
 def test_two_rank_line_carries_c4_leg():
-    """with --gpus N > 1 the C2 line (value, config.workload =
-    C2) also carries a `config_c4` sub-record for BASELINE configs[3] timed in
+    """the C2 line (value, config.workload = C2) also carries
+    a `config_c4` sub-record for BASELINE configs[3] timed in
     the same ranks after the C2 leg; each rank checksummed ITS part of the C4
     batch (global ids r*32768..)."""
     from photonlibos_amd import datagen
@@ -155,9 +155,13 @@ def test_two_rank_line_carries_c4_leg():
     # the C4 leg's value is its own bytes over its own slowest-rank time
     slow = max(p["wall_s"] for p in c4["per_rank"])
     assert c4["value"] == pytest.approx(2 * 2 * 4 * (1 << 20) / slow / (1 << 30), rel=0.05)
-    # and the one-GPU line has none (the driver's N = 1 run stays C2 only)
+    # the one-GPU line carries it too (the driver's 1/2/4/8 sweep measures
+    # C4 weak scaling), and --no-c4-leg drops it
     r1 = _run_bench("--gpus", "1", "--cpu-rehearsal", "--steps", "1", "--warmup", "0")
-    assert "config_c4" not in json.loads([ln for ln in r1.stdout.splitlines() if ln.startswith("{")][0])
+    one = json.loads([ln for ln in r1.stdout.splitlines() if ln.startswith("{")][0])
+    assert one["config_c4"]["buffers_total"] == 32768 and one["config"]["config"] == "c2"
+    r0 = _run_bench("--gpus", "2", "--cpu-rehearsal", "--steps", "1", "--warmup", "0", "--no-c4-leg")
+    assert "config_c4" not in json.loads([ln for ln in r0.stdout.splitlines() if ln.startswith("{")][0])
 
 
 def oracle_crc(data):
