@@ -37,8 +37,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <sys/prctl.h>
+
 #include <atomic>
 #include <chrono>
+#include <memory>
 #include <map>
 #include <tuple>
 #include <mutex>
@@ -1771,7 +1774,6 @@ struct RoutedStream {
     void* h;  // host address of the result area
     void* d;  // its device address
     uint32_t tag;  // last tag of a spin-waited call (crc32c_small_kernel slots)
-    hipEvent_t done;  // blocking-sync event: the wait after the spin window sleeps in the driver
 };
 std::mutex g_rs_mu;
 std::vector<RoutedStream*> g_rs_free;
@@ -1786,9 +1788,8 @@ int routed_lease(int dev, RoutedStream** out) {
                 return 0;
             }
     }
-    auto* r = new RoutedStream{dev, nullptr, nullptr, nullptr, 0, nullptr};
+    auto* r = new RoutedStream{dev, nullptr, nullptr, nullptr, 0};
     hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->done, hipEventBlockingSync | hipEventDisableTiming);
     // coherent: the small kernel's system-scope tag stores reach the host directly
     if (e == hipSuccess)
         e = hipHostMalloc(&r->h, 512, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
@@ -1796,7 +1797,6 @@ int routed_lease(int dev, RoutedStream** out) {
     if (e == hipSuccess) e = hipHostGetDevicePointer(&r->d, r->h, 0);
     if (e != hipSuccess) {
         if (r->h) (void)hipHostFree(r->h);
-        if (r->done) (void)hipEventDestroy(r->done);
         if (r->st) (void)hipStreamDestroy(r->st);
         delete r;
         return hip_fail(e, "routed stream");
@@ -1854,23 +1854,38 @@ int with_scratch(int dev, uint64_t bytes, void* h_out, uint64_t out_bytes, F f) 
 // would add microseconds to a 5 µs kernel. The poll is bounded so that a
 // routed call does not hold a Photon vCPU (rpc.cpp:379: coroutines share the
 // thread, thread/thread.h:511-520) for the whole of a long kernel:
-//   1. a call whose kernel is expected to run longer than the spin window
-//      (its bytes at the nominal rate below) first sleeps through all but
-//      the window (nanosleep; the CPU is free for other threads);
-//   2. then polls the tags with a pause between reads for at most the spin
-//      window (g_routed_wait, default 30 µs);
-//   3. then sleeps in the driver until the stream's work has finished
-//      (an event with hipEventBlockingSync recorded behind the kernel) and
-//      reads the tags once more; a stream that finished (or failed) without
-//      every tag returns its error.
+//   1. a call whose kernel is expected to run longer than the poll window
+//      (its bytes at a nominal 6.5 GB/ms) first sleeps through 80 % of that
+//      time (nanosleep with this thread's timer slack at 1 ns for the wait,
+//      restored after: the default 50 µs slack would add that much latency);
+//   2. then polls the tags with a pause between reads for at most the window
+//      (g_routed_wait, default 30 µs);
+//   3. then sleeps in 10 µs slices, reading the tags after each and asking
+//      the stream for errors every 10th; a stream that finished (or failed)
+//      without every tag returns its error.
+// (hipEventSynchronize on a hipEventBlockingSync event kept the thread 100 %
+// busy on ROCm 7.2, profiles/r05d_bench_extend.json: it is not used.)
 // photon_crc_set_routed_wait (tuning.h) changes the window and step 1.
-constexpr double kNominalBytesPerUs = 6.0e6;           // ~75 % of 8 TB/s: a long kernel's expected rate
+constexpr double kNominalBytesPerUs = 6.5e6;  // ~81 % of 8 TB/s: a long kernel's expected rate
 
 inline void cpu_relax() {
 #if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
     __builtin_ia32_pause();
 #endif
 }
+
+// This thread's timer slack at 1 ns while it lives (PR_SET_TIMERSLACK is per
+// thread; the caller's value is restored).
+struct FineSleep {
+    long prev = -1;
+    FineSleep() {
+        prev = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+        if (prev > 1) (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
+    }
+    ~FineSleep() {
+        if (prev > 1) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)prev, 0, 0, 0);
+    }
+};
 
 // Wait until the `per` tagged words of each of `n` workgroups (slots w[per
 // b + h]) carry `tag`; x[h] = XOR of their low words. `bytes`: the call's
@@ -1889,21 +1904,33 @@ int wait_tagged(RoutedStream* r, uint32_t tag, uint32_t n, uint32_t* x, uint32_t
         return done == total;
     };
     const uint32_t pol = g_routed_wait.load(std::memory_order_relaxed);
-    const auto spin = std::chrono::microseconds(pol & 0xffffu);
+    const uint32_t spin_us = pol & 0xffffu;
     const double expect_us = (double)bytes / kNominalBytesPerUs;
-    if ((pol >> 16) && expect_us > (double)(pol & 0xffffu) + 20.0)
-        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(expect_us - (double)(pol & 0xffffu))));
+    if (scan()) return 0;
+    std::unique_ptr<FineSleep> fine;
+    if ((pol >> 16) && expect_us > (double)spin_us + 20.0) {
+        fine.reset(new FineSleep);
+        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(0.8 * expect_us)));
+    }
     const auto t0 = clk::now();
     while (!scan()) {
-        if (clk::now() - t0 > spin) break;
+        if (clk::now() - t0 > std::chrono::microseconds(spin_us)) break;
         for (int k = 0; k < 8; ++k) cpu_relax();
     }
     if (done == total) return 0;
-    hipError_t e = hipEventRecord(r->done, r->st);
-    if (e == hipSuccess) e = hipEventSynchronize(r->done);
-    if (e != hipSuccess) (void)hipStreamSynchronize(r->st);  // nothing left running on a returned stream
-    if (scan()) return 0;
-    return hip_fail(e != hipSuccess ? e : hipErrorUnknown, what);
+    if (!fine) fine.reset(new FineSleep);
+    for (uint32_t slice = 1;; ++slice) {
+        std::this_thread::sleep_for(std::chrono::microseconds(10));
+        if (scan()) return 0;
+        if (slice % 10 == 0) {
+            const hipError_t q = hipStreamQuery(r->st);
+            if (q == hipErrorNotReady) continue;
+            // finished (or failed) without every tag seen yet: a last look, then its verdict
+            if (scan()) return 0;
+            const hipError_t e = hipStreamSynchronize(r->st);
+            return hip_fail(e != hipSuccess ? e : (q != hipSuccess ? q : hipErrorUnknown), what);
+        }
+    }
 }
 
 int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_out) {

@@ -16,6 +16,9 @@
 #ifndef PCRC_LONG_LEAD
 #define PCRC_LONG_LEAD true  // long kernels: lead rows + partial row preloaded (A/B: false)
 #endif
+#ifndef PCRC_LONG_MERGE_HEAD
+#define PCRC_LONG_MERGE_HEAD 0  // long kernels: the head read with body chunk 0 (A/B: 1)
+#endif
 #ifndef PCRC_BATCH_LEAD
 #define PCRC_BATCH_LEAD false  // the same in the buffer batch (A/B: true)
 #endif
@@ -1137,11 +1140,30 @@ __device__ __forceinline__ uint32_t mul_lanes(uint32_t v, uint32_t bw, uint32_t 
     return group_xor<32>(((v >> l32) & 1u) ? bw : 0u);
 }
 
-// The bytes of slot v: [*p, *p + *n) and the seed (empty slots: 0 bytes).
+// The bytes of slot v: [*p, *p + *n) (empty slots: 0 bytes); *head: the
+// slot carries the head [data, A) and so the seed. With a body
+// (PCRC_LONG_MERGE_HEAD), the head is read as the front of body chunk 0's
+// slot -- [data, A + chunk) from the unaligned start -- instead of as slot D -
+// 1: the same algebra (crc(head | chunk0) = crc(head) X ^ crc(chunk0), and
+// the head's slot factor was X times chunk 0's), without round 3-4's extra
+// round -1 for group S - 1 when D = 0 (the reference's 1 GiB at buf+1).
 template <typename A>
-__device__ __forceinline__ void long_slot(const A& a, int64_t v, const uint8_t** p, uint64_t* n, bool* last) {
-    const int64_t t = v - a.lead;  // body chunk, or -1 for the head
+__device__ __forceinline__ void long_slot(const A& a, int64_t v, const uint8_t** p, uint64_t* n, bool* last,
+                                          bool* head) {
+    const int64_t t = v - a.lead;  // body chunk, or -1 for the head slot
     *last = t == a.nchunks - 1;
+    if (PCRC_LONG_MERGE_HEAD && a.nchunks > 0) {
+        *head = t == 0;
+        if (t < 0) {
+            *p = a.data;
+            *n = 0;
+        } else {
+            *p = t == 0 ? a.data : a.data + a.head + (uint64_t)t * a.chunk;
+            *n = (t == 0 ? a.head : 0) + (*last ? a.last : a.chunk);
+        }
+        return;
+    }
+    *head = t == -1;
     if (t == -1) {
         *p = a.data;
         *n = a.head;
@@ -1152,6 +1174,13 @@ __device__ __forceinline__ void long_slot(const A& a, int64_t v, const uint8_t**
         *p = a.data + a.head + (uint64_t)t * a.chunk;
         *n = *last ? a.last : a.chunk;
     }
+}
+
+// The first round of a launch: -1 when the head has a slot of its own before
+// group S - 1's first round (D = 0, head not merged).
+template <typename A>
+__device__ __forceinline__ int long_first_round(const A& a) {
+    return (a.lead == 0 && !(PCRC_LONG_MERGE_HEAD && a.nchunks > 0)) ? -1 : 0;
 }
 
 // Every wave: its workgroup's value (after the wave and workgroup factors),
@@ -1230,13 +1259,13 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
     asm volatile("" ::"v"(bw_z), "v"(bw_f));  // done before the chunk loop (crc64_long_run)
     uint32_t acc = 0, lastc = 0;
     // Rounds; a first round -1 when the head is slot -1 (D = 0: group S-1).
-    for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
+    for (int r = long_first_round(a); r < (int)a.rounds; ++r) {
         const int64_t v = g + (int64_t)r * S;
         const uint8_t* p;
         uint64_t n;
-        bool last;
-        long_slot(a, v, &p, &n, &last);
-        const uint32_t seed = v == a.lead - 1 ? a.seed : 0u;  // the head carries the seed
+        bool last, head;
+        long_slot(a, v, &p, &n, &last, &head);
+        const uint32_t seed = head ? a.seed : 0u;  // the head carries the seed
         uint32_t crc = 0;
         if (__ballot(n != 0 || seed != 0))  // a wave with only empty slots skips the round's loads
             crc = buffer_crc<G, U, PCRC_LONG_LEAD>(lds, p, n, seed, gl, la);

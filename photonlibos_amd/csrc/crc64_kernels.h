@@ -785,13 +785,12 @@ __device__ __forceinline__ void crc64_long_run(const Long64Args& a, const LaneCo
     asm volatile("" ::"v"(bw_z), "v"(bw_f), "v"(bx0), "v"(bx1));
     if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memrealtime();
     uint64_t acc = 0, lastc = 0;  // uniform across the group (reg and the lane XOR are)
-    for (int r = a.lead == 0 ? -1 : 0; r < (int)a.rounds; ++r) {
+    for (int r = long_first_round(a); r < (int)a.rounds; ++r) {
         const int64_t v = g + (int64_t)r * S;
         const uint8_t* p;
         uint64_t n;
-        bool last;
-        long_slot(a, v, &p, &n, &last);
-        const bool head = v == a.lead - 1;  // the head carries the (inverted) seed
+        bool last, head;  // the head carries the (inverted) seed
+        long_slot(a, v, &p, &n, &last, &head);
         uint64_t reg = 0;
         if (__ballot(n != 0 || head)) {
             reg = buffer_reg64<G>(lds, p, n, head ? ~a.seed : 0ull, gl, lane, la);  // valid on gl == 0
