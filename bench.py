@@ -630,7 +630,7 @@ def run_extend(args, stream):
     # the calling thread's CPU time (CLOCK_THREAD_CPUTIME_ID) over >= 0.3 s of
     # back-to-back calls each, for spin windows / sleep-ahead on and off.
     policies = {}
-    for spin_us, ahead in ((30, True), (30, False), (0, False), (100, True), (1000, False)):
+    for spin_us, ahead in ((40, True), (30, True), (0, False), (100, True), (1000, False)):
         ck.set_routed_wait(spin_us, ahead)
         row = {}
         for label, nb in (("128KiB", 128 << 10), ("1GiB", n)):
@@ -644,7 +644,7 @@ def run_extend(args, stream):
                           "thread_cpu_frac": round((time.thread_time() - c0) / (time.perf_counter() - w0), 3),
                           "calls": len(lat)}
         policies[f"spin{spin_us}{'_sleep_ahead' if ahead else ''}"] = row
-    ck.set_routed_wait(30, True)
+    ck.set_routed_wait(40, True)
     ck.set_device_dispatch(False)
     hbuf = np.frombuffer(d[:1024 * 4096].cpu().numpy().tobytes(), np.uint8)
     base = hbuf.ctypes.data

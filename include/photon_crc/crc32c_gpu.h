@@ -202,7 +202,7 @@ int photon_crc32c_extend_spans(const photon_crc_span* spans, int nspans, uint32_
  * calling thread (a photon vCPU: its coroutines wait with it) does not spin
  * through a long kernel: a call whose bytes would take longer than the poll
  * window first sleeps through most of its expected time, then polls the
- * result words with a pause between reads for at most 30 us, then sleeps in
+ * result words with a pause between reads for at most 40 us, then sleeps in
  * 10 us slices between reads (photon_crc_set_routed_wait, tuning.h). Off (the
  * default, also at load time) restores the host engines. The reference signatures have no error channel and the reference
  * always computes (crc.cpp:114-117), so a routed call whose device work

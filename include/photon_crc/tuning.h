@@ -66,10 +66,10 @@ int photon_crc64_set_full_rows(int mode, int rows_per_step);
 
 /* Routed drop-in calls (photon_crc_set_device_dispatch) collect their result
  * by polling tagged words in pinned memory for at most `spin_us` microseconds
- * (default 30, with a pause between reads), then sleep in 10 us slices,
+ * (default 40, with a pause between reads), then sleep in 10 us slices,
  * reading the words after each; with sleep_ahead != 0 (the default) a call
  * whose bytes at a nominal 6.5 GB/ms would take longer than the window first
- * sleeps through 80 % of that time. spin_us = 0: no polling window. */
+ * sleeps through 85 % of that time. spin_us = 0: no polling window. */
 int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
 
 /* Lanes per buffer the engine picks for buffers of typical length n (the

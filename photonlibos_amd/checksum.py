@@ -515,7 +515,7 @@ def set_long_shape(lanes=0, rounds=0):
     _check(lib().photon_crc_set_long_shape(lanes, rounds))
 
 
-def set_routed_wait(spin_us=30, sleep_ahead=True):
+def set_routed_wait(spin_us=40, sleep_ahead=True):
     """Routed drop-in calls: tag-polling window in µs, then a blocking wait;
     sleep_ahead: long calls sleep through their expected time first (tuning)."""
     _check(lib().photon_crc_set_routed_wait(spin_us, 1 if sleep_ahead else 0))

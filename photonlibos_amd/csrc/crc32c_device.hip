@@ -94,7 +94,7 @@ std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2
 // DESIGN.md §4.1).
 std::atomic<uint32_t> g_full64{2u << 4 | 3u};
 // Routed drop-in calls: spin window in µs | sleep-ahead << 16 (wait_tagged).
-std::atomic<uint32_t> g_routed_wait{30u | 1u << 16};
+std::atomic<uint32_t> g_routed_wait{40u | 1u << 16};
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -1855,16 +1855,19 @@ int with_scratch(int dev, uint64_t bytes, void* h_out, uint64_t out_bytes, F f) 
 // routed call does not hold a Photon vCPU (rpc.cpp:379: coroutines share the
 // thread, thread/thread.h:511-520) for the whole of a long kernel:
 //   1. a call whose kernel is expected to run longer than the poll window
-//      (its bytes at a nominal 6.5 GB/ms) first sleeps through 80 % of that
+//      (its bytes at a nominal 6.5 GB/ms) first sleeps through 85 % of that
 //      time (nanosleep with this thread's timer slack at 1 ns for the wait,
 //      restored after: the default 50 µs slack would add that much latency);
 //   2. then polls the tags with a pause between reads for at most the window
-//      (g_routed_wait, default 30 µs);
+//      (g_routed_wait, default 40 µs);
 //   3. then sleeps in 10 µs slices, reading the tags after each and asking
 //      the stream for errors every 10th; a stream that finished (or failed)
 //      without every tag returns its error.
 // (hipEventSynchronize on a hipEventBlockingSync event kept the thread 100 %
-// busy on ROCm 7.2, profiles/r05d_bench_extend.json: it is not used.)
+// busy on ROCm 7.2, repo:profiles/r05d_bench_extend.json: it is not used.
+// 1 GiB at buf+1, repo:profiles/r05e_bench_extend.json: pure spinning 172.0
+// µs at 100 % of a core; 80 % sleep + 30 µs window 180.2 µs at 20.9 %; 10 µs
+// slices only 178.0 µs at 12.7 %; 128 KiB 10.9-11.7 µs either way.)
 // photon_crc_set_routed_wait (tuning.h) changes the window and step 1.
 constexpr double kNominalBytesPerUs = 6.5e6;  // ~81 % of 8 TB/s: a long kernel's expected rate
 
@@ -1910,7 +1913,7 @@ int wait_tagged(RoutedStream* r, uint32_t tag, uint32_t n, uint32_t* x, uint32_t
     std::unique_ptr<FineSleep> fine;
     if ((pol >> 16) && expect_us > (double)spin_us + 20.0) {
         fine.reset(new FineSleep);
-        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(0.8 * expect_us)));
+        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(0.85 * expect_us)));
     }
     const auto t0 = clk::now();
     while (!scan()) {

@@ -17,7 +17,7 @@
 #define PCRC_LONG_LEAD true  // long kernels: lead rows + partial row preloaded (A/B: false)
 #endif
 #ifndef PCRC_LONG_MERGE_HEAD
-#define PCRC_LONG_MERGE_HEAD 0  // long kernels: the head read with body chunk 0 (A/B: 1)
+#define PCRC_LONG_MERGE_HEAD 1  // long kernels: the head read with body chunk 0 (A/B: 0)
 #endif
 #ifndef PCRC_BATCH_LEAD
 #define PCRC_BATCH_LEAD false  // the same in the buffer batch (A/B: true)

@@ -292,13 +292,13 @@ def test_routed_long_call_cpu_use(torch_dev, oracle):
         assert cpu < 0.25 * wall, (cpu, wall, calls)
         small = dbuf[5:5 + 100000].cpu().numpy()
         want_small = oracle.crc32c(small, 9)
-        for spin_us, ahead in ((0, False), (0, True), (30, False), (1000, True), (30, True)):
+        for spin_us, ahead in ((0, False), (0, True), (40, False), (1000, True), (40, True)):
             ck.set_routed_wait(spin_us, ahead)
             assert ck.crc32c_extend_at(dbuf.data_ptr() + 1, n, 0x77) == want, (spin_us, ahead)
             assert ck.crc32c_extend_at(dbuf.data_ptr() + 5, 100000, 9) == want_small, (spin_us, ahead)
             assert ck.crc64ecma_extend_at(dbuf.data_ptr() + 5, 100000, 9) == oracle.crc64ecma(small, 9)
     finally:
-        ck.set_routed_wait(30, True)
+        ck.set_routed_wait(40, True)
         ck.set_device_dispatch(False)
     assert ck.dispatch_fallbacks() == 0
 

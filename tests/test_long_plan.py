@@ -57,32 +57,41 @@ def _plan(addr, n, cus, lanes=0, rounds=0, crc64=False):
     return p
 
 
-def _replay(p, data, seed, oracle, crc64=False):
-    """The kernels' combine over `data` (bytes at the plan's address)."""
+def _replay(p, data, seed, oracle, crc64=False, merge_head=True):
+    """The kernels' combine over `data` (bytes at the plan's address).
+    merge_head (the product, PCRC_LONG_MERGE_HEAD): with a body, the head is
+    read as the front of body chunk 0's slot; else it has slot D - 1 (round
+    -1 of group S - 1 when D = 0). Both give the CRC."""
     width = 64 if crc64 else 32
     head, chunk, T, L, R, grid, S, D = (p[k] for k in ("head", "chunk", "T", "L", "R", "grid", "S", "D"))
     gpw = 64 // p["lanes"]
     assert R * S - T == D and 0 <= D and S == grid * 16 * gpw and grid <= 256
     assert T == 0 or (T - 1) * chunk + L == len(data) - head
+    merged = merge_head and T > 0
+
+    def raw(seg, s):
+        if crc64:  # the raw register: starts at ~seed (0 for a body chunk: ~all-ones), not inverted at the end
+            return oracle.crc64ecma(seg, s if s is not None else 0xFFFFFFFFFFFFFFFF) ^ 0xFFFFFFFFFFFFFFFF
+        return oracle.crc32c(seg, s or 0)
 
     def slot_crc(v):
         t = v - D
-        if t == -1:  # the head, with the seed (CRC-64: the register starts at ~seed)
-            seg = data[:head]
-            if crc64:
-                return oracle.crc64ecma(seg, seed) ^ 0xFFFFFFFFFFFFFFFF  # the raw register
-            return oracle.crc32c(seg, seed)
-        if t < 0:
+        if merged:
+            if t < 0:
+                return 0
+            if t == 0:  # the head, with the seed, then body chunk 0
+                return raw(data[:head + (L if T == 1 else chunk)], seed)
+        elif t == -1:  # the head, with the seed (CRC-64: the register starts at ~seed)
+            return raw(data[:head], seed)
+        elif t < 0:
             return 0
         seg = data[head + t * chunk: head + t * chunk + (L if t == T - 1 else chunk)]
-        if crc64:
-            return oracle.crc64ecma(seg, 0xFFFFFFFFFFFFFFFF) ^ 0xFFFFFFFFFFFFFFFF  # register from 0
-        return oracle.crc32c(seg, 0)
+        return raw(seg, None)
 
     accs, lasts = [], []
     for g in range(S):
         acc = lastc = 0
-        for r in range(-1 if D == 0 else 0, R):
+        for r in range(-1 if (D == 0 and not merged) else 0, R):
             v = g + r * S
             c = slot_crc(v)
             m = _mul_basis(acc, p["xsb"])
@@ -126,7 +135,9 @@ def test_long_plan_replays_to_the_crc(oracle, shape, cus):
         p = _plan(addr_off, n, cus, lanes, rounds)
         data = buf[addr_off:addr_off + n]
         assert p["head"] == (-addr_off) % 4096
-        assert _replay(p, data, seed, oracle) == oracle.crc32c(data, seed), (shape, cus, addr_off, n, p["D"])
+        for merge in (True, False):
+            assert _replay(p, data, seed, oracle, merge_head=merge) == oracle.crc32c(data, seed), \
+                (shape, cus, addr_off, n, p["D"], merge)
 
 
 @pytest.mark.parametrize("shape", [(0, 0), (64, 2), (32, 2)])
@@ -141,14 +152,18 @@ def test_long_plan_replays_crc64(oracle, shape):
         seed = (0x9E3779B97F4A7C15 * (k + 1)) & 0xFFFFFFFFFFFFFFFF
         p = _plan(addr_off, n, 2, lanes, rounds, crc64=True)
         data = buf[addr_off:addr_off + n]
-        assert _replay(p, data, seed, oracle, crc64=True) == oracle.crc64ecma(data, seed), (shape, addr_off, n)
+        for merge in (True, False):
+            assert _replay(p, data, seed, oracle, crc64=True, merge_head=merge) == oracle.crc64ecma(data, seed), \
+                (shape, addr_off, n, merge)
 
 
 def test_reference_perf_shape_is_balanced():
     """1 GiB at buf+1 on 256 CUs (the automatic 32 lanes x 2 rounds): no empty
-    slot, the head and the short last chunk share one group's last slot, so
-    every lane group reads exactly 2 x 64 KiB (round 3's cut: 130 KiB for most
-    groups, 65 KiB for 250 of them); CRC-64 takes the same shape."""
+    slot and head + short last chunk = one chunk, so every lane group reads 2 x
+    64 KiB but the two holding chunk 0 (head in front: + 4095 B) and the last
+    chunk (- 4095 B); round 4 gave group S - 1 the head as an extra round -1
+    (round 3's cut: 130 KiB for most groups, 65 KiB for 250 of them); CRC-64
+    takes the same shape."""
     p = _plan(4096 * 100 + 1, 1 << 30, 256)
     assert (p["lanes"], p["R"], p["grid"]) == (32, 2, 256)
     assert p["chunk"] == 64 << 10 and p["D"] == 0 and p["T"] == p["R"] * p["S"]
