@@ -645,6 +645,22 @@ def run_extend(args, stream):
                           "calls": len(lat)}
         policies[f"spin{spin_us}{'_sleep_ahead' if ahead else ''}"] = row
     ck.set_routed_wait(40, True)
+    # The resident small-buffer service (photon_crc_set_small_service, opt-in):
+    # the same 128 KiB call with no launch per call (the first call of a launch
+    # takes the launch path and is not timed); and its thread CPU time.
+    ck.set_small_service(20000)
+    ok = ok and ck.crc32c_extend_at(d.data_ptr() + 1, 128 << 10, 0) == want
+    svc0 = ck.small_service_stats()
+    svc = []
+    c0, w0 = time.thread_time(), time.perf_counter()
+    for _ in range(400):
+        t0 = time.perf_counter()
+        r = ck.crc32c_extend_at(d.data_ptr() + 1, 128 << 10, 0)
+        svc.append(time.perf_counter() - t0)
+        ok = ok and r == want
+    svc_cpu = (time.thread_time() - c0) / (time.perf_counter() - w0)
+    svc1 = ck.small_service_stats()
+    ck.set_small_service(0)
     ck.set_device_dispatch(False)
     hbuf = np.frombuffer(d[:1024 * 4096].cpu().numpy().tobytes(), np.uint8)
     base = hbuf.ctypes.data
@@ -683,6 +699,10 @@ def run_extend(args, stream):
     res["routed_crc32c_extend_128KiB_device_us_median"] = round(float(np.median(routed)) * 1e6, 1)
     res["routed_crc32c_extend_1GiB_device_us_median"] = round(float(np.median(routed_1g)) * 1e6, 1)
     res["routed_wait_policies"] = policies
+    res["routed_crc32c_extend_128KiB_service"] = {
+        "us_median": round(float(np.median(svc)) * 1e6, 1), "us_p10": round(float(np.percentile(svc, 10)) * 1e6, 1),
+        "us_p90": round(float(np.percentile(svc, 90)) * 1e6, 1), "thread_cpu_frac": round(svc_cpu, 3),
+        "served": svc1[0] - svc0[0], "calls": len(svc), "starts": svc1[1] - svc0[1]}
     res["host_pointer_call_us"] = {"dispatch_off": round(off_us, 3), "dispatch_on": round(on_us, 3),
                                    "note": "C1 (1024 x 4 KiB host buffers) through crc32c_auto from Python "
                                            "ctypes; the difference is the per-call hipPointerGetAttributes probe"}

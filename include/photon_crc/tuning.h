@@ -72,6 +72,23 @@ int photon_crc64_set_full_rows(int mode, int rows_per_step);
  * sleeps through 85 % of that time. spin_us = 0: no polling window. */
 int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
 
+/* Resident small-buffer service for routed crc32c_extend calls of up to 256
+ * KiB (device pointers, photon_crc_set_device_dispatch): idle_us > 0 keeps a
+ * launch of 32 workgroups (256 threads, 14 KiB of LDS each) on the device
+ * that polls a request word in pinned memory, so a call costs no kernel
+ * launch and no table load; the launch ends after idle_us without a request
+ * (and after 100 ms in any case; the next call starts a new one and itself
+ * takes the launch path). 0 (the default) = off, a launch per call; turning
+ * it off ends running launches. One call at a time uses it; concurrent
+ * calls take the launch path. While it runs, hipDeviceSynchronize() and
+ * anything else that waits for every stream of the device wait until it ends
+ * (at most idle_us after the last call), and the 32 workgroups hold their
+ * CUs' resources beside other kernels. DESIGN.md §4.0 has the latency. */
+int photon_crc_set_small_service(int idle_us);
+/* Routed small calls served by the service, launches of it, and calls that
+ * found it ending and took the launch path (tests). */
+int photon_crc_small_service_stats(uint64_t* served, uint64_t* starts, uint64_t* missed);
+
 /* Lanes per buffer the engine picks for buffers of typical length n (the
  * lane-group table of DESIGN.md §4, or the override when one is set). */
 int photon_crc_lanes_for(uint64_t nbytes);

@@ -521,6 +521,21 @@ def set_routed_wait(spin_us=40, sleep_ahead=True):
     _check(lib().photon_crc_set_routed_wait(spin_us, 1 if sleep_ahead else 0))
 
 
+def set_small_service(idle_us):
+    """Routed small crc32c_extend calls through a resident service launch that
+    ends after idle_us without a call; 0 = off (the default) (tuning)."""
+    _check(lib().photon_crc_set_small_service(int(idle_us)))
+
+
+def small_service_stats():
+    """(served, starts, missed): routed small calls the service served, its
+    launches, calls that found it ending (tests)."""
+    import ctypes
+    v = [ctypes.c_uint64(0) for _ in range(3)]
+    _check(lib().photon_crc_small_service_stats(*[ctypes.byref(x) for x in v]))
+    return tuple(x.value for x in v)
+
+
 def set_full_rows64(mode, rows_per_step=2):
     """CRC-64 whole-step uniform batches: 0 generic kernel, 1 full-row kernel,
     2 full-row kernel with cross-buffer prefetch, 3 automatic (the default:

@@ -95,6 +95,11 @@ std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2
 std::atomic<uint32_t> g_full64{2u << 4 | 3u};
 // Routed drop-in calls: spin window in µs | sleep-ahead << 16 (wait_tagged).
 std::atomic<uint32_t> g_routed_wait{40u | 1u << 16};
+// Resident small-buffer service (crc32c_small_service_kernel): idle time in
+// µs after which it ends, 0 = off (the default: launch per call).
+std::atomic<int> g_svc_idle_us{0};
+std::atomic<uint64_t> g_svc_served{0}, g_svc_starts{0}, g_svc_missed{0};
+void service_end_all();  // (below) end every running service launch
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -1012,6 +1017,20 @@ int photon_crc64_set_full_rows(int mode, int rows_per_step) {
 int photon_crc_set_routed_wait(int spin_us, int sleep_ahead) {
     if (spin_us < 0 || spin_us > 65535) return fail(-EINVAL, "spin window must be 0..65535 us");
     g_routed_wait.store((uint32_t)spin_us | (sleep_ahead ? 1u << 16 : 0u), std::memory_order_relaxed);
+    return 0;
+}
+
+int photon_crc_set_small_service(int idle_us) {
+    if (idle_us < 0 || idle_us > 1000000) return fail(-EINVAL, "service idle time must be 0..1000000 us");
+    g_svc_idle_us.store(idle_us, std::memory_order_relaxed);
+    if (idle_us == 0) service_end_all();  // idle times of running launches stay as they were started
+    return 0;
+}
+
+int photon_crc_small_service_stats(uint64_t* served, uint64_t* starts, uint64_t* missed) {
+    if (served) *served = g_svc_served.load(std::memory_order_relaxed);
+    if (starts) *starts = g_svc_starts.load(std::memory_order_relaxed);
+    if (missed) *missed = g_svc_missed.load(std::memory_order_relaxed);
     return 0;
 }
 
@@ -2039,6 +2058,178 @@ int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* cr
     return rc;
 }
 
+// The resident small-buffer service (crc32c_kernels.h
+// crc32c_small_service_kernel; opt-in, photon_crc_set_small_service). One
+// per device: a non-blocking stream, the pinned request / slot area, the
+// last seq posted. One call at a time uses it (try-lock: a call that finds
+// it busy, or not running, takes the launch path, routed_small); the first
+// call after it ended starts a new launch and itself takes the launch path
+// while the service loads its tables.
+struct SmallService {
+    std::mutex mu;
+    hipStream_t st = nullptr;
+    uint64_t* h = nullptr;     // host view of the pinned area (quit, slots)
+    uint64_t* d = nullptr;     // its device view
+    uint64_t* bell = nullptr;  // the doorbell: uncached device memory (large BAR: the host writes it
+                               // through the BAR at the same address) or the pinned area (h / d)
+    uint64_t* bell_d = nullptr;
+    bool bar = false;
+    uint32_t seq = 0;          // last seq posted (never 0)
+    bool live = false;         // a launch that has not been seen to end
+};
+
+// Doorbell words from the host; the BAR mapping is write-combined: the
+// stores leave the CPU at the sfence.
+inline void bell_put(SmallService* s, uint32_t i, uint64_t v) { __atomic_store_n(&s->bell[i], v, __ATOMIC_RELAXED); }
+inline void bell_flush() { __builtin_ia32_sfence(); }
+PerDevice<SmallService*> g_svc;
+std::mutex g_svc_list_mu;
+std::vector<SmallService*> g_svc_list;
+constexpr uint32_t kSvcLifeTicks = 10000000u;  // 100 ms of the 100 MHz clock, then a new launch
+
+// Tell a live service to end and wait for its waves (caller holds s->mu).
+void service_end(SmallService* s) {
+    if (!s->live) return;
+    bell_put(s, kSvcStop, 1ull);
+    bell_flush();
+    (void)hipStreamSynchronize(s->st);
+    s->live = false;
+}
+
+void service_end_all() {
+    std::lock_guard<std::mutex> lk(g_svc_list_mu);
+    for (SmallService* s : g_svc_list) {
+        std::lock_guard<std::mutex> l2(s->mu);
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        int dev = -1;
+        if (hipStreamGetDevice(s->st, &dev) == hipSuccess) (void)hipSetDevice(dev);
+        service_end(s);
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+}
+
+int service_get(int dev, SmallService** out) {
+    return g_svc.get(dev, out, [](int, SmallService*& slot) {
+        auto* s = new SmallService;
+        const hipError_t e = relaxed_capture([&] {
+            hipError_t r = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking);
+            if (r == hipSuccess)
+                r = hipHostMalloc(reinterpret_cast<void**>(&s->h), 8 * kSvcWords + (PCRC_SVC_STAMP ? 128 * kSmallWg : 0),
+                                  hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
+            if (r == hipSuccess) r = hipHostGetDevicePointer(reinterpret_cast<void**>(&s->d), s->h, 0);
+            int dev = 0, large_bar = 0;
+            if (r == hipSuccess) r = hipGetDevice(&dev);
+            if (r == hipSuccess && hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) == hipSuccess &&
+                large_bar == 1 &&
+                hipExtMallocWithFlags(reinterpret_cast<void**>(&s->bell), 4096, hipDeviceMallocUncached) == hipSuccess) {
+                s->bar = true;  // host stores through the BAR at the device address
+                s->bell_d = s->bell;
+                r = hipMemset(s->bell, 0, 4096);
+            } else {
+                (void)hipGetLastError();
+                s->bell = nullptr;
+            }
+            return r;
+        });
+        if (e != hipSuccess) {
+            if (s->bell) (void)hipFree(s->bell);
+            if (s->h) (void)hipHostFree(s->h);
+            if (s->st) (void)hipStreamDestroy(s->st);
+            delete s;
+            return hip_fail(e, "small-buffer service");
+        }
+        memset(s->h, 0, 8 * kSvcWords + (PCRC_SVC_STAMP ? 128 * kSmallWg : 0));
+        if (!s->bar) {
+            s->bell = s->h;
+            s->bell_d = s->d;
+        }
+        std::lock_guard<std::mutex> lk(g_svc_list_mu);
+        if (g_svc_list.empty()) atexit(service_end_all);  // after HIP's init: runs before its teardown
+        g_svc_list.push_back(s);
+        slot = s;
+        return 0;
+    });
+}
+
+// Serve one routed small call through the service: 0 = *crc_out is the CRC,
+// 1 = not served (take the launch path).
+int service_small(int dev, const SmallArgs& sa, uint32_t* crc_out) {
+    const int idle_us = g_svc_idle_us.load(std::memory_order_relaxed);
+    if (idle_us <= 0) return 1;
+    SmallService* s = nullptr;
+    if (service_get(dev, &s)) return 1;
+    std::unique_lock<std::mutex> lk(s->mu, std::try_to_lock);
+    if (!lk.owns_lock()) return 1;
+    volatile uint64_t* h = s->h;
+    if (s->live && h[kSvcQuit]) {  // it ended itself (idle / life): its waves leave at their next poll
+        (void)hipStreamSynchronize(s->st);
+        s->live = false;
+    }
+    if (!s->live) {
+        const uint32_t* img = nullptr;
+        if (small_image(dev, &img)) return 1;
+        bell_put(s, kSvcStop, 0ull);
+        bell_put(s, kSvcQuit, 0ull);
+        bell_flush();
+        __atomic_store_n(&s->h[kSvcQuit], 0ull, __ATOMIC_RELAXED);
+        ServiceArgs a{img, s->bell_d, s->d, s->seq, 100u * (uint32_t)idle_us, kSvcLifeTicks};
+        const hipError_t e = relaxed_capture([&] {
+            hipLaunchKernelGGL(crc32c_small_service_kernel, dim3(kSmallWg), dim3(256), 0, s->st, a);
+            return hipGetLastError();
+        });
+        if (e == hipSuccess) {
+            s->live = true;
+            g_svc_starts.fetch_add(1, std::memory_order_relaxed);
+        }
+        return 1;
+    }
+    uint32_t seq = s->seq + 1u;
+    if (seq == 0) seq = 1;
+    s->seq = seq;
+    const uint64_t tag = (uint64_t)seq << 32;
+    const uint64_t f[5] = {(uint32_t)reinterpret_cast<uintptr_t>(sa.a0),
+                           (uint32_t)(reinterpret_cast<uintptr_t>(sa.a0) >> 32),
+                           sa.nb | sa.s0 << 16 | sa.k << 20 | sa.wg0 << 25, sa.eoff, sa.seed};
+    for (uint32_t i = 0; i < 5; ++i) bell_put(s, i, tag | f[i]);
+    bell_flush();
+    const uint32_t n = kSmallWg - sa.wg0;
+    uint32_t done = 0, x = 0;
+    auto scan = [&] {
+        while (done < n) {
+            const uint64_t v = h[kSvcSlots + kSvcSlotStride * (sa.wg0 + done)];
+            if ((v >> 32) != seq) break;
+            x ^= (uint32_t)v;
+            ++done;
+        }
+        return done == n;
+    };
+    // as wait_tagged: a pause-polled window, then 10 µs sleeps; a service seen
+    // to end (quit set, or its stream done) without every slot: not served
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const uint32_t spin_us = g_routed_wait.load(std::memory_order_relaxed) & 0xffffu;
+    std::unique_ptr<FineSleep> fine;
+    while (!scan()) {
+        if (clk::now() - t0 < std::chrono::microseconds(spin_us)) {
+            for (int j = 0; j < 8; ++j) cpu_relax();
+            continue;
+        }
+        if (!fine) fine.reset(new FineSleep);
+        std::this_thread::sleep_for(std::chrono::microseconds(10));
+        if (h[kSvcQuit] || hipStreamQuery(s->st) != hipErrorNotReady) {
+            (void)hipStreamSynchronize(s->st);  // every wave has left: the slots are final
+            s->live = false;
+            if (scan()) break;
+            g_svc_missed.fetch_add(1, std::memory_order_relaxed);
+            return 1;
+        }
+    }
+    g_svc_served.fetch_add(1, std::memory_order_relaxed);
+    *crc_out = x;
+    return 0;
+}
+
 uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     const int dev = n ? device_of(p) : -1;
     if (dev < 0) return host_engine(&g_host_crc)(p, n, crc);
@@ -2048,7 +2239,7 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     uint32_t sgrid = 0;
     int rc;
     if (small_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, XORed here
-        rc = routed_small(dev, sa, sgrid, &r);
+        rc = service_small(dev, sa, &r) == 0 ? 0 : routed_small(dev, sa, sgrid, &r);
     } else {
         rc = routed_long(dev, p, n, crc, &r);
     }
@@ -2179,3 +2370,14 @@ extern "C" int photon_crc_set_device_dispatch(int on) {
 }
 
 extern "C" uint64_t photon_crc_dispatch_fallbacks(void) { return pcrc::g_fallbacks.load(); }
+
+#if PCRC_SVC_STAMP
+// bench-only builds: the current device's service area (host view)
+extern "C" void* photon_crc_test_service_area(void) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    pcrc::SmallService* s = nullptr;
+    return pcrc::service_get(dev, &s) ? nullptr : s->h;
+}
+#endif
+

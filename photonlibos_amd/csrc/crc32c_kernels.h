@@ -35,6 +35,9 @@
 #ifndef PCRC_SHIFT_INIT
 #define PCRC_SHIFT_INIT 1
 #endif
+#ifndef PCRC_SVC_STAMP
+#define PCRC_SVC_STAMP 0  // bench-only builds: s_memrealtime stamps of each small-buffer service request
+#endif
 
 namespace pcrc {
 
@@ -1380,6 +1383,108 @@ __device__ __forceinline__ uint32_t tail_word(uint32_t w, int off, int eoff) {
     return mc == 4 ? w : w & (uint32_t)((1ull << (8 * mc)) - 1ull);
 }
 
+// Steps 2-3 of one wave's share (blocks w[] loaded for virtual lane vt, the
+// tables at lds): the column, the shift to the end of the wave and the
+// wave's factor (bw_wave): the wave's value, on every lane.
+__device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const uint32_t* lds,
+                                                     const uint4 (&w)[kSmallRows], uint32_t vt, uint32_t bw_wave,
+                                                     uint64_t* ts = nullptr) {
+    auto stamp = [&](int i, uint32_t dep) {  // bench-only builds (PCRC_SVC_STAMP): time after `dep` is known
+        if (PCRC_SVC_STAMP && ts) {
+            asm volatile("" ::"v"(dep));
+            ts[i] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    const uint32_t lane = threadIdx.x & 63u, l32 = lane & 31u;
+    // uniform (a scalar branch below): rows past the last are not computed
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
+    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;  // this thread's block in row 0
+    // 2. The column: lagged blocks (independent per row) and the row shift.
+    // A wave64 VALU instruction takes 4 cycles on a SIMD16: at 1-3 rows per
+    // thread the column is most of a small call's device time, so a row that
+    // does not exist costs nothing (PCRC_SVC_STAMP probe: 1.0 µs for 3 rows).
+    uint32_t c[kSmallRows];
+#pragma unroll
+    for (int r = 0; r < (int)kSmallRows; ++r) {
+        c[r] = 0;
+        if ((uint32_t)r >= rows) continue;
+        const int b = first + r * (int)kSmallLanes;
+        uint4 v = w[r];
+        if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + seed
+            const int off = b * 16;
+            v.x = head_word_sel(tail_word(v.x, off, (int)a.eoff), off, (int)a.s0, a.seed);
+            v.y = head_word_sel(tail_word(v.y, off + 4, (int)a.eoff), off + 4, (int)a.s0, a.seed);
+            v.z = head_word_sel(tail_word(v.z, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.seed);
+            v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
+            if (b < 0) v = make_uint4(0, 0, 0, 0);
+        }
+        // lag16: D(D(D(w0) ^ w1) ^ w2) ^ w3 = w0 x^96 ^ w1 x^64 ^ w2 x^32 ^ w3
+        c[r] = xor3(nib_mul(lds + (kSmD + 2 * kNib) / 4, v.x), nib_mul(lds + (kSmD + kNib) / 4, v.y),
+                    nib_mul(lds + kSmD / 4, v.z)) ^ v.w;
+    }
+    stamp(8, c[0] ^ c[kSmallRows - 1]);
+    uint32_t q = c[0];
+#pragma unroll
+    for (int r = 1; r < (int)kSmallRows; ++r)
+        if ((uint32_t)r < rows) q = nib_mul(lds + kSmS / 4, q) ^ c[r];
+    stamp(9, q);
+    // 3. Q -> P and the shift to the end of the wave: x^(32 + 128 dl), then x^(1024 dh), d = 63 - lane.
+    const uint32_t d = 63u - lane, dh = d >> 3;
+    const uint32_t x = nib_mul(lds + (kSmA + (d & 7u) * kNib) / 4, q);
+    const uint32_t y = nib_mul(lds + (kSmB + (dh ? dh - 1u : 0u) * kNib) / 4, x);
+    stamp(10, y);
+    uint32_t v = group_xor<64>(dh ? y : x);
+    stamp(11, v);
+    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (127 - (4 wg + wave))): the wave to the end of the layout
+    stamp(12, v);
+    return v;
+}
+
+// The workgroup's value (small_wave_value of its 4 waves XORed, times the
+// tail factor bw_tail), valid on wave 0 (every lane); one barrier.
+__device__ __forceinline__ uint32_t small_value(const SmallArgs& a, const uint32_t* lds, const uint4 (&w)[kSmallRows],
+                                                uint32_t vt, uint32_t bw_wave, uint32_t bw_tail, uint32_t* red,
+                                                uint64_t* ts = nullptr) {
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_id(), l32 = lane & 31u;
+    const uint32_t v = small_wave_value(a, lds, w, vt, bw_wave, ts);
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    uint32_t u = 0;
+    if (wave == 0) {
+        u = red[0] ^ red[1] ^ red[2] ^ red[3];
+        u = mul_lanes(u, bw_tail, l32);  // x^(-8k): the zero bytes after the end (linear: per workgroup)
+    }
+    return u;
+}
+
+// This thread's blocks: only blocks that overlap the data are read (a block
+// at or past the end -- the seed's cover, n = 0 -- is all masked bytes, and
+// may lie on an unmapped page). COHERENT: agent-scope loads that
+// skip the CU's L1 (the resident service below reads buffers that other
+// launches rewrite between its requests); else nontemporal loads.
+template <bool COHERENT>
+__device__ __forceinline__ void small_load(const SmallArgs& a, uint32_t vt, uint4 (&w)[kSmallRows]) {
+    const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
+    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
+#pragma unroll
+    for (int r = 0; r < (int)kSmallRows; ++r) {
+        const int b = first + r * (int)kSmallLanes;
+        w[r] = make_uint4(0, 0, 0, 0);
+        if ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) {
+            const uint8_t* p = a.a0 + 16 * (uint32_t)b;
+            if constexpr (COHERENT) {
+                typedef __attribute__((address_space(1))) const uint64_t g_u64;  // global_, not flat_, loads
+                g_u64* q = (g_u64*)p;
+                const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                w[r] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+            } else {
+                w[r] = load16(p);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSmLds / 4];
     __shared__ uint32_t red[4];
@@ -1395,18 +1500,8 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
         const uint32_t j = (uint32_t)i * 256u + tid;
         tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
     }
-    const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
-    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;  // this thread's block in row 0
     uint4 w[kSmallRows];
-#pragma unroll
-    for (int r = 0; r < (int)kSmallRows; ++r) {
-        const int b = first + r * (int)kSmallLanes;
-        // only blocks that overlap the data are read: a block at or past the
-        // end (the seed's cover, n = 0) is all masked bytes, and may lie on an
-        // unmapped page
-        w[r] = ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) ? load16(a.a0 + 16 * (uint32_t)b)
-                                                                           : make_uint4(0, 0, 0, 0);
-    }
+    small_load<false>(a, vt, w);
     const uint32_t bw_wave = a.image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
     const uint32_t bw_tail = a.image[kSmTail / 4 + a.k * 32u + l32];
 #pragma unroll
@@ -1415,39 +1510,8 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
         if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
     }
     lds_barrier();
-    // 2. The column: lagged blocks (independent per row) and the row shift.
-    uint32_t c[kSmallRows];
-#pragma unroll
-    for (int r = 0; r < (int)kSmallRows; ++r) {
-        const int b = first + r * (int)kSmallLanes;
-        uint4 v = w[r];
-        if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + seed
-            const int off = b * 16;
-            v.x = head_word_sel(tail_word(v.x, off, (int)a.eoff), off, (int)a.s0, a.seed);
-            v.y = head_word_sel(tail_word(v.y, off + 4, (int)a.eoff), off + 4, (int)a.s0, a.seed);
-            v.z = head_word_sel(tail_word(v.z, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.seed);
-            v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
-            if (b < 0 || (uint32_t)r >= rows) v = make_uint4(0, 0, 0, 0);
-        }
-        // lag16: D(D(D(w0) ^ w1) ^ w2) ^ w3 = w0 x^96 ^ w1 x^64 ^ w2 x^32 ^ w3
-        c[r] = xor3(nib_mul(lds + (kSmD + 2 * kNib) / 4, v.x), nib_mul(lds + (kSmD + kNib) / 4, v.y),
-                    nib_mul(lds + kSmD / 4, v.z)) ^ v.w;
-    }
-    uint32_t q = c[0];
-#pragma unroll
-    for (int r = 1; r < (int)kSmallRows; ++r)
-        if ((uint32_t)r < rows) q = nib_mul(lds + kSmS / 4, q) ^ c[r];
-    // 3. Q -> P and the shift to the end of the wave: x^(32 + 128 dl), then x^(1024 dh), d = 63 - lane.
-    const uint32_t d = 63u - lane, dh = d >> 3;
-    const uint32_t x = nib_mul(lds + (kSmA + (d & 7u) * kNib) / 4, q);
-    const uint32_t y = nib_mul(lds + (kSmB + (dh ? dh - 1u : 0u) * kNib) / 4, x);
-    uint32_t v = group_xor<64>(dh ? y : x);
-    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (127 - (4 wg + wave))): the wave to the end of the layout
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
+    const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red);
     if (wave == 0) {
-        uint32_t u = red[0] ^ red[1] ^ red[2] ^ red[3];
-        u = mul_lanes(u, bw_tail, l32);  // x^(-8k): the zero bytes after the end (linear: per workgroup)
         if (a.slots) {
             if (lane == 0) {
                 if (a.tag)  // one 8-byte store: the host never sees a tag without its value
@@ -1459,6 +1523,162 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
         } else {
             long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
         }
+    }
+}
+
+// The resident small-buffer service (routed drop-in calls of <= 256 KiB,
+// opt-in: photon_crc_set_small_service). A launch of kSmallWg workgroups
+// that stays on the chip between calls: the tables and the basis words are
+// loaded ONCE, and a call costs no launch -- the host writes the request into
+// the doorbell, wave 0 of every workgroup polls it and hands it to its
+// workgroup through LDS, the workgroup computes its share of the layout
+// exactly as crc32c_small_kernel (small_value) and stores its tagged value
+// into its own slot in pinned host memory; the host XORs the slots. No
+// GPU-side ordering across workgroups is needed (the host collects). One slot
+// per workgroup, each on a 64-byte line of its own: 8-byte writes of 128
+// waves into 16 shared lines cost ~5 µs more at 128 KiB than 32 workgroup
+// slots (the host link serialises partial writes to one line).
+//
+// The doorbell (64-bit words; DEVICE memory the host writes through the PCIe
+// BAR on large-BAR systems -- the device polls it in 0.2-0.4 µs instead of
+// 1.2-2.8 µs over the host link, repo:scripts/probe_doorbell.hip -- else
+// pinned host memory):
+//   0-4  the request, each word {seq (high 32), field (low 32)}: a0 low, a0
+//        high, nb | s0 << 16 | k << 20 | wg0 << 25, eoff, seed. A request is
+//        taken when all five carry one seq that is not the last one served
+//        (the host writes the words in any order; a torn read retries);
+//   5    stop (host -> device): nonzero ends the service;
+//   6    quit: set by workgroup 0 when it ends the service (idle for `idle`
+//        ticks of the 100 MHz clock, or `life` ticks old), here for the other
+//        workgroups and in the pinned area's word 6 for the host, which then
+//        starts a new launch for later calls.
+// Pinned area: word 6 quit (above); 16 + 8 b: slot of workgroup b, {seq,
+// value}.
+// Every wave exits: workgroup 0 on stop / idle / life, the others on stop,
+// quit or 2 x life by their own clock (a workgroup 0 that never became
+// resident cannot keep them alive). The request's bytes are read with
+// agent-scope loads (small_load<true>): a buffer rewritten by another launch
+// since this one last read it must not come from this CU's L1.
+constexpr uint32_t kSvcStop = 5, kSvcQuit = 6, kSvcSlots = 16, kSvcSlotStride = 8;  // one 64-byte line per slot
+constexpr uint32_t kSvcWords = kSvcSlots + kSvcSlotStride * kSmallWg;
+constexpr uint32_t kSvcLds = kSmLds + 32u * 32u * 4u;  // the tables, then the tail basis words
+
+struct ServiceArgs {
+    const uint32_t* image;  // the small kernel's image (tables, wave and tail basis words)
+    uint64_t* bell;         // the doorbell (device view)
+    uint64_t* area;         // the pinned area (device view)
+    uint32_t last;          // the seq served last (by an earlier launch): not served again
+    uint32_t idle;          // ticks without a request before workgroup 0 ends the service
+    uint32_t life;          // ticks after which workgroup 0 ends it
+};
+
+__global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSvcLds / 4];
+    __shared__ uint32_t cmd[2][8];  // per poll parity: request words 0-4, seq, command
+    __shared__ uint32_t red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id(), l32 = lane & 31u;
+    const uint32_t wg = blockIdx.x, vt = wg * 256u + tid;
+    for (uint32_t j = tid; j < kSmLds / 16; j += 256u)
+        *reinterpret_cast<u32x4*>(lds + 4 * j) = *((const g_u32x4*)s.image + j);
+    for (uint32_t j = tid; j < 32u * 32u / 4u; j += 256u)
+        *reinterpret_cast<u32x4*>(lds + kSmLds / 4 + 4 * j) = *((const g_u32x4*)(s.image + kSmTail / 4) + j);
+    const uint32_t bw_wave = s.image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
+    __syncthreads();
+    uint32_t last = s.last;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t tl = t0;
+#if PCRC_SVC_STAMP
+    uint64_t st[16] = {};  // issue, seen, decoded, loaded, value, done (realtime); seen, done (shader cycles);
+                           // 8-12: inside small_wave_value
+#endif
+    for (uint32_t round = 0;; ++round) {
+        uint32_t* c = cmd[round & 1u];
+        if (wave == 0) {
+#if PCRC_SVC_STAMP
+            const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
+#endif
+            const uint64_t v = lane <= kSvcQuit ? __hip_atomic_load(s.bell + lane, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_SYSTEM)
+                                                : 0ull;
+            const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+            const bool same = lane >= 5 || (uint32_t)(v >> 32) == seq;
+            const bool fresh = __ballot(same) == ~0ull && seq != last;
+            const bool stop = __shfl(v, kSvcStop) != 0 || __shfl(v, kSvcQuit) != 0;
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            uint32_t cm = fresh ? 1u : 0u;
+            if (stop) {
+                cm = 2u;
+            } else if (!fresh) {
+                if (wg == 0 && (now - tl > s.idle || now - t0 > s.life)) {
+                    cm = 2u;
+                    if (lane == 0) {
+                        __hip_atomic_store(s.bell + kSvcQuit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(s.area + kSvcQuit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                } else if (now - t0 > 2ull * s.life) {
+                    cm = 2u;
+                }
+            }
+            if (fresh) {
+                last = seq;
+                tl = now;
+#if PCRC_SVC_STAMP
+                st[0] = t_issue;
+                st[1] = now;
+                st[6] = __builtin_amdgcn_s_memtime();
+#endif
+            }
+            if (lane < 5) c[lane] = (uint32_t)v;
+            if (lane == 0) {
+                c[5] = seq;
+                c[6] = cm;
+            }
+        }
+        __syncthreads();
+        const uint32_t cm = c[6];
+        if (cm == 2u) break;
+        if (cm == 0u) continue;
+        SmallArgs a{};
+        a.a0 = reinterpret_cast<const uint8_t*>((uint64_t)c[1] << 32 | c[0]);
+        a.nb = c[2] & 0xffffu;
+        a.s0 = (c[2] >> 16) & 15u;
+        a.k = (c[2] >> 20) & 31u;
+        a.wg0 = (c[2] >> 25) & 31u;
+        a.eoff = c[3];
+        a.seed = c[4];
+        if (wg < a.wg0) continue;  // no data in this workgroup's part of the layout
+#if PCRC_SVC_STAMP
+        st[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+        uint4 w[kSmallRows];
+        small_load<true>(a, vt, w);
+        const uint32_t bw_tail = lds[kSmLds / 4 + a.k * 32u + l32];
+#if PCRC_SVC_STAMP
+        __builtin_amdgcn_s_waitcnt(0);
+        st[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+#if PCRC_SVC_STAMP
+        const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red, st);
+#else
+        const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red);
+#endif
+#if PCRC_SVC_STAMP
+        if (wave == 0) {
+            asm volatile("" ::"v"(u));
+            st[4] = __builtin_amdgcn_s_memrealtime();
+            st[5] = __builtin_amdgcn_s_memrealtime();
+            st[7] = __builtin_amdgcn_s_memtime();
+            if (lane < 16) {
+                uint64_t x = st[0];
+#pragma unroll
+                for (int i = 1; i < 16; ++i) x = lane == (uint32_t)i ? st[i] : x;
+                __hip_atomic_store(s.area + kSvcWords + 16 * wg + lane, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+#endif
+        if (wave == 0 && lane == 0)
+            __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg, (uint64_t)c[5] << 32 | u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 

@@ -1,0 +1,163 @@
+"""The resident small-buffer service (photon_crc_set_small_service,
+crc32c_kernels.h crc32c_small_service_kernel): routed crc32c_extend calls of
+up to 256 KiB on device pointers served by a launch that stays on the chip,
+bit-exact against the pinned oracle (reference: crc32c.h:30-33,
+crc.cpp:339-358 -- the routed call returns what crc32c_extend returns).
+
+What can go wrong only with a resident launch is checked here: a buffer
+rewritten between two requests (by another kernel, by a host-to-device copy)
+must not be read from the service CU's caches; the service ends by itself
+after its idle time and the next call starts a new one; concurrent callers
+fall back to the launch path; turning it off ends it (a device-wide
+synchronise then returns at once)."""
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from photonlibos_amd import checksum as ck
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+@pytest.fixture(autouse=True)
+def _service(torch_dev):
+    ck.set_device_dispatch(True)
+    ck.set_small_service(20000)  # 20 ms idle: the whole test on one launch
+    yield
+    ck.set_small_service(0)
+    ck.set_device_dispatch(False)
+    assert ck.dispatch_fallbacks() == 0
+
+
+def _served():
+    return ck.small_service_stats()[0]
+
+
+def test_sizes_offsets_seeds(torch_dev, oracle):
+    """0 B .. 256 KiB at every offset mod 16, random seeds, the reference's
+    128 KiB at buf+1: every call equal to the oracle, (almost) all served by
+    the service (the first call of a launch takes the launch path; n = 0
+    stays on the host)."""
+    torch = torch_dev
+    n_max = 256 * 1024
+    host = np.random.default_rng(0x5E41).integers(0, 256, n_max + 64, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).cuda()
+    torch.cuda.synchronize()
+    base = dbuf.data_ptr()
+    rng = random.Random(7)
+    cases = [(1, 128 * 1024, 0), (0, 0, 0x1234), (3, 1, 5), (15, 3, 0xFFFFFFFF), (0, n_max, 9), (1, n_max - 1, 9)]
+    cases += [(rng.randrange(16), rng.choice([rng.randrange(64), rng.randrange(4096), rng.randrange(n_max - 15)]),
+               rng.getrandbits(32)) for _ in range(300)]
+    s0 = _served()
+    for off, n, seed in cases:
+        want = oracle.crc32c(host[off:off + n], seed)
+        assert ck.crc32c_extend_at(base + off, n, seed) == want, (off, n, seed)
+    served = _served() - s0
+    routed = sum(1 for c in cases if c[1] > 0)  # n = 0 never leaves the host (crc32c_extend returns the seed)
+    assert served >= routed - 1, (served, routed, ck.small_service_stats())
+
+
+def test_rewritten_buffer_is_read_fresh(torch_dev, oracle):
+    """One device buffer, rewritten between requests by a kernel on another
+    stream and by host-to-device copies, at the reference's 128 KiB at buf+1
+    and at 4 KiB (L1-sized): every CRC is of the new bytes (the service reads
+    with agent-scope loads, never this CU's stale L1)."""
+    torch = torch_dev
+    n = 128 * 1024
+    dbuf = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+    side = torch.cuda.Stream()
+    rng = np.random.default_rng(0xF2E5)
+    s0 = _served()
+    calls = 0
+    for it in range(120):
+        host = rng.integers(0, 256, n + 64, dtype=np.uint8)
+        # stream waits only: a device-wide synchronise would wait for the
+        # resident launch to end (tuning.h)
+        cur = torch.cuda.current_stream()
+        if it % 2:
+            dbuf.copy_(torch.from_numpy(host))  # host-to-device copy
+            cur.synchronize()
+        else:
+            src = torch.from_numpy(host).cuda()
+            cur.synchronize()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                dbuf.copy_(src)  # a kernel / copy on another stream
+            side.synchronize()
+        for off, length in ((1, n), (1 + 4096 * (it % 8), 4096), (0, 16)):
+            want = oracle.crc32c(host[off:off + length], it)
+            assert ck.crc32c_extend_at(dbuf.data_ptr() + off, length, it) == want, (it, off, length)
+            calls += 1
+    assert _served() - s0 >= calls - 2
+
+
+def test_idle_end_and_restart(torch_dev, oracle):
+    """A short idle time: the service ends after it, the next call starts a
+    new launch (and is itself served by the launch path), calls after that
+    are served again; turning the service off ends the running launch, so a
+    device-wide synchronise returns at once."""
+    torch = torch_dev
+    n = 100000
+    host = np.random.default_rng(3).integers(0, 256, n + 16, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).cuda()
+    torch.cuda.synchronize()
+    want = oracle.crc32c(host[3:3 + n], 77)
+    ck.set_small_service(300)  # launches from now on end 300 us after their last call
+    ck.set_small_service(0)    # ... and the running 20 ms one ends now
+    ck.set_small_service(300)
+    for _ in range(3):
+        srv0, st0, _ = ck.small_service_stats()
+        for _ in range(20):
+            assert ck.crc32c_extend_at(dbuf.data_ptr() + 3, n, 77) == want
+        srv1, st1, _ = ck.small_service_stats()
+        assert st1 >= st0 + 1 and srv1 >= srv0 + 18, (srv0, st0, srv1, st1)
+        time.sleep(0.005)  # > 300 us idle: the launch ends by itself
+    ck.set_small_service(20000)
+    assert ck.crc32c_extend_at(dbuf.data_ptr() + 3, n, 77) == want
+    assert ck.crc32c_extend_at(dbuf.data_ptr() + 3, n, 77) == want
+    ck.set_small_service(0)
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 0.01
+
+
+def test_concurrent_callers(torch_dev, oracle):
+    """8 threads of routed calls at once: one at a time uses the service, the
+    others take the launch path; every result equal to the oracle."""
+    torch = torch_dev
+    n_max = 256 * 1024
+    host = np.random.default_rng(11).integers(0, 256, n_max + 64, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).cuda()
+    torch.cuda.synchronize()
+    base = dbuf.data_ptr()
+    errors = []
+
+    def worker(t):
+        rng = random.Random(t)
+        try:
+            for _ in range(60):
+                off, n, seed = rng.randrange(16), rng.randrange(n_max - 15), rng.getrandbits(32)
+                got = ck.crc32c_extend_at(base + off, n, seed)
+                if got != oracle.crc32c(host[off:off + n], seed):
+                    errors.append((t, off, n, seed))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    s0 = _served()
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+    assert _served() > s0
