@@ -615,6 +615,7 @@ def run_extend(args, stream):
     # (default stream, synchronous), and the routing probe's price on host
     # pointers (C1: 1024 x 4 KiB).
     ck.set_device_dispatch(True)
+    ck.set_small_service(0)  # the launch path first (the service: below)
     routed = []
     for _ in range(50):
         t0 = time.perf_counter()
@@ -645,10 +646,11 @@ def run_extend(args, stream):
                           "calls": len(lat)}
         policies[f"spin{spin_us}{'_sleep_ahead' if ahead else ''}"] = row
     ck.set_routed_wait(40, True)
-    # The resident small-buffer service (photon_crc_set_small_service, opt-in):
-    # the same 128 KiB call with no launch per call (the first call of a launch
-    # takes the launch path and is not timed); and its thread CPU time.
-    ck.set_small_service(20000)
+    # The resident small-buffer services (photon_crc_set_small_service, the
+    # default, 200 us idle): the same 128 KiB calls with no launch per call
+    # (the first call of a launch takes the launch path and is not timed);
+    # the calling thread's CPU time.
+    ck.set_small_service(200)
     ok = ok and ck.crc32c_extend_at(d.data_ptr() + 1, 128 << 10, 0) == want
     svc0 = ck.small_service_stats()
     svc = []
@@ -660,7 +662,21 @@ def run_extend(args, stream):
         ok = ok and r == want
     svc_cpu = (time.thread_time() - c0) / (time.perf_counter() - w0)
     svc1 = ck.small_service_stats()
+    want64 = ck.crc64ecma_extend_at(d.data_ptr() + 1, 128 << 10, 0)  # starts the CRC-64 service
+    svc64 = []
+    for _ in range(400):
+        t0 = time.perf_counter()
+        r = ck.crc64ecma_extend_at(d.data_ptr() + 1, 128 << 10, 0)
+        svc64.append(time.perf_counter() - t0)
+        ok = ok and r == want64
     ck.set_small_service(0)
+    launch64 = []
+    for _ in range(100):
+        t0 = time.perf_counter()
+        r = ck.crc64ecma_extend_at(d.data_ptr() + 1, 128 << 10, 0)
+        launch64.append(time.perf_counter() - t0)
+        ok = ok and r == want64
+    ck.set_small_service(200)
     ck.set_device_dispatch(False)
     hbuf = np.frombuffer(d[:1024 * 4096].cpu().numpy().tobytes(), np.uint8)
     base = hbuf.ctypes.data
@@ -703,6 +719,8 @@ def run_extend(args, stream):
         "us_median": round(float(np.median(svc)) * 1e6, 1), "us_p10": round(float(np.percentile(svc, 10)) * 1e6, 1),
         "us_p90": round(float(np.percentile(svc, 90)) * 1e6, 1), "thread_cpu_frac": round(svc_cpu, 3),
         "served": svc1[0] - svc0[0], "calls": len(svc), "starts": svc1[1] - svc0[1]}
+    res["routed_crc64ecma_extend_128KiB_us_median"] = {
+        "service": round(float(np.median(svc64)) * 1e6, 1), "launch_path": round(float(np.median(launch64)) * 1e6, 1)}
     res["host_pointer_call_us"] = {"dispatch_off": round(off_us, 3), "dispatch_on": round(on_us, 3),
                                    "note": "C1 (1024 x 4 KiB host buffers) through crc32c_auto from Python "
                                            "ctypes; the difference is the per-call hipPointerGetAttributes probe"}

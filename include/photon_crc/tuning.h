@@ -75,11 +75,16 @@ int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
 /* Resident small-buffer service for routed crc32c_extend calls of up to 256
  * KiB (device pointers, photon_crc_set_device_dispatch): idle_us > 0 keeps a
  * launch of 32 workgroups (256 threads, 14 KiB of LDS each) on the device
- * that polls a request word in pinned memory, so a call costs no kernel
+ * that polls a request doorbell (device memory the host writes through the
+ * PCIe BAR; pinned memory without a large BAR), so a call costs no kernel
  * launch and no table load; the launch ends after idle_us without a request
  * (and after 100 ms in any case; the next call starts a new one and itself
- * takes the launch path). 0 (the default) = off, a launch per call; turning
- * it off ends running launches. One call at a time uses it; concurrent
+ * takes the launch path). Default 200 (or the environment variable
+ * PHOTON_CRC_SMALL_SERVICE at load); 0 = off, a launch per call; turning it
+ * off ends running launches. crc64ecma_extend has a service of its own (34
+ * KiB of LDS per workgroup). A library launch whose workgroups could not
+ * share a CU with a service's (the CRC-64 batch and long kernels, 158 KiB of
+ * LDS) ends the running services first. One call at a time uses it; concurrent
  * calls take the launch path. While it runs, hipDeviceSynchronize() and
  * anything else that waits for every stream of the device wait until it ends
  * (at most idle_us after the last call), and the 32 workgroups hold their

@@ -522,8 +522,9 @@ def set_routed_wait(spin_us=40, sleep_ahead=True):
 
 
 def set_small_service(idle_us):
-    """Routed small crc32c_extend calls through a resident service launch that
-    ends after idle_us without a call; 0 = off (the default) (tuning)."""
+    """Routed small crc32c_extend / crc64ecma_extend calls through a resident
+    service launch that ends after idle_us without a call; 0 = off, a launch
+    per call; default 200 or PHOTON_CRC_SMALL_SERVICE (tuning)."""
     _check(lib().photon_crc_set_small_service(int(idle_us)))
 
 

@@ -95,11 +95,25 @@ std::atomic<int> g_msg_mode{0};  // messages: 0 automatic, 1 one fused kernel, 2
 std::atomic<uint32_t> g_full64{2u << 4 | 3u};
 // Routed drop-in calls: spin window in µs | sleep-ahead << 16 (wait_tagged).
 std::atomic<uint32_t> g_routed_wait{40u | 1u << 16};
-// Resident small-buffer service (crc32c_small_service_kernel): idle time in
-// µs after which it ends, 0 = off (the default: launch per call).
-std::atomic<int> g_svc_idle_us{0};
+// Resident small-buffer services (crc32c_small_service_kernel,
+// crc64_small_service_kernel): idle time in µs after which a launch ends, 0
+// = off (a launch per routed call). Default 200 µs; the environment variable
+// PHOTON_CRC_SMALL_SERVICE (read at load) sets another value.
+constexpr int kSvcIdleDefault = 200;
+int svc_idle_from_env() {
+    const char* e = getenv("PHOTON_CRC_SMALL_SERVICE");
+    if (!e || !*e) return kSvcIdleDefault;
+    const long v = strtol(e, nullptr, 10);
+    return v < 0 ? 0 : v > 1000000 ? 1000000 : (int)v;
+}
+std::atomic<int> g_svc_idle_us{svc_idle_from_env()};
 std::atomic<uint64_t> g_svc_served{0}, g_svc_starts{0}, g_svc_missed{0};
 void service_end_all();  // (below) end every running service launch
+// (below) before a launch that needs `lds` bytes of LDS per workgroup: end
+// the running small-buffer services whose workgroups would keep it off
+// their CUs (their LDS + lds > 160 KiB)
+void svc_yield(uint32_t lds);
+constexpr uint32_t kWholeCu = 160u * 1024u;  // the CRC-64 batch / long kernels (158 KiB)
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -398,6 +412,16 @@ int batch_rows(int g) {
     return u >= 0 ? u : g == 16 ? 2 : 4;
 }
 
+uint32_t lds_for_lanes(int g) {
+    switch (g) {
+        case 64: return lds_bytes_for<64>();
+        case 32: return lds_bytes_for<32>();
+        case 16: return lds_bytes_for<16>();
+        case 8: return lds_bytes_for<8>();
+        default: return lds_bytes_for<4>();
+    }
+}
+
 // lanes: 0 = by typical_len (batch_lanes), else the lane-group size.
 int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, int lanes = 0) {
     if (a.count == 0) return 0;
@@ -412,6 +436,7 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
     if (const int cap = g_grid_cap.load(std::memory_order_relaxed)) grid = grid > (uint64_t)cap ? (uint64_t)cap : grid;
     const int rows_per_step = batch_rows(g);
     const LaneConsts& kc = lane_consts(g);
+    svc_yield(lds_for_lanes(g));
 #define LB(GG, UU) \
     hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc, pow_table())
 #define LBG(UU)                    \
@@ -468,6 +493,7 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     uint64_t grid = (waves + kWaves - 1) / kWaves;
     if (grid > (uint64_t)cus) grid = cus;
     const LaneConsts64& kc = lane_consts64(g);
+    svc_yield(kWholeCu);
     // Whole-step uniform batches: the full-row kernel (crc64_kernels.h).
     const uint32_t full = g_full64.load(std::memory_order_relaxed);
     const int fu = (int)(full >> 4);
@@ -1278,6 +1304,7 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
         uint64_t grid = ((nmsg + gpw - 1) / gpw + kWaves - 1) / kWaves;
         if (grid > (uint64_t)cus) grid = cus;
         const LaneConsts& kc = lane_consts(g);
+        svc_yield(lds_for_lanes(g));
 #define LM(GG, UU)                                                                                            \
     do {                                                                                                      \
         if (a.out)                                                                                            \
@@ -1455,6 +1482,7 @@ int extend64_device_long(const void* d_data, uint64_t nbytes, uint64_t seed, uin
     Long64Args a{};
     long_args64(&a, lp, pw, d_data, seed, d_out);
     a.out_tag = tag;
+    svc_yield(kWholeCu);
     return long_launch(st, lp.grid, "crc64_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint64_t*>(state);
         a.tbase = base;
@@ -1572,6 +1600,7 @@ int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint3
     LongArgs a{};
     long_args(&a, lp, pw, d_data, seed, d_out);
     a.out_tag = tag;
+    svc_yield(lds_for_lanes(lp.lanes));
     return long_launch(st, lp.grid, "crc32c_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint32_t*>(state);
         a.tbase = base;
@@ -2058,15 +2087,18 @@ int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* cr
     return rc;
 }
 
-// The resident small-buffer service (crc32c_kernels.h
-// crc32c_small_service_kernel; opt-in, photon_crc_set_small_service). One
-// per device: a non-blocking stream, the pinned request / slot area, the
-// last seq posted. One call at a time uses it (try-lock: a call that finds
-// it busy, or not running, takes the launch path, routed_small); the first
-// call after it ended starts a new launch and itself takes the launch path
-// while the service loads its tables.
+// The resident small-buffer services (crc32c_kernels.h
+// crc32c_small_service_kernel, crc64_kernels.h crc64_small_service_kernel;
+// opt-in, photon_crc_set_small_service). One per device and CRC width, each
+// started by the first routed call of its width: a non-blocking stream, the
+// doorbell, the pinned slot area, the last seq posted. One call at a time
+// uses a service (try-lock: a call that finds it busy, or not running, takes
+// the launch path, routed_small / routed_small64); the first call after it
+// ended starts a new launch and itself takes the launch path while the
+// service loads its tables.
 struct SmallService {
     std::mutex mu;
+    int kind = 0;              // 0 CRC32C, 1 CRC-64/ECMA
     hipStream_t st = nullptr;
     uint64_t* h = nullptr;     // host view of the pinned area (quit, slots)
     uint64_t* d = nullptr;     // its device view
@@ -2075,14 +2107,18 @@ struct SmallService {
     uint64_t* bell_d = nullptr;
     bool bar = false;
     uint32_t seq = 0;          // last seq posted (never 0)
-    bool live = false;         // a launch that has not been seen to end
+    std::atomic<bool> live{false};  // a launch that has not been seen to end
 };
+std::atomic<int> g_svc_live{0};  // services with live == true (svc_yield's fast path)
+void set_live(SmallService* s, bool on) {
+    if (s->live.exchange(on) != on) g_svc_live.fetch_add(on ? 1 : -1, std::memory_order_relaxed);
+}
 
 // Doorbell words from the host; the BAR mapping is write-combined: the
 // stores leave the CPU at the sfence.
 inline void bell_put(SmallService* s, uint32_t i, uint64_t v) { __atomic_store_n(&s->bell[i], v, __ATOMIC_RELAXED); }
 inline void bell_flush() { __builtin_ia32_sfence(); }
-PerDevice<SmallService*> g_svc;
+PerDevice<SmallService*> g_svc[2];
 std::mutex g_svc_list_mu;
 std::vector<SmallService*> g_svc_list;
 constexpr uint32_t kSvcLifeTicks = 10000000u;  // 100 ms of the 100 MHz clock, then a new launch
@@ -2093,7 +2129,7 @@ void service_end(SmallService* s) {
     bell_put(s, kSvcStop, 1ull);
     bell_flush();
     (void)hipStreamSynchronize(s->st);
-    s->live = false;
+    set_live(s, false);
 }
 
 void service_end_all() {
@@ -2109,13 +2145,15 @@ void service_end_all() {
     }
 }
 
-int service_get(int dev, SmallService** out) {
-    return g_svc.get(dev, out, [](int, SmallService*& slot) {
+int service_get(int dev, int kind, SmallService** out) {
+    return g_svc[kind].get(dev, out, [kind](int, SmallService*& slot) {
         auto* s = new SmallService;
+        s->kind = kind;
+        const uint64_t bytes = 8 * kSvcWords + (PCRC_SVC_STAMP ? 128 * kSmallWg : 0);
         const hipError_t e = relaxed_capture([&] {
             hipError_t r = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking);
             if (r == hipSuccess)
-                r = hipHostMalloc(reinterpret_cast<void**>(&s->h), 8 * kSvcWords + (PCRC_SVC_STAMP ? 128 * kSmallWg : 0),
+                r = hipHostMalloc(reinterpret_cast<void**>(&s->h), bytes,
                                   hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
             if (r == hipSuccess) r = hipHostGetDevicePointer(reinterpret_cast<void**>(&s->d), s->h, 0);
             int dev = 0, large_bar = 0;
@@ -2139,7 +2177,7 @@ int service_get(int dev, SmallService** out) {
             delete s;
             return hip_fail(e, "small-buffer service");
         }
-        memset(s->h, 0, 8 * kSvcWords + (PCRC_SVC_STAMP ? 128 * kSmallWg : 0));
+        memset(s->h, 0, bytes);
         if (!s->bar) {
             s->bell = s->h;
             s->bell_d = s->d;
@@ -2152,34 +2190,68 @@ int service_get(int dev, SmallService** out) {
     });
 }
 
-// Serve one routed small call through the service: 0 = *crc_out is the CRC,
-// 1 = not served (take the launch path).
-int service_small(int dev, const SmallArgs& sa, uint32_t* crc_out) {
+// LDS per workgroup of the two services (the kernels' tables, command words
+// and reduce words, rounded up to 1 KiB).
+constexpr uint32_t kSvcLdsBytes[2] = {14u * 1024u, 35u * 1024u};
+
+void svc_yield(uint32_t lds) {
+    if (g_svc_live.load(std::memory_order_relaxed) == 0) return;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    for (int kind = 0; kind < 2; ++kind) {
+        if (lds + kSvcLdsBytes[kind] <= kWholeCu) continue;
+        SmallService* s = g_svc[kind].peek(dev);
+        if (!s || !s->live.load()) continue;
+        // no lock: a call in flight sees quit, waits for the stream and takes
+        // the launch path; the next call starts a new launch
+        bell_put(s, kSvcStop, 1ull);
+        bell_flush();
+        __atomic_store_n(&s->h[kSvcQuit], 1ull, __ATOMIC_RELAXED);
+    }
+}
+
+// Serve one routed small call through the service of its width: 0 = the
+// slots' XOR is in x[0] (CRC-64: x[1] the high words), 1 = not served (take
+// the launch path). The request: a0, nb, s0, k, wg0, eoff as small_args /
+// small64_args computed them, seed (CRC-64: the inverted init).
+int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0, uint32_t k, uint32_t wg0,
+                  uint32_t eoff, uint64_t seed, uint32_t x[2]) {
     const int idle_us = g_svc_idle_us.load(std::memory_order_relaxed);
     if (idle_us <= 0) return 1;
     SmallService* s = nullptr;
-    if (service_get(dev, &s)) return 1;
+    if (service_get(dev, kind, &s)) return 1;
     std::unique_lock<std::mutex> lk(s->mu, std::try_to_lock);
     if (!lk.owns_lock()) return 1;
     volatile uint64_t* h = s->h;
-    if (s->live && h[kSvcQuit]) {  // it ended itself (idle / life): its waves leave at their next poll
+    if (s->live && h[kSvcQuit]) {  // it ended (idle / life / svc_yield): its waves leave at their next poll
         (void)hipStreamSynchronize(s->st);
-        s->live = false;
+        set_live(s, false);
     }
     if (!s->live) {
-        const uint32_t* img = nullptr;
-        if (small_image(dev, &img)) return 1;
+        const void* img = nullptr;
+        if (kind == 0) {
+            const uint32_t* i32 = nullptr;
+            if (small_image(dev, &i32)) return 1;
+            img = i32;
+        } else {
+            const uint64_t* i64 = nullptr;
+            if (small64_image(dev, &i64)) return 1;
+            img = i64;
+        }
         bell_put(s, kSvcStop, 0ull);
         bell_put(s, kSvcQuit, 0ull);
         bell_flush();
         __atomic_store_n(&s->h[kSvcQuit], 0ull, __ATOMIC_RELAXED);
         ServiceArgs a{img, s->bell_d, s->d, s->seq, 100u * (uint32_t)idle_us, kSvcLifeTicks};
         const hipError_t e = relaxed_capture([&] {
-            hipLaunchKernelGGL(crc32c_small_service_kernel, dim3(kSmallWg), dim3(256), 0, s->st, a);
+            if (kind == 0)
+                hipLaunchKernelGGL(crc32c_small_service_kernel, dim3(kSmallWg), dim3(256), 0, s->st, a);
+            else
+                hipLaunchKernelGGL(crc64_small_service_kernel, dim3(kSmallWg), dim3(256), 0, s->st, a);
             return hipGetLastError();
         });
         if (e == hipSuccess) {
-            s->live = true;
+            set_live(s, true);
             g_svc_starts.fetch_add(1, std::memory_order_relaxed);
         }
         return 1;
@@ -2188,18 +2260,22 @@ int service_small(int dev, const SmallArgs& sa, uint32_t* crc_out) {
     if (seq == 0) seq = 1;
     s->seq = seq;
     const uint64_t tag = (uint64_t)seq << 32;
-    const uint64_t f[5] = {(uint32_t)reinterpret_cast<uintptr_t>(sa.a0),
-                           (uint32_t)(reinterpret_cast<uintptr_t>(sa.a0) >> 32),
-                           sa.nb | sa.s0 << 16 | sa.k << 20 | sa.wg0 << 25, sa.eoff, sa.seed};
-    for (uint32_t i = 0; i < 5; ++i) bell_put(s, i, tag | f[i]);
+    const uint64_t f[kSvcStop] = {(uint32_t)reinterpret_cast<uintptr_t>(a0),
+                                  (uint32_t)(reinterpret_cast<uintptr_t>(a0) >> 32),
+                                  nb | s0 << 16 | k << 20 | wg0 << 25,
+                                  eoff,
+                                  (uint32_t)seed,
+                                  (uint32_t)(seed >> 32)};
+    for (uint32_t i = 0; i < kSvcStop; ++i) bell_put(s, i, tag | f[i]);
     bell_flush();
-    const uint32_t n = kSmallWg - sa.wg0;
-    uint32_t done = 0, x = 0;
+    const uint32_t per = kind ? 2 : 1, n = per * (kSmallWg - wg0);
+    uint32_t done = 0;
+    x[0] = x[1] = 0;
     auto scan = [&] {
         while (done < n) {
-            const uint64_t v = h[kSvcSlots + kSvcSlotStride * (sa.wg0 + done)];
+            const uint64_t v = h[kSvcSlots + kSvcSlotStride * (wg0 + done / per) + done % per];
             if ((v >> 32) != seq) break;
-            x ^= (uint32_t)v;
+            x[done % per] ^= (uint32_t)v;
             ++done;
         }
         return done == n;
@@ -2219,14 +2295,13 @@ int service_small(int dev, const SmallArgs& sa, uint32_t* crc_out) {
         std::this_thread::sleep_for(std::chrono::microseconds(10));
         if (h[kSvcQuit] || hipStreamQuery(s->st) != hipErrorNotReady) {
             (void)hipStreamSynchronize(s->st);  // every wave has left: the slots are final
-            s->live = false;
+            set_live(s, false);
             if (scan()) break;
             g_svc_missed.fetch_add(1, std::memory_order_relaxed);
             return 1;
         }
     }
     g_svc_served.fetch_add(1, std::memory_order_relaxed);
-    *crc_out = x;
     return 0;
 }
 
@@ -2239,7 +2314,13 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     uint32_t sgrid = 0;
     int rc;
     if (small_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, XORed here
-        rc = service_small(dev, sa, &r) == 0 ? 0 : routed_small(dev, sa, sgrid, &r);
+        uint32_t x[2];
+        if (service_small(dev, 0, sa.a0, sa.nb, sa.s0, sa.k, sa.wg0, sa.eoff, sa.seed, x) == 0) {
+            r = x[0];
+            rc = 0;
+        } else {
+            rc = routed_small(dev, sa, sgrid, &r);
+        }
     } else {
         rc = routed_long(dev, p, n, crc, &r);
     }
@@ -2321,7 +2402,13 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     uint32_t sgrid = 0;
     int rc;
     if (small64_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, folded here
-        rc = routed_small64(dev, sa, sgrid, &r);
+        uint32_t x[2];
+        if (service_small(dev, 1, sa.a0, sa.nb, sa.s0, sa.k, sa.wg0, sa.eoff, sa.init, x) == 0) {
+            r = ~(((uint64_t)x[1] << 32) | x[0]);  // as routed_small64: XOR of the raw values, inverted
+            rc = 0;
+        } else {
+            rc = routed_small64(dev, sa, sgrid, &r);
+        }
     } else {
         rc = routed_long64(dev, p, n, crc, &r);
     }
@@ -2377,7 +2464,7 @@ extern "C" void* photon_crc_test_service_area(void) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     pcrc::SmallService* s = nullptr;
-    return pcrc::service_get(dev, &s) ? nullptr : s->h;
+    return pcrc::service_get(dev, 0, &s) ? nullptr : s->h;
 }
 #endif
 

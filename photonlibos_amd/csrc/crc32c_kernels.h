@@ -1462,8 +1462,8 @@ __device__ __forceinline__ uint32_t small_value(const SmallArgs& a, const uint32
 // may lie on an unmapped page). COHERENT: agent-scope loads that
 // skip the CU's L1 (the resident service below reads buffers that other
 // launches rewrite between its requests); else nontemporal loads.
-template <bool COHERENT>
-__device__ __forceinline__ void small_load(const SmallArgs& a, uint32_t vt, uint4 (&w)[kSmallRows]) {
+template <bool COHERENT, typename A>
+__device__ __forceinline__ void small_load(const A& a, uint32_t vt, uint4 (&w)[kSmallRows]) {
     const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
     const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
 #pragma unroll
@@ -1527,81 +1527,80 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
 }
 
 // The resident small-buffer service (routed drop-in calls of <= 256 KiB,
-// opt-in: photon_crc_set_small_service). A launch of kSmallWg workgroups
-// that stays on the chip between calls: the tables and the basis words are
-// loaded ONCE, and a call costs no launch -- the host writes the request into
-// the doorbell, wave 0 of every workgroup polls it and hands it to its
+// opt-in: photon_crc_set_small_service; CRC-64: crc64_kernels.h
+// crc64_small_service_kernel). A launch of kSmallWg workgroups that stays on
+// the chip between calls: the tables and the basis words are loaded ONCE,
+// and a call costs no launch -- the host writes the request into the
+// doorbell, wave 0 of every workgroup polls it and hands it to its
 // workgroup through LDS, the workgroup computes its share of the layout
-// exactly as crc32c_small_kernel (small_value) and stores its tagged value
-// into its own slot in pinned host memory; the host XORs the slots. No
-// GPU-side ordering across workgroups is needed (the host collects). One slot
-// per workgroup, each on a 64-byte line of its own: 8-byte writes of 128
-// waves into 16 shared lines cost ~5 µs more at 128 KiB than 32 workgroup
-// slots (the host link serialises partial writes to one line).
+// exactly as the small kernel (small_value) and stores its tagged value into
+// its own slot in pinned host memory; the host XORs the slots. No GPU-side
+// ordering across workgroups is needed (the host collects). One slot per
+// workgroup, each on a 64-byte line of its own: 8-byte writes of 128 waves
+// into 16 shared lines cost ~5 µs more at 128 KiB than 32 workgroup slots
+// (the host link serialises partial writes to one line).
 //
 // The doorbell (64-bit words; DEVICE memory the host writes through the PCIe
 // BAR on large-BAR systems -- the device polls it in 0.2-0.4 µs instead of
-// 1.2-2.8 µs over the host link, repo:scripts/probe_doorbell.hip -- else
-// pinned host memory):
-//   0-4  the request, each word {seq (high 32), field (low 32)}: a0 low, a0
-//        high, nb | s0 << 16 | k << 20 | wg0 << 25, eoff, seed. A request is
-//        taken when all five carry one seq that is not the last one served
-//        (the host writes the words in any order; a torn read retries);
-//   5    stop (host -> device): nonzero ends the service;
-//   6    quit: set by workgroup 0 when it ends the service (idle for `idle`
+// 1.2-2.8 µs over the host link, repo:profiles/r05h_doorbell_probe.jsonl --
+// else pinned host memory):
+//   0-5  the request, each word {seq (high 32), field (low 32)}: a0 low, a0
+//        high, nb | s0 << 16 | k << 20 | wg0 << 25, eoff, seed low, seed high
+//        (CRC-64: the inverted init). A request is taken when all six carry
+//        one seq that is not the last one served (the host writes the words
+//        in any order; a torn read retries);
+//   6    stop (host -> device): nonzero ends the service;
+//   7    quit: set by workgroup 0 when it ends the service (idle for `idle`
 //        ticks of the 100 MHz clock, or `life` ticks old), here for the other
-//        workgroups and in the pinned area's word 6 for the host, which then
+//        workgroups and in the pinned area's word 7 for the host, which then
 //        starts a new launch for later calls.
-// Pinned area: word 6 quit (above); 16 + 8 b: slot of workgroup b, {seq,
-// value}.
+// Pinned area: word 7 quit (above); 16 + 8 b: slot of workgroup b, {seq,
+// value} (CRC-64: {seq, low}, {seq, high}).
 // Every wave exits: workgroup 0 on stop / idle / life, the others on stop,
 // quit or 2 x life by their own clock (a workgroup 0 that never became
-// resident cannot keep them alive). The request's bytes are read with
-// agent-scope loads (small_load<true>): a buffer rewritten by another launch
-// since this one last read it must not come from this CU's L1.
-constexpr uint32_t kSvcStop = 5, kSvcQuit = 6, kSvcSlots = 16, kSvcSlotStride = 8;  // one 64-byte line per slot
+// resident cannot keep them alive). The decision is per workgroup (wave 0's,
+// through LDS): all four waves always take the same path, so a workgroup
+// barrier inside the work never misses a wave. The request's bytes are read
+// with agent-scope loads (small_load<true>): a buffer rewritten by another
+// launch since this one last read it must not come from this CU's L1.
+constexpr uint32_t kSvcStop = 6, kSvcQuit = 7, kSvcSlots = 16, kSvcSlotStride = 8;  // one 64-byte line per slot
 constexpr uint32_t kSvcWords = kSvcSlots + kSvcSlotStride * kSmallWg;
 constexpr uint32_t kSvcLds = kSmLds + 32u * 32u * 4u;  // the tables, then the tail basis words
 
 struct ServiceArgs {
-    const uint32_t* image;  // the small kernel's image (tables, wave and tail basis words)
-    uint64_t* bell;         // the doorbell (device view)
-    uint64_t* area;         // the pinned area (device view)
-    uint32_t last;          // the seq served last (by an earlier launch): not served again
-    uint32_t idle;          // ticks without a request before workgroup 0 ends the service
-    uint32_t life;          // ticks after which workgroup 0 ends it
+    const void* image;  // the small kernel's image (tables, wave and tail basis words)
+    uint64_t* bell;     // the doorbell (device view)
+    uint64_t* area;     // the pinned area (device view)
+    uint32_t last;      // the seq served last (by an earlier launch): not served again
+    uint32_t idle;      // ticks without a request before workgroup 0 ends the service
+    uint32_t life;      // ticks after which workgroup 0 ends it
 };
 
-__global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kSvcLds / 4];
-    __shared__ uint32_t cmd[2][8];  // per poll parity: request words 0-4, seq, command
-    __shared__ uint32_t red[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id(), l32 = lane & 31u;
-    const uint32_t wg = blockIdx.x, vt = wg * 256u + tid;
-    for (uint32_t j = tid; j < kSmLds / 16; j += 256u)
-        *reinterpret_cast<u32x4*>(lds + 4 * j) = *((const g_u32x4*)s.image + j);
-    for (uint32_t j = tid; j < 32u * 32u / 4u; j += 256u)
-        *reinterpret_cast<u32x4*>(lds + kSmLds / 4 + 4 * j) = *((const g_u32x4*)(s.image + kSmTail / 4) + j);
-    const uint32_t bw_wave = s.image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
-    __syncthreads();
+// One request as the doorbell carries it.
+struct SvcReq {
+    const uint8_t* a0;
+    uint32_t nb, s0, k, wg0, eoff, seq;
+    uint64_t seed;
+};
+
+// The poll loop of both services: work(req) for each request whose part of
+// the layout has data in this workgroup. st (PCRC_SVC_STAMP builds): stamps
+// 0 poll issue, 1 seen (realtime), 6 seen (shader cycles) of the request.
+template <typename Work>
+__device__ __forceinline__ void service_loop(const ServiceArgs& s, uint32_t (&cmd)[2][8], uint64_t* st, Work work) {
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_id(), wg = blockIdx.x;
     uint32_t last = s.last;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tl = t0;
-#if PCRC_SVC_STAMP
-    uint64_t st[16] = {};  // issue, seen, decoded, loaded, value, done (realtime); seen, done (shader cycles);
-                           // 8-12: inside small_wave_value
-#endif
     for (uint32_t round = 0;; ++round) {
         uint32_t* c = cmd[round & 1u];
         if (wave == 0) {
-#if PCRC_SVC_STAMP
             const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
-#endif
             const uint64_t v = lane <= kSvcQuit ? __hip_atomic_load(s.bell + lane, __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_SYSTEM)
                                                 : 0ull;
             const uint32_t seq = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-            const bool same = lane >= 5 || (uint32_t)(v >> 32) == seq;
+            const bool same = lane >= kSvcStop || (uint32_t)(v >> 32) == seq;
             const bool fresh = __ballot(same) == ~0ull && seq != last;
             const bool stop = __shfl(v, kSvcStop) != 0 || __shfl(v, kSvcQuit) != 0;
             const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -1622,51 +1621,70 @@ __global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s
             if (fresh) {
                 last = seq;
                 tl = now;
-#if PCRC_SVC_STAMP
-                st[0] = t_issue;
-                st[1] = now;
-                st[6] = __builtin_amdgcn_s_memtime();
-#endif
+                if (PCRC_SVC_STAMP && st) {
+                    st[0] = t_issue;
+                    st[1] = now;
+                    st[6] = __builtin_amdgcn_s_memtime();
+                }
             }
-            if (lane < 5) c[lane] = (uint32_t)v;
+            if (lane < kSvcStop) c[lane] = (uint32_t)v;
             if (lane == 0) {
-                c[5] = seq;
-                c[6] = cm;
+                c[6] = seq;
+                c[7] = cm;
             }
         }
         __syncthreads();
-        const uint32_t cm = c[6];
+        const uint32_t cm = c[7];
         if (cm == 2u) break;
         if (cm == 0u) continue;
+        SvcReq r;
+        r.a0 = reinterpret_cast<const uint8_t*>((uint64_t)c[1] << 32 | c[0]);
+        r.nb = c[2] & 0xffffu;
+        r.s0 = (c[2] >> 16) & 15u;
+        r.k = (c[2] >> 20) & 31u;
+        r.wg0 = (c[2] >> 25) & 31u;
+        r.eoff = c[3];
+        r.seed = (uint64_t)c[5] << 32 | c[4];
+        r.seq = c[6];
+        if (wg < r.wg0) continue;  // no data in this workgroup's part of the layout
+        work(r);
+    }
+}
+
+__global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSvcLds / 4];
+    __shared__ uint32_t cmd[2][8];  // per poll parity: request words 0-5, seq, command
+    __shared__ uint32_t red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id(), l32 = lane & 31u;
+    const uint32_t wg = blockIdx.x, vt = wg * 256u + tid;
+    const uint32_t* image = static_cast<const uint32_t*>(s.image);
+    for (uint32_t j = tid; j < kSmLds / 16; j += 256u)
+        *reinterpret_cast<u32x4*>(lds + 4 * j) = *((const g_u32x4*)image + j);
+    for (uint32_t j = tid; j < 32u * 32u / 4u; j += 256u)
+        *reinterpret_cast<u32x4*>(lds + kSmLds / 4 + 4 * j) = *((const g_u32x4*)(image + kSmTail / 4) + j);
+    const uint32_t bw_wave = image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
+    __syncthreads();
+    uint64_t st[16] = {};  // PCRC_SVC_STAMP builds: 0-7 service_loop / below, 8-12 inside small_wave_value
+    service_loop(s, cmd, PCRC_SVC_STAMP ? st : nullptr, [&](const SvcReq& r) {
         SmallArgs a{};
-        a.a0 = reinterpret_cast<const uint8_t*>((uint64_t)c[1] << 32 | c[0]);
-        a.nb = c[2] & 0xffffu;
-        a.s0 = (c[2] >> 16) & 15u;
-        a.k = (c[2] >> 20) & 31u;
-        a.wg0 = (c[2] >> 25) & 31u;
-        a.eoff = c[3];
-        a.seed = c[4];
-        if (wg < a.wg0) continue;  // no data in this workgroup's part of the layout
-#if PCRC_SVC_STAMP
-        st[2] = __builtin_amdgcn_s_memrealtime();
-#endif
+        a.a0 = r.a0;
+        a.nb = r.nb;
+        a.s0 = r.s0;
+        a.k = r.k;
+        a.eoff = r.eoff;
+        a.seed = (uint32_t)r.seed;
+        if (PCRC_SVC_STAMP) st[2] = __builtin_amdgcn_s_memrealtime();
         uint4 w[kSmallRows];
         small_load<true>(a, vt, w);
         const uint32_t bw_tail = lds[kSmLds / 4 + a.k * 32u + l32];
-#if PCRC_SVC_STAMP
-        __builtin_amdgcn_s_waitcnt(0);
-        st[3] = __builtin_amdgcn_s_memrealtime();
-#endif
-#if PCRC_SVC_STAMP
-        const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red, st);
-#else
-        const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red);
-#endif
-#if PCRC_SVC_STAMP
-        if (wave == 0) {
+        if (PCRC_SVC_STAMP) {
+            __builtin_amdgcn_s_waitcnt(0);
+            st[3] = __builtin_amdgcn_s_memrealtime();
+        }
+        const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red, PCRC_SVC_STAMP ? st : nullptr);
+        if (PCRC_SVC_STAMP && wave == 0) {
             asm volatile("" ::"v"(u));
-            st[4] = __builtin_amdgcn_s_memrealtime();
-            st[5] = __builtin_amdgcn_s_memrealtime();
+            st[4] = st[5] = __builtin_amdgcn_s_memrealtime();
             st[7] = __builtin_amdgcn_s_memtime();
             if (lane < 16) {
                 uint64_t x = st[0];
@@ -1675,11 +1693,10 @@ __global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s
                 __hip_atomic_store(s.area + kSvcWords + 16 * wg + lane, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
-#endif
         if (wave == 0 && lane == 0)
-            __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg, (uint64_t)c[5] << 32 | u, __ATOMIC_RELAXED,
+            __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg, (uint64_t)r.seq << 32 | u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    });
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {

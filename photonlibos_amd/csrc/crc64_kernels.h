@@ -896,49 +896,29 @@ __device__ __forceinline__ uint64_t tail_word64(uint64_t w, int off, int eoff) {
     return m >= 8 ? w : m <= 0 ? 0ull : w & ((1ull << (8 * m)) - 1ull);
 }
 
-__global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kSm64Lds / 4];
-    __shared__ uint64_t red[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
-    const uint32_t wg = a.wg0 + blockIdx.x;
-    const uint32_t vt = wg * 256u + tid;
-    // 1. Table copy first, then the payload rows, then the basis words.
-    constexpr uint32_t kVec = kSm64Lds / 16;  // 2176 16-byte pieces: up to 9 per thread
-    constexpr uint32_t kPer = (kVec + 255) / 256;
-    u32x4 tv[kPer];
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-        const uint32_t j = i * 256u + tid;
-        tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
-    }
-    const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
+// Steps 2-3 of one workgroup's share (blocks w[] loaded for virtual lane vt):
+// the column, the shift to the end of the wave, the wave's factor, the XOR
+// over the 4 waves and the tail factor; the value on wave 0, one barrier.
+__device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const uint32_t* lds,
+                                                  const uint4 (&w)[kSmallRows], uint32_t vt, uint64_t bw_wave,
+                                                  uint64_t bw_tail, uint64_t* red) {
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_id();
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
     const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
-    uint4 w[kSmallRows];
-#pragma unroll
-    for (int r = 0; r < (int)kSmallRows; ++r) {
-        const int b = first + r * (int)kSmallLanes;
-        w[r] = ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) ? load16(a.a0 + 16 * (uint32_t)b)
-                                                                           : make_uint4(0, 0, 0, 0);  // as crc32c_small_kernel
-    }
-    const uint64_t bw_wave = a.image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
-    const uint64_t bw_tail = a.image[kSm64Tail / 8 + a.k * 64u + lane];
-#pragma unroll
-    for (uint32_t i = 0; i < kPer; ++i) {
-        const uint32_t j = i * 256u + tid;
-        if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
-    }
-    lds_barrier();
-    // 2. The column: lagged blocks and the row shift.
+    // 2. The column: lagged blocks and the row shift (rows that do not exist
+    //    cost nothing: crc32c_kernels.h small_wave_value).
     uint64_t c[kSmallRows];
 #pragma unroll
     for (int r = 0; r < (int)kSmallRows; ++r) {
+        c[r] = 0;
+        if ((uint32_t)r >= rows) continue;
         const int b = first + r * (int)kSmallLanes;
         uint64_t lo = ((uint64_t)w[r].y << 32) | w[r].x, hi = ((uint64_t)w[r].w << 32) | w[r].z;
         if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + init
             const int off = b * 16;
             lo = head_word64(tail_word64(lo, off, (int)a.eoff), off, (int)a.s0, a.init);
             hi = head_word64(tail_word64(hi, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.init);
-            if (b < 0 || (uint32_t)r >= rows) lo = hi = 0ull;
+            if (b < 0) lo = hi = 0ull;
         }
         c[r] = nib_mul64_pos(lds, kSm64D, lo) ^ hi;
     }
@@ -954,9 +934,41 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
     v = mul_wave64(v, bw_wave, lane);
     if (lane == 0) red[wave] = v;
     __syncthreads();
+    uint64_t u = 0;
     if (wave == 0) {
-        uint64_t u = red[0] ^ red[1] ^ red[2] ^ red[3];
+        u = red[0] ^ red[1] ^ red[2] ^ red[3];
         u = mul_wave64(u, bw_tail, lane);
+    }
+    return u;
+}
+
+__global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSm64Lds / 4];
+    __shared__ uint64_t red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t wg = a.wg0 + blockIdx.x;
+    const uint32_t vt = wg * 256u + tid;
+    // 1. Table copy first, then the payload rows, then the basis words.
+    constexpr uint32_t kVec = kSm64Lds / 16;  // 2176 16-byte pieces: up to 9 per thread
+    constexpr uint32_t kPer = (kVec + 255) / 256;
+    u32x4 tv[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t j = i * 256u + tid;
+        tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
+    }
+    uint4 w[kSmallRows];
+    small_load<false>(a, vt, w);  // as crc32c_small_kernel: only blocks that overlap the data
+    const uint64_t bw_wave = a.image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
+    const uint64_t bw_tail = a.image[kSm64Tail / 8 + a.k * 64u + lane];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t j = i * 256u + tid;
+        if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
+    }
+    lds_barrier();
+    const uint64_t u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+    if (wave == 0) {
         if (a.slots) {  // routed: the host XORs the workgroups' raw values and inverts
             if (lane == 0) {
                 __hip_atomic_store(a.slots + 2 * blockIdx.x, (uint64_t)a.tag << 32 | (uint32_t)u, __ATOMIC_RELAXED,
@@ -968,6 +980,41 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
             long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122
         }
     }
+}
+
+// The resident small-buffer service for routed crc64ecma_extend calls
+// (crc32c_kernels.h crc32c_small_service_kernel, the same doorbell and poll
+// loop): the CRC-64 tables (34 KiB) stay in LDS, a workgroup's raw value goes
+// to its slot as {seq, low}, {seq, high}; the host XORs and inverts. The
+// request's seed words carry the inverted init.
+__global__ __launch_bounds__(256) void crc64_small_service_kernel(ServiceArgs s) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSm64Lds / 4];
+    __shared__ uint32_t cmd[2][8];
+    __shared__ uint64_t red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t wg = blockIdx.x, vt = wg * 256u + tid;
+    const uint64_t* image = static_cast<const uint64_t*>(s.image);
+    for (uint32_t j = tid; j < kSm64Lds / 16; j += 256u)
+        *reinterpret_cast<u32x4*>(lds + 4 * j) = *((const g_u32x4*)image + j);
+    const uint64_t bw_wave = image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
+    __syncthreads();
+    service_loop(s, cmd, nullptr, [&](const SvcReq& r) {
+        Small64Args a{};
+        a.a0 = r.a0;
+        a.nb = r.nb;
+        a.s0 = r.s0;
+        a.k = r.k;
+        a.eoff = r.eoff;
+        a.init = r.seed;
+        uint4 w[kSmallRows];
+        small_load<true>(a, vt, w);
+        const uint64_t bw_tail = image[kSm64Tail / 8 + a.k * 64u + lane];  // L2-resident: 16 KiB for all k
+        const uint64_t u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+        if (wave == 0 && lane < 2)
+            __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg + lane,
+                               (uint64_t)r.seq << 32 | (uint32_t)(lane ? u >> 32 : u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    });
 }
 
 }  // namespace pcrc

@@ -69,6 +69,11 @@ struct PerDevice {
         *out = v[dev];
         return 0;
     }
+    // Slot `dev` as it is (value-initialised when never built).
+    T peek(int dev) {
+        std::lock_guard<std::mutex> lk(mu);
+        return dev >= 0 && dev < (int)v.size() ? v[dev] : T{};
+    }
 };
 
 // Run body(slice) for every slice of `plan` on a thread of its own whose

@@ -8,6 +8,7 @@
 // Usage: routed_latency [calls]
 #include <hip/hip_runtime.h>
 #include <photon/common/checksum/crc32c.h>
+#include <photon/common/checksum/crc64ecma.h>
 #include <photon_crc/crc32c_gpu.h>
 #include <photon_crc/tuning.h>
 
@@ -64,11 +65,31 @@ int main(int argc, char** argv) {
         photon_crc_set_small_service(0);
         photon_crc_set_device_dispatch(0);
         const double cpu = median_us(calls, [&] { sink = crc32c_extend(host.data() + 1, n, 0); });
-        printf("{\"bytes\": %zu, \"routed_launch_us\": %.2f, \"routed_service_us\": %.2f, \"service_served\": %llu, "
+        printf("{\"crc\": \"crc32c\", \"bytes\": %zu, \"routed_launch_us\": %.2f, \"routed_service_us\": %.2f, \"service_served\": %llu, "
                "\"host_engine_on_host_copy_us\": %.2f, \"ok\": %s}\n",
                n, launch, svc, (unsigned long long)(s1 - s0), cpu, bad ? "false" : "true");
         fflush(stdout);
     }
+    for (size_t n : {(size_t)16, (size_t)(128u << 10)}) {  // crc64ecma_extend (test_checksum.cpp:204-216)
+        const uint64_t want = crc64ecma_extend(host.data() + 1, n, 0);
+        photon_crc_set_device_dispatch(1);
+        photon_crc_set_small_service(0);
+        volatile uint64_t sink = 0;
+        const double launch = median_us(calls, [&] { sink = crc64ecma_extend(d + 1, n, 0); });
+        bad += sink != want;
+        photon_crc_set_small_service(20000);
+        (void)crc64ecma_extend(d + 1, n, 0);
+        const double svc = median_us(calls, [&] { sink = crc64ecma_extend(d + 1, n, 0); });
+        bad += sink != want;
+        photon_crc_set_small_service(0);
+        photon_crc_set_device_dispatch(0);
+        const double cpu = median_us(calls, [&] { sink = crc64ecma_extend(host.data() + 1, n, 0); });
+        printf("{\"crc\": \"crc64ecma\", \"bytes\": %zu, \"routed_launch_us\": %.2f, \"routed_service_us\": %.2f, "
+               "\"host_engine_on_host_copy_us\": %.2f, \"ok\": %s}\n",
+               n, launch, svc, cpu, bad ? "false" : "true");
+        fflush(stdout);
+    }
+    photon_crc_set_small_service(200);
     (void)hipFree(d);
     return bad ? 1 : 0;
 }
