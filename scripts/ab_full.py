@@ -25,7 +25,8 @@ ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
 ap.add_argument("--crc", type=int, default=64, choices=[64])  # (round 5's CRC-32C full-row kernel measured slower: removed)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--reps", type=int, default=30)
-ap.add_argument("--variants", default="0:2,1:2,2:2,1:4,2:4")
+ap.add_argument("--variants", default="0:2,1:2,2:2,1:4,2:4",
+                help="mode:rows[:lanes] per variant (lanes 0 = --lanes / automatic)")
 ap.add_argument("--lanes", type=int, default=0)
 ap.add_argument("--no-check", action="store_true", help="ablation builds (PHOTON_CRC_LIB): results are not CRCs")
 args = ap.parse_args()
@@ -38,12 +39,14 @@ out = torch.zeros(count, dtype=torch.int64 if args.crc == 64 else torch.int32, d
 setk = ck.set_full_rows64
 run = ck.batch64_strided if args.crc == 64 else ck.batch_strided
 ck.set_lanes_per_buffer(args.lanes)
-variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
+variants = [tuple(int(x) for x in (v + ":0").split(":")[:3]) if v.count(":") == 1 else tuple(int(x) for x in v.split(":"))
+            for v in args.variants.split(",")]
 ref = None
 times = {v: [] for v in variants}
 for r in range(args.rounds):
     for v in (variants if r % 2 == 0 else variants[::-1]):
-        setk(*v)
+        setk(v[0], v[1])
+        ck.set_lanes_per_buffer(v[2] or args.lanes)
         run(buf, nbytes, nbytes, count, out, stream=st)  # warm this shape
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.reps + 1)]
         ev[0].record(st)
@@ -60,7 +63,8 @@ setk(3, 2)
 ck.set_lanes_per_buffer(0)
 for v in variants:
     ms = np.asarray(times[v])
-    print(json.dumps({"config": args.config + ("_crc64" if args.crc == 64 else ""), "mode": v[0], "rows": v[1], "lanes": args.lanes or "auto",
+    print(json.dumps({"config": args.config + ("_crc64" if args.crc == 64 else ""), "mode": v[0], "rows": v[1],
+                      "lanes": v[2] or args.lanes or "auto",
                       "launches": int(ms.size), "ms_mean": round(float(ms.mean()), 5),
                       "ms_median": round(float(np.median(ms)), 5),
                       "frac_mean": round(nbytes * count / (ms.mean() * 1e-3) / 8e12, 4),
