@@ -261,7 +261,7 @@ int photon_crc64ecma_batch_msg_n(const photon_crc_iovec* d_iov, const uint64_t* 
                                  uint64_t* d_out, void* stream);
 /* photon_crc32c_extend_device for CRC-64/ECMA (crc64ecma_extend, crc.cpp:
  * 119-122): the same latency path for spans up to 256 KiB (a small kernel of
- * up to 32 workgroups), one launch over the chip above, the same per-stream
+ * up to 33 workgroups), one launch over the chip above, the same per-stream
  * state and capture rules. */
 int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out,
                                    void* stream);

@@ -74,7 +74,7 @@ int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
 
 /* Resident small-buffer service for routed crc32c_extend calls of up to 256
  * KiB (device pointers, photon_crc_set_device_dispatch): idle_us > 0 keeps a
- * launch of 32 workgroups (256 threads, 14 KiB of LDS each) on the device
+ * launch of 33 workgroups (256 threads, 14 KiB of LDS each) on the device
  * that polls a request doorbell (device memory the host writes through the
  * PCIe BAR; pinned memory without a large BAR), so a call costs no kernel
  * launch and no table load; the launch ends after idle_us without a request
@@ -87,7 +87,7 @@ int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
  * LDS) ends the running services first. One call at a time uses it; concurrent
  * calls take the launch path. While it runs, hipDeviceSynchronize() and
  * anything else that waits for every stream of the device wait until it ends
- * (at most idle_us after the last call), and the 32 workgroups hold their
+ * (at most idle_us after the last call), and the 33 workgroups hold their
  * CUs' resources beside other kernels. DESIGN.md §4.0 has the latency. */
 int photon_crc_set_small_service(int idle_us);
 /* Routed small calls served by the service, launches of it, and calls that

@@ -1811,11 +1811,15 @@ uint32_t host_crc_of_device(const uint8_t* p, size_t n, uint32_t crc) {
 // streams (created on demand and kept), never on the null stream: a routed
 // call does not serialise against the process's other blocking streams, and
 // routed calls from many threads each get a stream of their own (VERDICT r3
-// next #3). Each pooled stream carries 512 bytes of pinned, device-mapped
+// next #3). Each pooled stream carries kRoutedArea bytes of pinned, device-mapped
 // host memory that a kernel writes its result into: the caller waits for
 // the stream and reads the word(s), no D2H copy. A small buffer's CRC comes
 // back as one word per workgroup of crc32c_small_kernel, XORed here: no
 // cross-workgroup reduce on the device.
+// Bytes of a routed stream's pinned result area: the small kernels' slots
+// (CRC-64: 16 bytes per workgroup) or a long kernel's tagged words.
+constexpr uint64_t kRoutedArea = 16 * kSmallWg > 512 ? 1024 : 512;
+static_assert(16 * kSmallWg <= kRoutedArea, "routed result area");
 struct RoutedStream {
     int dev;
     hipStream_t st;
@@ -1840,8 +1844,8 @@ int routed_lease(int dev, RoutedStream** out) {
     hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
     // coherent: the small kernel's system-scope tag stores reach the host directly
     if (e == hipSuccess)
-        e = hipHostMalloc(&r->h, 512, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
-    if (e == hipSuccess) memset(r->h, 0, 512);
+        e = hipHostMalloc(&r->h, kRoutedArea, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);
+    if (e == hipSuccess) memset(r->h, 0, kRoutedArea);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&r->d, r->h, 0);
     if (e != hipSuccess) {
         if (r->h) (void)hipHostFree(r->h);

@@ -1319,14 +1319,14 @@ __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneCon
 // Geometry: the block grid [a0, a0 + 16 nb) covers the data from its aligned
 // start through its end rounded up to 16 bytes (and at least the 4 seed
 // bytes). All threads of the kSmallWg x 256 slots form ONE lane group of
-// V = 8192 virtual lanes walking rows of V blocks anchored at the END: slot
+// V = 256 kSmallWg virtual lanes walking rows of V blocks anchored at the END: slot
 // vt (workgroup b, wave w, lane l: vt = (4 b + w) 64 + l) takes block
 // nb - V (rows - r) + vt in row r (a negative block is a leading zero block,
 // which does not change a CRC). Every slot's last block is in the last row,
 // V - 1 - vt blocks before the end, so every factor is a constant of the
 // layout, independent of the buffer: the lane's x^(32 + 128 (63 - l))
 // (nibble tables A_dl, B_dh: Q -> P and the shift inside the wave) and the
-// wave's x^(8192 (127 - (4 b + w))) (basis words from the image). Only the
+// wave's x^(8192 (4 kSmallWg - 1 - (4 b + w))) (basis words from the image). Only the
 // workgroups that hold data are launched (the last ones). Masking: bytes
 // before the data start and at or after its end are zero, the seed is XORed
 // into the data's first 4 bytes; the k zero bytes after the end multiply the
@@ -1339,14 +1339,16 @@ __global__ __launch_bounds__(kBlock) void crc32c_long_kernel(LongArgs a, LaneCon
 // when `slots` is set (the routed drop-in: pinned host memory, the host XORs
 // them), else to *out through long_reduce (one workgroup: directly).
 constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of blocks
-constexpr uint32_t kSmallWg = 32, kSmallLanes = kSmallWg * 256;  // V = 8192 virtual lanes
-constexpr uint32_t kSmallRows = (kSmallBlocks + 1 + kSmallLanes - 1) / kSmallLanes;  // 3
+// 33 workgroups: V = 8448 virtual lanes, so 128 KiB at ANY alignment with the
+// seed's cover (the reference's 128 KiB at buf+1 is 8193 blocks) is one row.
+constexpr uint32_t kSmallWg = 33, kSmallLanes = kSmallWg * 256;  // V = 8448 virtual lanes
+constexpr uint32_t kSmallRows = (kSmallBlocks + 1 + kSmallLanes - 1) / kSmallLanes;  // 2
 constexpr uint32_t kNib = 512;                                // bytes of one nibble-sliced multiplier
 // D_j: x^(32 j), j = 1..3 (a block's lagged CRC in ONE table step, not three
 // dependent ones), S: one row, A_dl, B_dh: the lane's finish.
 constexpr uint32_t kSmD = 0, kSmS = 3 * kNib, kSmA = 4 * kNib, kSmB = kSmA + 8 * kNib;
 constexpr uint32_t kSmLds = kSmB + 7 * kNib;                  // 9728 B of tables in LDS
-constexpr uint32_t kSmWave = kSmLds;                          // 128 x 32 words: basis of x^(8192 (127 - wave))
+constexpr uint32_t kSmWave = kSmLds;  // 4 kSmallWg x 32 words: basis of x^(8192 (4 kSmallWg - 1 - wave))
 constexpr uint32_t kSmTail = kSmWave + 4u * kSmallWg * 32u * 4u;  // 32 x 32 words: basis of x^(-8 k), k < 32
 constexpr uint32_t kSmImage = kSmTail + 32u * 32u * 4u;       // bytes of the device image
 
@@ -1435,7 +1437,7 @@ __device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const u
     stamp(10, y);
     uint32_t v = group_xor<64>(dh ? y : x);
     stamp(11, v);
-    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (127 - (4 wg + wave))): the wave to the end of the layout
+    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (4 kSmallWg - 1 - (4 wg + wave))): the wave to the layout's end
     stamp(12, v);
     return v;
 }
@@ -1545,7 +1547,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
 // 1.2-2.8 µs over the host link, repo:profiles/r05h_doorbell_probe.jsonl --
 // else pinned host memory):
 //   0-5  the request, each word {seq (high 32), field (low 32)}: a0 low, a0
-//        high, nb | s0 << 16 | k << 20 | wg0 << 25, eoff, seed low, seed high
+//        high, nb | s0 << 16 | k << 20 | wg0 << 25 (6 bits), eoff, seed low, seed high
 //        (CRC-64: the inverted init). A request is taken when all six carry
 //        one seq that is not the last one served (the host writes the words
 //        in any order; a torn read retries);
@@ -1642,7 +1644,7 @@ __device__ __forceinline__ void service_loop(const ServiceArgs& s, uint32_t (&cm
         r.nb = c[2] & 0xffffu;
         r.s0 = (c[2] >> 16) & 15u;
         r.k = (c[2] >> 20) & 31u;
-        r.wg0 = (c[2] >> 25) & 31u;
+        r.wg0 = (c[2] >> 25) & 63u;
         r.eoff = c[3];
         r.seed = (uint64_t)c[5] << 32 | c[4];
         r.seq = c[6];

@@ -842,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
 
 // photon_crc64ecma_extend_device for buffers whose 16-byte block span is at
 // most kSmallBlocks (256 KiB): crc32c_kernels.h crc32c_small_kernel's layout
-// (up to 32 workgroups x 256 threads = V = 8192 virtual lanes walking rows of
+// (up to kSmallWg = 33 workgroups x 256 threads = V = 8448 virtual lanes walking rows of
 // V blocks anchored at the end, every factor a constant of the layout, tables
 // copied from a device image) at 64 bits: a block's lagged value is lo * x^64
 // ^ hi (ONE nibble-sliced multiply), Q <- Q * x^(128 V) ^ v per row, then
