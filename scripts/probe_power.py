@@ -22,7 +22,8 @@ Phases are separated by IDLE_S seconds of idle GPU. One JSON line per phase.
   (crc@W: the product kernel on a grid capped at W workgroups, photon_crc_set_batch_grid;
    c3: CRC-32C on the same 4 GiB as 1 Mi x 4 KiB buffers; c3_64 / c2_64: CRC-64/ECMA on
    4 KiB / 64 KiB buffers with the generic batch kernel, c3_64full / c2_64full: with the
-   full-row kernel, cross-buffer prefetch, 2 rows per step)
+   full-row kernel, cross-buffer prefetch, 2 rows per step; c4: CRC-32C on 4 Ki x 1 MiB; readp: the
+   product's read-only row-pattern kernel, read_stream_kernel)
 """
 import ctypes
 import json
@@ -146,6 +147,12 @@ def launch(kernel, k):
                                     st.cuda_stream)
     elif kernel == "c3":
         ck.batch_strided(buf, 4096, 4096, nbytes // 4096, out3, stream=st)
+        rc = 0
+    elif kernel == "c4":
+        ck.batch_strided(buf, 1 << 20, 1 << 20, nbytes >> 20, out3, stream=st)
+        rc = 0
+    elif kernel == "readp":  # the product's read-only reference kernel (read_stream_kernel, row pattern)
+        ck.read_stream(buf, nbytes, sink, sink.numel(), stream=st)
         rc = 0
     elif kernel.startswith("c3_64") or kernel.startswith("c2_64"):
         ck.set_full_rows64(2 if kernel.endswith("full") else 0, 2)
