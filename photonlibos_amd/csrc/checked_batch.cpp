@@ -358,7 +358,10 @@ photon_crc_msg_batch* photon_crc_msg_batch_create(uint32_t max_messages, uint32_
     dm((void**)&b->d_out, b->h_out, M * 4);
     if (e == hipSuccess) e = hipMalloc((void**)&b->d_seg, S * 4);
     if (e == hipSuccess) e = hipMalloc((void**)&b->d_zero, 16);
-    if (e == hipSuccess) e = hipMemset(b->d_zero, 0, 16);
+    // complete before any launch on any stream (a plain hipMemset is queued on
+    // the null stream, which does not order against non-blocking streams)
+    if (e == hipSuccess) e = hipMemsetAsync(b->d_zero, 0, 16, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         report_hip_error(e, "photon_crc_msg_batch_create");

@@ -227,7 +227,11 @@ int scratch_alloc(void** p, uint64_t bytes, hipStream_t st, bool zeroed = false)
             delete b;
             return hip_fail(e, "hipMalloc(scratch)");
         }
-        if (zeroed && (e = hipMemset(b->p, 0, cap)) != hipSuccess) {
+        // stream-ordered before its first use on `st`: a plain hipMemset runs on
+        // the null stream, which does not order against non-blocking streams
+        // (the zeroing of a reduce state landed after the first kernel that
+        // used it: scripts/soak_service.py)
+        if (zeroed && (e = hipMemsetAsync(b->p, 0, cap, st)) != hipSuccess) {
             (void)hipFree(b->p);
             delete b;
             return hip_fail(e, "hipMemset(state)");
@@ -731,7 +735,7 @@ int long_state(hipStream_t st, LongState** out, void** lease) {
         delete ls;
         return hip_fail(e, "hipMalloc(long state)");
     }
-    if ((e = hipMemset(ls->p, 0, kStateBytes)) != hipSuccess) {
+    if ((e = hipMemsetAsync(ls->p, 0, kStateBytes, st)) != hipSuccess) {  // ordered before the launches on st
         (void)hipFree(ls->p);
         delete ls;
         return hip_fail(e, "hipMemset(long state)");
@@ -744,6 +748,25 @@ int long_state(hipStream_t st, LongState** out, void** lease) {
     }
     *out = ins.first->second;
     return 0;
+}
+
+// For an error message: the stream's reduce-state ticket on the device
+// against the count the host expects after every enqueued launch.
+std::string long_state_diag(hipStream_t st) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return "";
+    LongState* ls = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_ls_mu);
+        auto it = g_long_state.find(std::make_tuple(dev, reinterpret_cast<uintptr_t>(st), std::thread::id()));
+        if (it == g_long_state.end()) return "; no reduce state";
+        ls = it->second;
+    }
+    uint64_t ticket = 0;
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpy(&ticket, ls->p, 8, hipMemcpyDeviceToHost);
+    std::lock_guard<std::mutex> lk(ls->mu);
+    return "; reduce ticket " + std::to_string(ticket) + ", expected " + std::to_string(ls->base);
 }
 
 // Enqueue a long launch on its state: `launch(state, base, reset)` returns
@@ -1942,6 +1965,20 @@ struct FineSleep {
     }
 };
 
+// How long tagged result words may trail their stream's completion (µs).
+constexpr int64_t kLandGraceUs = 2000;
+
+// Poll scan() (pause between reads) for up to `us` microseconds.
+template <typename S>
+bool scan_until(S& scan, int64_t us) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!scan()) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(us)) return false;
+        for (int k = 0; k < 8; ++k) cpu_relax();
+    }
+    return true;
+}
+
 // Wait until the `per` tagged words of each of `n` workgroups (slots w[per
 // b + h]) carry `tag`; x[h] = XOR of their low words. `bytes`: the call's
 // payload (the sleep-ahead estimate).
@@ -1980,9 +2017,14 @@ int wait_tagged(RoutedStream* r, uint32_t tag, uint32_t n, uint32_t* x, uint32_t
         if (slice % 10 == 0) {
             const hipError_t q = hipStreamQuery(r->st);
             if (q == hipErrorNotReady) continue;
-            // finished (or failed) without every tag seen yet: a last look, then its verdict
-            if (scan()) return 0;
+            // finished (or failed) without every tag seen yet. The stream's
+            // completion can reach the host BEFORE the kernel's last
+            // system-scope stores (the command processor's signal and the
+            // shader's writes take different paths over the host link;
+            // scripts/soak_service.py saw it 4 times in 1.2 M calls under
+            // load), so the words get a grace period before the verdict.
             const hipError_t e = hipStreamSynchronize(r->st);
+            if (e == hipSuccess && q == hipSuccess && scan_until(scan, kLandGraceUs)) return 0;
             return hip_fail(e != hipSuccess ? e : (q != hipSuccess ? q : hipErrorUnknown), what);
         }
     }
@@ -2032,7 +2074,14 @@ int routed_long(int dev, const uint8_t* p, uint64_t n, uint32_t crc, uint32_t* c
     if (!rc) {
         uint32_t x = 0;
         rc = wait_tagged(r, tag, 1, &x, 1, n, "crc32c_long_kernel (routed)");
-        if (!rc) *crc_out = x;
+        if (!rc) {
+            *crc_out = x;
+        } else {
+            const volatile uint64_t* w = static_cast<const volatile uint64_t*>(r->h);
+            char buf[96];
+            snprintf(buf, sizeof buf, "; word %016llx, tag %08x", (unsigned long long)w[0], tag);
+            g_err += buf + long_state_diag(r->st);
+        }
     } else {
         (void)hipStreamSynchronize(r->st);
     }
@@ -2056,6 +2105,13 @@ int routed_long64(int dev, const uint8_t* p, uint64_t n, uint64_t crc, uint64_t*
     if (!rc) {
         uint32_t x[2] = {0, 0};
         rc = wait_tagged(r, tag, 1, x, 2, n, "crc64_long_kernel (routed)");
+        if (rc) {
+            const volatile uint64_t* w = static_cast<const volatile uint64_t*>(r->h);
+            char buf[128];
+            snprintf(buf, sizeof buf, "; words %016llx %016llx, tag %08x", (unsigned long long)w[0],
+                     (unsigned long long)w[1], tag);
+            g_err += buf + long_state_diag(r->st);
+        }
         if (!rc) *crc_out = ((uint64_t)x[1] << 32) | x[0];  // long_reduce already inverted it
     } else {
         (void)hipStreamSynchronize(r->st);
@@ -2167,7 +2223,8 @@ int service_get(int dev, int kind, SmallService** out) {
                 hipExtMallocWithFlags(reinterpret_cast<void**>(&s->bell), 4096, hipDeviceMallocUncached) == hipSuccess) {
                 s->bar = true;  // host stores through the BAR at the device address
                 s->bell_d = s->bell;
-                r = hipMemset(s->bell, 0, 4096);
+                r = hipMemsetAsync(s->bell, 0, 4096, s->st);  // complete before the host writes it
+                if (r == hipSuccess) r = hipStreamSynchronize(s->st);
             } else {
                 (void)hipGetLastError();
                 s->bell = nullptr;
@@ -2298,9 +2355,9 @@ int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0
         if (!fine) fine.reset(new FineSleep);
         std::this_thread::sleep_for(std::chrono::microseconds(10));
         if (h[kSvcQuit] || hipStreamQuery(s->st) != hipErrorNotReady) {
-            (void)hipStreamSynchronize(s->st);  // every wave has left: the slots are final
+            (void)hipStreamSynchronize(s->st);  // every wave has left: the slots are final once they land
             set_live(s, false);
-            if (scan()) break;
+            if (scan_until(scan, kLandGraceUs / 10)) break;
             g_svc_missed.fetch_add(1, std::memory_order_relaxed);
             return 1;
         }

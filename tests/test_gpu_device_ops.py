@@ -427,3 +427,38 @@ def test_scratch_release_frees_idle_buffers(torch_dev, oracle):
         assert list(u32(out)) == want, rep
         assert ck.scratch_release() > 0, rep
     assert ck.scratch_release() == 0
+
+
+def test_new_stream_state_zeroed_in_stream_order(torch_dev, oracle):
+    """A stream's first long launch creates its reduce state. Its zeroing used
+    to be a plain hipMemset, queued on the NULL stream, which does not order
+    against non-blocking streams: with the null stream busy, the first kernel
+    on a fresh non-blocking stream ran before the zeroing, the late zeroing
+    reset its ticket, and the stream's SECOND long call found no last
+    workgroup (no result; scripts/soak_service.py saw it as routed fallbacks).
+    Here: the null stream kept busy by batches, then two long calls on a fresh
+    non-blocking stream (photon_crc_stream_create): both results right."""
+    import ctypes
+    from photonlibos_amd._native import lib
+    torch = torch_dev
+    nb, count = 1 << 20, 1024
+    big = torch.empty(nb * count, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(big, nb, nb, count, 0x0DE5)
+    out = torch.zeros(count, dtype=torch.int32, device="cuda")
+    n = 3 << 20  # a long launch (more than one workgroup)
+    host = big[: n + 16].cpu().numpy()
+    want = [oracle.crc32c(host[1:1 + n], s) for s in (5, 6)]
+    for trial in range(3):
+        s = ctypes.c_void_p()
+        assert lib().photon_crc_stream_create(ctypes.byref(s)) == 0
+        res = torch.zeros(2, dtype=torch.int32, device="cuda")
+        for _ in range(64):  # ~10 ms of work queued on the null stream
+            ck.batch_strided(big, nb, nb, count, out, stream=0)
+        ck.extend_device(big.data_ptr() + 1, n, 5, res[0:1], stream=s.value)  # creates the state
+        assert lib().photon_crc_stream_sync(s) == 0
+        torch.cuda.synchronize()  # the null stream's work -- and a zeroing queued behind it -- is done
+        ck.extend_device(big.data_ptr() + 1, n, 6, res[1:2], stream=s.value)
+        assert lib().photon_crc_stream_sync(s) == 0
+        got = [int(x) for x in res.cpu().numpy().view(np.uint32)]
+        assert got == want, (trial, got, want)
+        assert lib().photon_crc_stream_destroy(s) == 0
