@@ -2251,6 +2251,16 @@ int service_get(int dev, int kind, SmallService** out) {
     });
 }
 
+void services_end_on_impl(int dev) {
+    if (g_svc_live.load(std::memory_order_relaxed) == 0) return;
+    for (int kind = 0; kind < 2; ++kind) {
+        SmallService* s = g_svc[kind].peek(dev);
+        if (!s || !s->live.load()) continue;
+        std::lock_guard<std::mutex> lk(s->mu);  // a call in flight finishes first
+        service_end(s);
+    }
+}
+
 // LDS per workgroup of the two services (the kernels' tables, command words
 // and reduce words, rounded up to 1 KiB).
 constexpr uint32_t kSvcLdsBytes[2] = {14u * 1024u, 35u * 1024u};
@@ -2529,3 +2539,5 @@ extern "C" void* photon_crc_test_service_area(void) {
 }
 #endif
 
+// internal.h: for the vDMA initiator's device-wide fence (vdma_hip.cpp).
+void pcrc::services_end_on(int dev) { services_end_on_impl(dev); }

@@ -25,4 +25,8 @@ int registered_range_check(const void* p, uint64_t n);
 // of the library (the vDMA target's register_memory), for the check above.
 void record_registration(const void* p, uint64_t n);
 void forget_registration(const void* p);
+// End the resident small-buffer services running on device `dev` (and wait
+// for their waves), so that a device-wide synchronise that follows does not
+// wait for their idle time (the next routed call starts them again).
+void services_end_on(int dev);
 }  // namespace pcrc

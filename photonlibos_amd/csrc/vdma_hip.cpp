@@ -310,6 +310,7 @@ private:
             }
         }
         DeviceScope scope(dev_);
+        pcrc::services_end_on(dev_);  // else the device-wide wait below waits for their idle time
         if (hipDeviceSynchronize() != hipSuccess) {
             errno = EIO;
             return -1;
