@@ -2211,7 +2211,15 @@ int service_get(int dev, int kind, SmallService** out) {
         s->kind = kind;
         const uint64_t bytes = 8 * kSvcWords + (PCRC_SVC_STAMP ? 128 * kSmallWg : 0);
         const hipError_t e = relaxed_capture([&] {
-            hipError_t r = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking);
+            // A hardware queue of its own: HIP multiplexes streams of one
+            // priority onto GPU_MAX_HW_QUEUES (4) queues, and a stream that
+            // shared the service's queue would wait behind the resident launch
+            // until its idle time ends (seen: a routed launch took the service's
+            // 20 ms idle time once enough streams existed). The greatest
+            // priority has a queue pool of its own (non-blocking, like the rest).
+            int least = 0, greatest = 0;
+            hipError_t r = hipDeviceGetStreamPriorityRange(&least, &greatest);
+            if (r == hipSuccess) r = hipStreamCreateWithPriority(&s->st, hipStreamNonBlocking, greatest);
             if (r == hipSuccess)
                 r = hipHostMalloc(reinterpret_cast<void**>(&s->h), bytes,
                                   hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent);

@@ -1053,8 +1053,8 @@ struct LongArgs {
 #endif
 constexpr uint32_t kLongMaxGrid = 512;
 template <typename T, typename F, bool FENCED = false>
-__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
-                                            uint32_t tag = 0) {
+__device__ __forceinline__ void long_reduce_slots(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
+                                                  uint32_t tag = 0) {
     const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
     // tag != 0 (routed calls, out in the routed stream's coherent pinned
     // area): 8-byte system-scope stores {tag, 32-bit word} (one, or two for
@@ -1112,6 +1112,77 @@ __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64
         put(fin(x));
         if (reset) __hip_atomic_store(ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// The same reduce with ONE round trip on the last workgroup's path (round 5;
+// the default, PCRC_LONG_REDUCE_WORD): per 32-bit half of the value, one
+// 64-bit state word {count (high 32), XOR (low 32)}. Each workgroup XORs its
+// half into the word (no return) and then adds 1 << 32 to it (returned),
+// back to back, no wait between: two atomics of one thread to ONE location
+// are in that location's modification order as issued (write-write coherence,
+// C++ [intro.races]; LLVM AMDGPU implements it), every other workgroup's add
+// came before the last one's, and each one's XOR before its add, so the add
+// that returns count = base + grid - 1 (mod 2^32) returns, in its low half,
+// the XOR of every workgroup's half. That workgroup writes fin(half) and puts
+// the word to {base + grid, 0} (a leased / captured state: to 0). CRC-64's
+// two halves have a word each and may have different last workgroups: each
+// writes its half (the routed form already carries one tagged word per half;
+// a device *out gets two 32-bit stores). A CRC32C launch's last workgroup also
+// sets the second word, so that both words count every launch on the state.
+// Saves the slot store's acknowledgement and the last workgroup's slot loads.
+#ifndef PCRC_LONG_REDUCE_WORD
+#define PCRC_LONG_REDUCE_WORD 1
+#endif
+template <typename T, typename F>
+__device__ __forceinline__ void long_reduce_word(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
+                                                 uint32_t tag = 0) {
+    constexpr uint32_t kHalves = sizeof(T) / 4;
+    const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
+    if (grid == 1) {
+        if (lane == 0) {
+            const T r = fin(v);
+            if (tag) {
+#pragma unroll
+                for (uint32_t h = 0; h < kHalves; ++h)
+                    __hip_atomic_store(reinterpret_cast<uint64_t*>(out) + h,
+                                       (uint64_t)tag << 32 | (uint32_t)((uint64_t)r >> (32 * h)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                *out = r;
+            }
+        }
+        return;
+    }
+    const uint64_t v0 = (uint64_t)__shfl((unsigned long long)(uint64_t)v, 0);  // v is valid on lane 0
+    if (lane < kHalves) {
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(state) + lane;
+        const uint32_t half = (uint32_t)(v0 >> (32 * lane));
+        (void)__hip_atomic_fetch_xor(w, (unsigned long long)half, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long old = __hip_atomic_fetch_add(w, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(old >> 32) == (uint32_t)(base + grid - 1)) {
+            // fin is bitwise per half for both CRCs (identity / inversion)
+            const uint32_t r = (uint32_t)((uint64_t)fin((T)((uint64_t)(uint32_t)old << (32 * lane))) >> (32 * lane));
+            if (tag)
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(out) + lane, (uint64_t)tag << 32 | r, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+                reinterpret_cast<uint32_t*>(out)[lane] = r;
+            const unsigned long long next = reset ? 0ull : (unsigned long long)(uint32_t)(base + grid) << 32;
+            __hip_atomic_store(w, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // a 32-bit CRC's launch advances the second word too: the state's
+            // count covers every launch on it, of either CRC
+            if (kHalves == 1) __hip_atomic_store(w + 1, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+template <typename T, typename F, bool FENCED = false>
+__device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
+                                            uint32_t tag = 0) {
+    if constexpr (PCRC_LONG_REDUCE_WORD && !FENCED)
+        long_reduce_word(v, state, out, fin, base, reset, tag);
+    else
+        long_reduce_slots<T, F, FENCED>(v, state, out, fin, base, reset, tag);
 }
 
 // v * x mod P (reflected: bit j = coefficient of x^(31-j)).
@@ -1221,7 +1292,7 @@ __device__ __forceinline__ void long_finish(const LongArgs& a, uint32_t acc, uin
         if constexpr (ABL & 16) {
             if (lane == 0) *a.out = u;
         } else if constexpr (ABL & 8) {
-            long_reduce<uint32_t, uint32_t (*)(uint32_t), true>(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase,
+            long_reduce_slots<uint32_t, uint32_t (*)(uint32_t), true>(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase,
                                                                 a.treset);
         } else {
             long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset, a.out_tag);

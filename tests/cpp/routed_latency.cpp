@@ -37,7 +37,7 @@ static double median_us(int calls, F f) {
 
 int main(int argc, char** argv) {
     const int calls = argc > 1 ? atoi(argv[1]) : 2000;
-    const size_t cap = (256u << 10) + 64;
+    const size_t cap = (16u << 20) + 64;
     std::vector<uint8_t> host(cap);
     uint64_t z = 0x5EED0128;
     for (auto& b : host) {
@@ -48,7 +48,8 @@ int main(int argc, char** argv) {
     if (hipMalloc((void**)&d, cap) != hipSuccess) return 2;
     if (hipMemcpy(d, host.data(), cap, hipMemcpyHostToDevice) != hipSuccess) return 2;
     int bad = 0;
-    for (size_t n : {(size_t)16, (size_t)4096, (size_t)(128u << 10), (size_t)(256u << 10) - 1}) {
+    for (size_t n : {(size_t)16, (size_t)4096, (size_t)(128u << 10), (size_t)(256u << 10) - 1, (size_t)(1u << 20),
+                     (size_t)(4u << 20), (size_t)(16u << 20)}) {
         const uint32_t want = crc32c_extend(host.data() + 1, n, 0);  // host engine (dispatch off)
         photon_crc_set_device_dispatch(1);
         photon_crc_set_small_service(0);

@@ -257,6 +257,8 @@ def test_service_beside_batch_kernels(torch_dev, oracle):
     cur = torch.cuda.current_stream()
     s0 = _served()
     calls = 0
+    trace = []
+    t_start = time.perf_counter()
     for it in range(40):
         side.wait_stream(cur)
         for _ in range(4):
@@ -265,13 +267,53 @@ def test_service_beside_batch_kernels(torch_dev, oracle):
             host = rng.integers(0, 256, small.numel(), dtype=np.uint8)
             small.copy_(torch.from_numpy(host))
             cur.synchronize()
+            if it < 2:
+                trace.append(("copied", ck.small_service_stats(), round(time.perf_counter() - t_start, 5)))
             off, n = 1 + j, 8000 - 37 * j
             assert ck.crc32c_extend_at(small.data_ptr() + off, n, it) == oracle.crc32c(host[off:off + n], it), (it, j)
             calls += 1
+            if it < 2:
+                trace.append(("called", ck.small_service_stats(), round(time.perf_counter() - t_start, 5)))
         side.synchronize()
     got = out.cpu().numpy().view(np.uint32)
     hbig = big[: 4 * nb].cpu().numpy()
     for i in range(4):
         assert int(got[i]) == oracle.crc32c(hbig[i * nb:(i + 1) * nb], 0)
     assert int(got[count - 1]) == oracle.crc32c(big[(count - 1) * nb:].cpu().numpy(), 0)
-    assert _served() - s0 >= calls // 2, (_served() - s0, calls)
+    assert _served() - s0 >= calls // 2, (_served() - s0, calls, ck.small_service_stats(), trace)
+
+
+def test_service_does_not_hold_other_streams(torch_dev, oracle):
+    """The resident launch must not hold up work on other streams: HIP maps
+    the streams of one priority onto a few hardware queues, and a stream that
+    shared the service's queue would wait behind it for its idle time (20 ms
+    here). With 16 more streams than hardware queues, a small kernel on each
+    finishes in well under that while the service runs, and routed calls made
+    between them are served."""
+    import ctypes
+    from photonlibos_amd._native import lib
+    torch = torch_dev
+    host = np.random.default_rng(9).integers(0, 256, 1 << 20, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).cuda()
+    torch.cuda.current_stream().synchronize()
+    want = oracle.crc32c(host[5:5 + 70000], 3)
+    assert ck.crc32c_extend_at(dbuf.data_ptr() + 5, 70000, 3) == want  # starts the service
+    streams = []
+    for _ in range(16):
+        s = ctypes.c_void_p()
+        assert lib().photon_crc_stream_create(ctypes.byref(s)) == 0
+        streams.append(s)
+    scratch = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+    st0 = ck.small_service_stats()
+    worst = 0.0
+    for s in streams:
+        t0 = time.perf_counter()
+        ck.fill_splitmix(scratch, 4096, 4096, 1, 7, stream=s.value)
+        assert lib().photon_crc_stream_sync(s) == 0
+        worst = max(worst, time.perf_counter() - t0)
+        assert ck.crc32c_extend_at(dbuf.data_ptr() + 5, 70000, 3) == want
+    st1 = ck.small_service_stats()
+    for s in streams:
+        assert lib().photon_crc_stream_destroy(s) == 0
+    assert worst < 0.01, worst
+    assert st1[0] - st0[0] >= 12, (st0, st1)
