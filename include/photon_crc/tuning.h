@@ -72,14 +72,15 @@ int photon_crc64_set_full_rows(int mode, int rows_per_step);
  * sleeps through 85 % of that time. spin_us = 0: no polling window. */
 int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
 
-/* Resident small-buffer service for routed crc32c_extend calls of up to 256
- * KiB (device pointers, photon_crc_set_device_dispatch): idle_us > 0 keeps a
+/* Resident small-buffer service for routed crc32c_extend calls of up to 2 MiB
+ * (block span <= 135,168 16-byte blocks; device pointers,
+ * photon_crc_set_device_dispatch): idle_us > 0 keeps a
  * launch of 33 workgroups (256 threads, 14 KiB of LDS each) on the device
  * that polls a request doorbell (device memory the host writes through the
  * PCIe BAR; pinned memory without a large BAR), so a call costs no kernel
  * launch and no table load; the launch ends after idle_us without a request
- * (and after 100 ms in any case; the next call starts a new one and itself
- * takes the launch path). Default 200 (or the environment variable
+ * (and after 100 ms in any case; the next call starts a new one and is its
+ * first request). Default 200 (or the environment variable
  * PHOTON_CRC_SMALL_SERVICE at load); 0 = off, a launch per call; turning it
  * off ends running launches. crc64ecma_extend has a service of its own (34
  * KiB of LDS per workgroup). A library launch whose workgroups could not

@@ -897,12 +897,13 @@ int small64_image(int dev, const uint64_t** out) {
 
 // The CRC-64 small kernel's geometry (as small_args; the grid covers the
 // init's 8 bytes).
-bool small64_args(const void* p, uint64_t n, uint64_t seed, Small64Args* a, uint32_t* grid) {
+bool small64_args(const void* p, uint64_t n, uint64_t seed, Small64Args* a, uint32_t* grid,
+                  uint64_t max_blocks = kSmallBlocks) {
     const uintptr_t d = reinterpret_cast<uintptr_t>(p);
     const uint64_t s0 = d & 15u, eoff = s0 + n;
     const uint64_t cover = eoff > s0 + 8 ? eoff : s0 + 8;
     const uint64_t nb = (cover + 15) >> 4;
-    if (nb > kSmallBlocks) return false;
+    if (nb > max_blocks) return false;
     a->a0 = reinterpret_cast<const uint8_t*>(d - s0);
     a->nb = (uint32_t)nb;
     a->s0 = (uint32_t)s0;
@@ -915,14 +916,16 @@ bool small64_args(const void* p, uint64_t n, uint64_t seed, Small64Args* a, uint
 }
 
 // The small kernel's geometry for [p, p + n), or false when the block span
-// exceeds kSmallBlocks (the long kernel's case). *grid = the workgroups that
+// exceeds max_blocks (kSmallBlocks: the long kernel's case; the service takes
+// up to kSvcMaxBlocks). *grid = the workgroups that
 // hold data (the last ones of the layout).
-bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t* grid) {
+bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t* grid,
+                  uint64_t max_blocks = kSmallBlocks) {
     const uintptr_t d = reinterpret_cast<uintptr_t>(p);
     const uint64_t s0 = d & 15u, eoff = s0 + n;
     const uint64_t cover = eoff > s0 + 4 ? eoff : s0 + 4;  // the seed's 4 bytes lie inside the grid
     const uint64_t nb = (cover + 15) >> 4;
-    if (nb > kSmallBlocks) return false;
+    if (nb > max_blocks) return false;
     a->a0 = reinterpret_cast<const uint8_t*>(d - s0);
     a->nb = (uint32_t)nb;
     a->s0 = (uint32_t)s0;
@@ -2154,8 +2157,7 @@ int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* cr
 // doorbell, the pinned slot area, the last seq posted. One call at a time
 // uses a service (try-lock: a call that finds it busy, or not running, takes
 // the launch path, routed_small / routed_small64); the first call after it
-// ended starts a new launch and itself takes the launch path while the
-// service loads its tables.
+// ended starts a new launch and is its first request.
 struct SmallService {
     std::mutex mu;
     int kind = 0;              // 0 CRC32C, 1 CRC-64/ECMA
@@ -2296,7 +2298,7 @@ void svc_yield(uint32_t lds) {
 int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0, uint32_t k, uint32_t wg0,
                   uint32_t eoff, uint64_t seed, uint32_t x[2]) {
     const int idle_us = g_svc_idle_us.load(std::memory_order_relaxed);
-    if (idle_us <= 0) return 1;
+    if (idle_us <= 0 || g_fail_next > 0) return 1;  // an injected failure (tuning.h) hits the launch path
     SmallService* s = nullptr;
     if (service_get(dev, kind, &s)) return 1;
     std::unique_lock<std::mutex> lk(s->mu, std::try_to_lock);
@@ -2329,11 +2331,12 @@ int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0
                 hipLaunchKernelGGL(crc64_small_service_kernel, dim3(kSmallWg), dim3(256), 0, s->st, a);
             return hipGetLastError();
         });
-        if (e == hipSuccess) {
-            set_live(s, true);
-            g_svc_starts.fetch_add(1, std::memory_order_relaxed);
-        }
-        return 1;
+        if (e != hipSuccess) return 1;
+        set_live(s, true);
+        g_svc_starts.fetch_add(1, std::memory_order_relaxed);
+        // and this call is the new launch's first request: it pays the launch
+        // either way, and a call over 256 KiB sent to the launch path instead
+        // would take the long kernel, whose svc_yield ends the launch again
     }
     uint32_t seq = s->seq + 1u;
     if (seq == 0) seq = 1;
@@ -2341,8 +2344,8 @@ int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0
     const uint64_t tag = (uint64_t)seq << 32;
     const uint64_t f[kSvcStop] = {(uint32_t)reinterpret_cast<uintptr_t>(a0),
                                   (uint32_t)(reinterpret_cast<uintptr_t>(a0) >> 32),
-                                  nb | s0 << 16 | k << 20 | wg0 << 25,
-                                  eoff,
+                                  nb | s0 << 20 | k << 24,
+                                  eoff | wg0 << 26,
                                   (uint32_t)seed,
                                   (uint32_t)(seed >> 32)};
     for (uint32_t i = 0; i < kSvcStop; ++i) bell_put(s, i, tag | f[i]);
@@ -2392,14 +2395,13 @@ uint32_t dispatch_crc(const uint8_t* p, size_t n, uint32_t crc) {
     SmallArgs sa{};
     uint32_t sgrid = 0;
     int rc;
-    if (small_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, XORed here
-        uint32_t x[2];
-        if (service_small(dev, 0, sa.a0, sa.nb, sa.s0, sa.k, sa.wg0, sa.eoff, sa.seed, x) == 0) {
-            r = x[0];
-            rc = 0;
-        } else {
-            rc = routed_small(dev, sa, sgrid, &r);
-        }
+    uint32_t x[2];
+    if (small_args(p, n, crc, &sa, &sgrid, kSvcMaxBlocks) &&
+        service_small(dev, 0, sa.a0, sa.nb, sa.s0, sa.k, sa.wg0, sa.eoff, sa.seed, x) == 0) {
+        r = x[0];  // per-workgroup words in pinned memory, XORed by service_small
+        rc = 0;
+    } else if (sa.nb && sa.nb <= kSmallBlocks) {
+        rc = routed_small(dev, sa, sgrid, &r);
     } else {
         rc = routed_long(dev, p, n, crc, &r);
     }
@@ -2480,14 +2482,13 @@ uint64_t dispatch_crc64(const uint8_t* p, size_t n, uint64_t crc) {
     Small64Args sa{};
     uint32_t sgrid = 0;
     int rc;
-    if (small64_args(p, n, crc, &sa, &sgrid)) {  // per-workgroup words in pinned memory, folded here
-        uint32_t x[2];
-        if (service_small(dev, 1, sa.a0, sa.nb, sa.s0, sa.k, sa.wg0, sa.eoff, sa.init, x) == 0) {
-            r = ~(((uint64_t)x[1] << 32) | x[0]);  // as routed_small64: XOR of the raw values, inverted
-            rc = 0;
-        } else {
-            rc = routed_small64(dev, sa, sgrid, &r);
-        }
+    uint32_t x[2];
+    if (small64_args(p, n, crc, &sa, &sgrid, kSvcMaxBlocks) &&
+        service_small(dev, 1, sa.a0, sa.nb, sa.s0, sa.k, sa.wg0, sa.eoff, sa.init, x) == 0) {
+        r = ~(((uint64_t)x[1] << 32) | x[0]);  // as routed_small64: XOR of the raw values, inverted
+        rc = 0;
+    } else if (sa.nb && sa.nb <= kSmallBlocks) {
+        rc = routed_small64(dev, sa, sgrid, &r);
     } else {
         rc = routed_long64(dev, p, n, crc, &r);
     }

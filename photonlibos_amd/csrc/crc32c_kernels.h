@@ -1456,6 +1456,39 @@ __device__ __forceinline__ uint32_t tail_word(uint32_t w, int off, int eoff) {
     return mc == 4 ? w : w & (uint32_t)((1ull << (8 * mc)) - 1ull);
 }
 
+// One 16-byte block's lagged CRC (block b of the grid, bytes w): masks and
+// the seed at the buffer's ends. lag16: D(D(D(w0) ^ w1) ^ w2) ^ w3 = w0 x^96
+// ^ w1 x^64 ^ w2 x^32 ^ w3.
+__device__ __forceinline__ uint32_t small_lag(const SmallArgs& a, const uint32_t* lds, uint4 v, int b) {
+    if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + seed
+        const int off = b * 16;
+        v.x = head_word_sel(tail_word(v.x, off, (int)a.eoff), off, (int)a.s0, a.seed);
+        v.y = head_word_sel(tail_word(v.y, off + 4, (int)a.eoff), off + 4, (int)a.s0, a.seed);
+        v.z = head_word_sel(tail_word(v.z, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.seed);
+        v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
+        if (b < 0) v = make_uint4(0, 0, 0, 0);
+    }
+    return xor3(nib_mul(lds + (kSmD + 2 * kNib) / 4, v.x), nib_mul(lds + (kSmD + kNib) / 4, v.y),
+                nib_mul(lds + kSmD / 4, v.z)) ^ v.w;
+}
+
+// Q -> the wave's value: x^(32 + 128 dl), then x^(1024 dh) (d = 63 - lane:
+// Q -> P and the shift to the end of the wave), the 64-lane XOR and the
+// wave's factor x^(8192 (4 kSmallWg - 1 - (4 wg + wave))) (bw_wave).
+template <typename Stamp>
+__device__ __forceinline__ uint32_t small_finish(const uint32_t* lds, uint32_t q, uint32_t bw_wave, Stamp stamp) {
+    const uint32_t lane = threadIdx.x & 63u, l32 = lane & 31u;
+    const uint32_t d = 63u - lane, dh = d >> 3;
+    const uint32_t x = nib_mul(lds + (kSmA + (d & 7u) * kNib) / 4, q);
+    const uint32_t y = nib_mul(lds + (kSmB + (dh ? dh - 1u : 0u) * kNib) / 4, x);
+    stamp(10, y);
+    uint32_t v = group_xor<64>(dh ? y : x);
+    stamp(11, v);
+    v = mul_lanes(v, bw_wave, l32);
+    stamp(12, v);
+    return v;
+}
+
 // Steps 2-3 of one wave's share (blocks w[] loaded for virtual lane vt, the
 // tables at lds): the column, the shift to the end of the wave and the
 // wave's factor (bw_wave): the wave's value, on every lane.
@@ -1468,7 +1501,6 @@ __device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const u
             ts[i] = __builtin_amdgcn_s_memrealtime();
         }
     };
-    const uint32_t lane = threadIdx.x & 63u, l32 = lane & 31u;
     // uniform (a scalar branch below): rows past the last are not computed
     const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
     const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;  // this thread's block in row 0
@@ -1481,19 +1513,7 @@ __device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const u
     for (int r = 0; r < (int)kSmallRows; ++r) {
         c[r] = 0;
         if ((uint32_t)r >= rows) continue;
-        const int b = first + r * (int)kSmallLanes;
-        uint4 v = w[r];
-        if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + seed
-            const int off = b * 16;
-            v.x = head_word_sel(tail_word(v.x, off, (int)a.eoff), off, (int)a.s0, a.seed);
-            v.y = head_word_sel(tail_word(v.y, off + 4, (int)a.eoff), off + 4, (int)a.s0, a.seed);
-            v.z = head_word_sel(tail_word(v.z, off + 8, (int)a.eoff), off + 8, (int)a.s0, a.seed);
-            v.w = head_word_sel(tail_word(v.w, off + 12, (int)a.eoff), off + 12, (int)a.s0, a.seed);
-            if (b < 0) v = make_uint4(0, 0, 0, 0);
-        }
-        // lag16: D(D(D(w0) ^ w1) ^ w2) ^ w3 = w0 x^96 ^ w1 x^64 ^ w2 x^32 ^ w3
-        c[r] = xor3(nib_mul(lds + (kSmD + 2 * kNib) / 4, v.x), nib_mul(lds + (kSmD + kNib) / 4, v.y),
-                    nib_mul(lds + kSmD / 4, v.z)) ^ v.w;
+        c[r] = small_lag(a, lds, w[r], first + r * (int)kSmallLanes);
     }
     stamp(8, c[0] ^ c[kSmallRows - 1]);
     uint32_t q = c[0];
@@ -1501,16 +1521,8 @@ __device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const u
     for (int r = 1; r < (int)kSmallRows; ++r)
         if ((uint32_t)r < rows) q = nib_mul(lds + kSmS / 4, q) ^ c[r];
     stamp(9, q);
-    // 3. Q -> P and the shift to the end of the wave: x^(32 + 128 dl), then x^(1024 dh), d = 63 - lane.
-    const uint32_t d = 63u - lane, dh = d >> 3;
-    const uint32_t x = nib_mul(lds + (kSmA + (d & 7u) * kNib) / 4, q);
-    const uint32_t y = nib_mul(lds + (kSmB + (dh ? dh - 1u : 0u) * kNib) / 4, x);
-    stamp(10, y);
-    uint32_t v = group_xor<64>(dh ? y : x);
-    stamp(11, v);
-    v = mul_lanes(v, bw_wave, l32);  // x^(8192 (4 kSmallWg - 1 - (4 wg + wave))): the wave to the layout's end
-    stamp(12, v);
-    return v;
+    // 3. Q -> P, the shift to the end of the wave, the wave's factor.
+    return small_finish(lds, q, bw_wave, stamp);
 }
 
 // The workgroup's value (small_wave_value of its 4 waves XORed, times the
@@ -1530,6 +1542,59 @@ __device__ __forceinline__ uint32_t small_value(const SmallArgs& a, const uint32
     return u;
 }
 
+// 16 bytes with agent-scope loads that skip the CU's L1 (two 8-byte global_
+// loads, not flat_).
+__device__ __forceinline__ uint4 load16_coherent(const uint8_t* p) {
+    typedef __attribute__((address_space(1))) const uint64_t g_u64;
+    g_u64* q = (g_u64*)p;
+    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+// The service's form for calls of up to kSvcRows rows (≈2 MiB; the small
+// kernel's layout, more rows per thread): every row's block of this thread
+// loaded at once (agent-scope loads), then the column, the finish and the
+// workgroup's value as small_value.
+constexpr uint32_t kSvcRows = 16;
+constexpr uint32_t kSvcMaxBlocks = kSvcRows * kSmallLanes;  // 135,168 blocks (2.06 MiB)
+
+// This thread's blocks of every row (as small_load<true>, kSvcRows rows; the
+// rows past the call's are not read).
+template <typename A>
+__device__ __forceinline__ void svc_load_rows(const A& a, uint32_t vt, uint4 (&w)[kSvcRows]) {
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
+    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
+#pragma unroll
+    for (int r = 0; r < (int)kSvcRows; ++r) {
+        w[r] = make_uint4(0, 0, 0, 0);
+        const int b = first + r * (int)kSmallLanes;
+        if ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) w[r] = load16_coherent(a.a0 + 16 * (uint32_t)b);
+    }
+}
+__device__ __forceinline__ uint32_t small_value_rows(const SmallArgs& a, const uint32_t* lds, uint32_t vt,
+                                                     uint32_t bw_wave, uint32_t bw_tail, uint32_t* red) {
+    const uint32_t lane = threadIdx.x & 63u, wave = wave_id(), l32 = lane & 31u;
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
+    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
+    uint4 w[kSvcRows];
+    svc_load_rows(a, vt, w);
+    uint32_t q = 0;
+#pragma unroll
+    for (int r = 0; r < (int)kSvcRows; ++r) {
+        if ((uint32_t)r < rows) {  // uniform
+            const uint32_t c = small_lag(a, lds, w[r], first + r * (int)kSmallLanes);
+            q = r ? nib_mul(lds + kSmS / 4, q) ^ c : c;
+        }
+    }
+    const uint32_t v = small_finish(lds, q, bw_wave, [](int, uint32_t) {});
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    uint32_t u = 0;
+    if (wave == 0) u = mul_lanes(red[0] ^ red[1] ^ red[2] ^ red[3], bw_tail, l32);
+    return u;
+}
+
 // This thread's blocks: only blocks that overlap the data are read (a block
 // at or past the end -- the seed's cover, n = 0 -- is all masked bytes, and
 // may lie on an unmapped page). COHERENT: agent-scope loads that
@@ -1546,11 +1611,7 @@ __device__ __forceinline__ void small_load(const A& a, uint32_t vt, uint4 (&w)[k
         if ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) {
             const uint8_t* p = a.a0 + 16 * (uint32_t)b;
             if constexpr (COHERENT) {
-                typedef __attribute__((address_space(1))) const uint64_t g_u64;  // global_, not flat_, loads
-                g_u64* q = (g_u64*)p;
-                const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                w[r] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+                w[r] = load16_coherent(p);
             } else {
                 w[r] = load16(p);
             }
@@ -1618,7 +1679,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
 // 1.2-2.8 µs over the host link, repo:profiles/r05h_doorbell_probe.jsonl --
 // else pinned host memory):
 //   0-5  the request, each word {seq (high 32), field (low 32)}: a0 low, a0
-//        high, nb | s0 << 16 | k << 20 | wg0 << 25 (6 bits), eoff, seed low, seed high
+//        high, nb | s0 << 20 | k << 24, eoff | wg0 << 26, seed low, seed high
 //        (CRC-64: the inverted init). A request is taken when all six carry
 //        one seq that is not the last one served (the host writes the words
 //        in any order; a torn read retries);
@@ -1712,11 +1773,11 @@ __device__ __forceinline__ void service_loop(const ServiceArgs& s, uint32_t (&cm
         if (cm == 0u) continue;
         SvcReq r;
         r.a0 = reinterpret_cast<const uint8_t*>((uint64_t)c[1] << 32 | c[0]);
-        r.nb = c[2] & 0xffffu;
-        r.s0 = (c[2] >> 16) & 15u;
-        r.k = (c[2] >> 20) & 31u;
-        r.wg0 = (c[2] >> 25) & 63u;
-        r.eoff = c[3];
+        r.nb = c[2] & 0xfffffu;
+        r.s0 = (c[2] >> 20) & 15u;
+        r.k = (c[2] >> 24) & 31u;
+        r.eoff = c[3] & 0x3ffffffu;
+        r.wg0 = c[3] >> 26;
         r.seed = (uint64_t)c[5] << 32 | c[4];
         r.seq = c[6];
         if (wg < r.wg0) continue;  // no data in this workgroup's part of the layout
@@ -1747,14 +1808,19 @@ __global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s
         a.eoff = r.eoff;
         a.seed = (uint32_t)r.seed;
         if (PCRC_SVC_STAMP) st[2] = __builtin_amdgcn_s_memrealtime();
-        uint4 w[kSmallRows];
-        small_load<true>(a, vt, w);
         const uint32_t bw_tail = lds[kSmLds / 4 + a.k * 32u + l32];
-        if (PCRC_SVC_STAMP) {
-            __builtin_amdgcn_s_waitcnt(0);
-            st[3] = __builtin_amdgcn_s_memrealtime();
+        uint32_t u;
+        if (a.nb > kSmallRows * kSmallLanes) {  // uniform: a mid-size call (up to kSvcRows rows)
+            u = small_value_rows(a, lds, vt, bw_wave, bw_tail, red);
+        } else {
+            uint4 w[kSmallRows];
+            small_load<true>(a, vt, w);
+            if (PCRC_SVC_STAMP) {
+                __builtin_amdgcn_s_waitcnt(0);
+                st[3] = __builtin_amdgcn_s_memrealtime();
+            }
+            u = small_value(a, lds, w, vt, bw_wave, bw_tail, red, PCRC_SVC_STAMP ? st : nullptr);
         }
-        const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red, PCRC_SVC_STAMP ? st : nullptr);
         if (PCRC_SVC_STAMP && wave == 0) {
             asm volatile("" ::"v"(u));
             st[4] = st[5] = __builtin_amdgcn_s_memrealtime();

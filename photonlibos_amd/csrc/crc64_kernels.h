@@ -899,17 +899,17 @@ __device__ __forceinline__ uint64_t tail_word64(uint64_t w, int off, int eoff) {
 // Steps 2-3 of one workgroup's share (blocks w[] loaded for virtual lane vt):
 // the column, the shift to the end of the wave, the wave's factor, the XOR
 // over the 4 waves and the tail factor; the value on wave 0, one barrier.
-__device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const uint32_t* lds,
-                                                  const uint4 (&w)[kSmallRows], uint32_t vt, uint64_t bw_wave,
-                                                  uint64_t bw_tail, uint64_t* red) {
+template <int R>
+__device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const uint32_t* lds, const uint4 (&w)[R],
+                                                  uint32_t vt, uint64_t bw_wave, uint64_t bw_tail, uint64_t* red) {
     const uint32_t lane = threadIdx.x & 63u, wave = wave_id();
     const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
     const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
     // 2. The column: lagged blocks and the row shift (rows that do not exist
     //    cost nothing: crc32c_kernels.h small_wave_value).
-    uint64_t c[kSmallRows];
+    uint64_t c[R];
 #pragma unroll
-    for (int r = 0; r < (int)kSmallRows; ++r) {
+    for (int r = 0; r < R; ++r) {
         c[r] = 0;
         if ((uint32_t)r >= rows) continue;
         const int b = first + r * (int)kSmallLanes;
@@ -924,7 +924,7 @@ __device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const ui
     }
     uint64_t q = c[0];
 #pragma unroll
-    for (int r = 1; r < (int)kSmallRows; ++r)
+    for (int r = 1; r < R; ++r)
         if ((uint32_t)r < rows) q = nib_mul64_pos(lds, kSm64S, q) ^ c[r];
     // 3. Q -> P and the shift to the end of the wave, the wave's and the tail's factors.
     const uint32_t d = 63u - lane, dh = d >> 3;
@@ -1006,10 +1006,17 @@ __global__ __launch_bounds__(256) void crc64_small_service_kernel(ServiceArgs s)
         a.k = r.k;
         a.eoff = r.eoff;
         a.init = r.seed;
-        uint4 w[kSmallRows];
-        small_load<true>(a, vt, w);
         const uint64_t bw_tail = image[kSm64Tail / 8 + a.k * 64u + lane];  // L2-resident: 16 KiB for all k
-        const uint64_t u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+        uint64_t u;
+        if (a.nb > kSmallRows * kSmallLanes) {  // uniform: a mid-size call (crc32c_kernels.h small_value_rows)
+            uint4 w[kSvcRows];
+            svc_load_rows(a, vt, w);
+            u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+        } else {
+            uint4 w[kSmallRows];
+            small_load<true>(a, vt, w);
+            u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+        }
         if (wave == 0 && lane < 2)
             __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg + lane,
                                (uint64_t)r.seq << 32 | (uint32_t)(lane ? u >> 32 : u), __ATOMIC_RELAXED,

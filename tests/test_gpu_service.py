@@ -117,7 +117,7 @@ def test_rewritten_buffer_is_read_fresh(torch_dev, oracle):
 
 def test_idle_end_and_restart(torch_dev, oracle):
     """A short idle time: the service ends after it, the next call starts a
-    new launch (and is itself served by the launch path), calls after that
+    new launch (and is its first request), calls after that
     are served again; turning the service off ends the running launch, so a
     device-wide synchronise returns at once."""
     torch = torch_dev
@@ -202,6 +202,61 @@ def test_crc64_sizes_offsets_seeds(torch_dev, oracle):
         want = oracle.crc64ecma(host[off:off + n], seed)
         assert ck.crc64ecma_extend_at(base + off, n, seed) == want, (off, n, seed)
     _check_served(st0, len(cases))
+
+
+SVC_MAX_BLOCKS = 16 * 33 * 256  # crc32c_kernels.h kSvcMaxBlocks: 16 rows of the 8448-lane layout
+
+
+@pytest.mark.parametrize("kind", ["crc32c", "crc64"])
+def test_mid_sizes_served(torch_dev, oracle, kind):
+    """256 KiB .. 2 MiB (the service's multi-row form, small_value_rows):
+    every row boundary and the span limit at every offset class, random
+    sizes and seeds, a buffer rewritten by a kernel and by a host copy in
+    between: every call equal to the oracle and served by the service; one
+    block past the limit takes the long kernel (not served) and is exact."""
+    torch = torch_dev
+    cap = SVC_MAX_BLOCKS * 16 + 64
+    rng = np.random.default_rng(0x3D1 + (kind == "crc64"))
+    host = rng.integers(0, 256, cap, dtype=np.uint8)
+    dbuf = torch.from_numpy(host).cuda()
+    torch.cuda.synchronize()
+    base = dbuf.data_ptr()
+    cover = 4 if kind == "crc32c" else 8  # the seed's (init's) bytes lie inside the grid
+
+    def one(off, n, seed):
+        if kind == "crc32c":
+            seed &= 0xFFFFFFFF
+            return ck.crc32c_extend_at(base + off, n, seed), oracle.crc32c(host[off:off + n], seed)
+        return ck.crc64ecma_extend_at(base + off, n, seed), oracle.crc64ecma(host[off:off + n], seed)
+
+    r = random.Random(11)
+    lane_bytes = 33 * 256 * 16
+    cases = [(0, 2 * lane_bytes + 1, 1), (15, 2 * lane_bytes - 14, 2), (1, SVC_MAX_BLOCKS * 16 - 1, 3),
+             (0, SVC_MAX_BLOCKS * 16, 4), (7, SVC_MAX_BLOCKS * 16 - 7, 5)]
+    cases += [(o, k * lane_bytes + d - o, r.getrandbits(64)) for k in range(3, 17) for o, d in ((0, 0), (1, 1), (9, -3))]
+    cases += [(r.randrange(16), r.randrange(2 * lane_bytes + 1, SVC_MAX_BLOCKS * 16 - 16), r.getrandbits(64))
+              for _ in range(40)]
+    cases = [(o, n, s) for o, n, s in cases if (o + max(n, cover) + 15) // 16 <= SVC_MAX_BLOCKS]
+    st0 = ck.small_service_stats()
+    for i, (off, n, seed) in enumerate(cases):
+        if i == len(cases) // 3:  # rewritten by a kernel on another stream
+            side = torch.cuda.Stream()
+            ck.fill_splitmix(dbuf, cap, cap, 1, 0xBEEF, stream=side.cuda_stream)
+            side.synchronize()
+            host = dbuf.cpu().numpy()
+        if i == 2 * len(cases) // 3:  # rewritten by a host-to-device copy
+            host = rng.integers(0, 256, cap, dtype=np.uint8)
+            dbuf.copy_(torch.from_numpy(host))
+            torch.cuda.current_stream().synchronize()
+        got, want = one(off, n, seed)
+        assert got == want, (kind, off, n, seed)
+    _check_served(st0, len(cases))
+    # one block past the span: the launch path (the long kernel), still exact
+    s1 = _served()
+    for off, n in ((0, SVC_MAX_BLOCKS * 16 + 1), (5, SVC_MAX_BLOCKS * 16 - 4)):
+        got, want = one(off, n, 77)
+        assert got == want, (kind, off, n)
+    assert _served() == s1
 
 
 def test_big_lds_launch_ends_service(torch_dev, oracle):
