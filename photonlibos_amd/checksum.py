@@ -521,6 +521,12 @@ def set_routed_wait(spin_us=40, sleep_ahead=True):
     _check(lib().photon_crc_set_routed_wait(spin_us, 1 if sleep_ahead else 0))
 
 
+def set_mid_kernel(on=True):
+    """Spans over 256 KiB up to 32 MiB: the mid layout (default) or, off, the
+    long kernel (tuning; tests of the long kernel's plan)."""
+    _check(lib().photon_crc_set_mid_kernel(1 if on else 0))
+
+
 def set_small_service(idle_us):
     """Routed small crc32c_extend / crc64ecma_extend calls through a resident
     service launch that ends after idle_us without a call; 0 = off, a launch

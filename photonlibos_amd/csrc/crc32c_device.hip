@@ -620,6 +620,7 @@ hipError_t relaxed_capture(F f) {
 // graph share its states and must not run at the same time (ADVICE r4:
 // multi-workgroup captures used to be refused with -ENOTSUP).
 constexpr uint64_t kStateBytes = 8 + 8 * kLongMaxGrid;
+static_assert(8 * kTreeLine * (1 + kTreeGroups) <= kStateBytes, "long_reduce_tree words");
 struct CapState {
     int dev;
     void* p;
@@ -815,11 +816,14 @@ std::vector<uint32_t> small_image_host() {
             for (uint32_t v = 0; v < 16; ++v) img[off / 4 + t * 16 + v] = mulmod(v << (4 * t), k);
     };
     for (uint32_t j = 1; j <= 3; ++j) nibbles(kSmD + (j - 1) * kNib, xpow(32ull * j));  // x^(32 j)
-    nibbles(kSmS, xpow(8ull * 16ull * kSmallLanes));        // one row of V blocks
+    nibbles(kSmS, xpow(8ull * 16ull * kSmallLanes));        // one row of the small layout's V blocks
     for (uint32_t dl = 0; dl < 8; ++dl) nibbles(kSmA + dl * kNib, xpow(32ull + 128ull * dl));
     for (uint32_t dh = 1; dh < 8; ++dh) nibbles(kSmB + (dh - 1) * kNib, xpow(1024ull * dh));
-    for (uint32_t w = 0; w < 4 * kSmallWg; ++w)
-        mul_basis(xpow(8192ull * (4 * kSmallWg - 1 - w)), &img[kSmWave / 4 + w * 32]);
+    nibbles(kSmS2, xpow(8ull * 16ull * kMidLanes));         // one row of the mid layout's
+    const uint32_t step = xpow(8192ull);                      // one wave of 64 blocks
+    uint32_t k = xpow(0);
+    for (uint32_t d = 0; d < 4 * kMidWg; ++d, k = mulmod(k, step))  // d waves after this one
+        mul_basis(k, &img[kSmWave / 4 + d * 32]);
     for (uint32_t k = 0; k < 32; ++k) mul_basis(xpow_inv(8ull * k), &img[kSmTail / 4 + k * 32]);
     return img;
 }
@@ -872,10 +876,11 @@ std::vector<uint64_t> small64_image_host() {
     nibbles(kSm64S, xpow64(8ull * 16ull * kSmallLanes));
     for (uint32_t dl = 0; dl < 8; ++dl) nibbles(kSm64A + dl * kNib64, xpow64(64ull + 128ull * dl));
     for (uint32_t dh = 1; dh < 8; ++dh) nibbles(kSm64B + (dh - 1) * kNib64, xpow64(1024ull * dh));
-    for (uint32_t w = 0; w < 4 * kSmallWg; ++w) {
-        const uint64_t k = xpow64(8192ull * (4 * kSmallWg - 1 - w));
-        for (int i = 0; i < 64; ++i) img[kSm64Wave / 8 + w * 64 + i] = mulmod64(1ull << i, k);
-    }
+    nibbles(kSm64S2, xpow64(8ull * 16ull * kMidLanes));
+    const uint64_t step = xpow64(8192ull);
+    uint64_t k = xpow64(0);
+    for (uint32_t d = 0; d < 4 * kMidWg; ++d, k = mulmod64(k, step))  // d waves after this one
+        for (int i = 0; i < 64; ++i) img[kSm64Wave / 8 + d * 64 + i] = mulmod64(1ull << i, k);
     for (uint32_t k = 0; k < 32; ++k) {
         const uint64_t kk = xpow64_inv(8ull * k);
         for (int i = 0; i < 64; ++i) img[kSm64Tail / 8 + k * 64 + i] = mulmod64(1ull << i, kk);
@@ -937,10 +942,33 @@ bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t
     return true;
 }
 
+// The mid layout (crc32c_kernels.h kMidWg): spans over kSmallBlocks up to
+// kMidBlocks (32 MiB; CRC-64 kMid64Blocks, 16 MiB) while
+// photon_crc_set_mid_kernel is on, else false (the long kernel's case).
+std::atomic<int> g_mid_kernel{1};
+
+template <typename A, typename Fit>
+bool mid_layout(A* a, uint32_t* grid, Fit fit) {
+    if (!g_mid_kernel.load(std::memory_order_relaxed) || !fit()) return false;
+    *grid = a->nb > kMidLanes ? kMidWg : (a->nb + 255) / 256;
+    a->wg0 = kMidWg - *grid;
+    return true;
+}
+bool mid_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t* grid) {
+    return mid_layout(a, grid, [&] { return small_args(p, n, seed, a, grid, kMidBlocks); });
+}
+bool mid64_args(const void* p, uint64_t n, uint64_t seed, Small64Args* a, uint32_t* grid) {
+    return mid_layout(a, grid, [&] { return small64_args(p, n, seed, a, grid, kMid64Blocks); });
+}
+
 }  // namespace
 
 int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st, int cus,
                        uint32_t tag);
+int extend_device_big(int dev, const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st,
+                      int cus, uint32_t tag);
+int extend64_device_big(int dev, const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
+                        int cus, uint32_t tag);
 int extend64_device_long(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
                          int cus, uint32_t tag);
 
@@ -984,6 +1012,12 @@ int photon_crc_set_batch_grid(int workgroups) {
 }
 
 void photon_crc_test_fail_next(int n) { g_fail_next = n > 0 ? n : 0; }
+
+int photon_crc_set_mid_kernel(int on) {
+    if (on != 0 && on != 1) return fail(-EINVAL, "mid kernel: 0 or 1");
+    g_mid_kernel.store(on, std::memory_order_relaxed);
+    return 0;
+}
 
 int photon_crc_test_tables(int which, uint32_t* out, int n) {
     if (!out) return fail(-EINVAL, "null output");
@@ -1491,15 +1525,35 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
             sa.acc = static_cast<uint64_t*>(state);
             sa.tbase = base;
             sa.treset = reset;
-            hipLaunchKernelGGL(crc64_small_kernel, dim3(sgrid), dim3(256), 0, st, sa);
+            hipLaunchKernelGGL((crc64_small_kernel<kSmallLanes, kSmallRows>), dim3(sgrid), dim3(256), 0, st, sa);
             return hipGetLastError();
         });
     }
-    return pcrc::extend64_device_long(d_data, nbytes, seed, d_out, st, cus, 0);
+    return pcrc::extend64_device_big(dev, d_data, nbytes, seed, d_out, st, cus, 0);
 }
 }  // extern "C"
 
 namespace pcrc {
+// A span over the small kernel's: the mid layout up to 32 MiB, else the long
+// kernel (tag: as extend64_device_long).
+int extend64_device_big(int dev, const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
+                        int cus, uint32_t tag) {
+    Small64Args sa{};
+    uint32_t grid = 0;
+    if (!mid64_args(d_data, nbytes, seed, &sa, &grid))
+        return extend64_device_long(d_data, nbytes, seed, d_out, st, cus, tag);
+    if (int rc = small64_image(dev, &sa.image)) return rc;
+    sa.out = d_out;
+    sa.tag = tag;  // slots unset: the tag goes to long_reduce's result words
+    return long_launch(st, grid, "crc64_small_kernel (mid) launch", [&](void* state, uint64_t base, uint32_t reset) {
+        sa.acc = static_cast<uint64_t*>(state);
+        sa.tbase = base;
+        sa.treset = reset;
+        hipLaunchKernelGGL((crc64_small_kernel<kMidLanes, kMid64Rows>), dim3(grid), dim3(256), 0, st, sa);
+        return hipGetLastError();
+    });
+}
+
 // The long kernel for photon_crc64ecma_extend_device (tag: as extend_device_long).
 int extend64_device_long(const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
                          int cus, uint32_t tag) {
@@ -1607,16 +1661,36 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
             sa.acc = static_cast<uint32_t*>(state);
             sa.tbase = base;
             sa.treset = reset;
-            hipLaunchKernelGGL(crc32c_small_kernel, dim3(sgrid), dim3(256), 0, st, sa);
+            hipLaunchKernelGGL((crc32c_small_kernel<kSmallLanes, kSmallRows>), dim3(sgrid), dim3(256), 0, st, sa);
             return hipGetLastError();
         });
     }
-    return pcrc::extend_device_long(d_data, nbytes, seed, d_out, st, cus, 0);
+    return pcrc::extend_device_big(dev, d_data, nbytes, seed, d_out, st, cus, 0);
 }
 
 }  // extern "C"
 
 namespace pcrc {
+// A span over the small kernel's: the mid layout up to 32 MiB, else the long
+// kernel (tag: as extend_device_long).
+int extend_device_big(int dev, const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st,
+                      int cus, uint32_t tag) {
+    SmallArgs sa{};
+    uint32_t grid = 0;
+    if (!mid_args(d_data, nbytes, seed, &sa, &grid))
+        return extend_device_long(d_data, nbytes, seed, d_out, st, cus, tag);
+    if (int rc = small_image(dev, &sa.image)) return rc;
+    sa.out = d_out;
+    sa.tag = tag;  // slots unset: the tag goes to long_reduce's result word
+    return long_launch(st, grid, "crc32c_small_kernel (mid) launch", [&](void* state, uint64_t base, uint32_t reset) {
+        sa.acc = static_cast<uint32_t*>(state);
+        sa.tbase = base;
+        sa.treset = reset;
+        hipLaunchKernelGGL((crc32c_small_kernel<kMidLanes, kMidRows>), dim3(grid), dim3(256), 0, st, sa);
+        return hipGetLastError();
+    });
+}
+
 // The long kernel for photon_crc32c_extend_device (and, with a tag, for a
 // routed call whose result word lands tagged in pinned memory).
 int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st, int cus,
@@ -2045,7 +2119,7 @@ int routed_small(int dev, const SmallArgs& sa0, uint32_t sgrid, uint32_t* crc_ou
         // writes them now, and no slot can carry this tag before the launch
         memset(r->h, 0, 8ull * sgrid);
         sa.slots = static_cast<uint32_t*>(r->d);
-        hipLaunchKernelGGL(crc32c_small_kernel, dim3(sgrid), dim3(256), 0, r->st, sa);
+        hipLaunchKernelGGL((crc32c_small_kernel<kSmallLanes, kSmallRows>), dim3(sgrid), dim3(256), 0, r->st, sa);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "crc32c_small_kernel launch");
     }
@@ -2072,11 +2146,11 @@ int routed_long(int dev, const uint8_t* p, uint64_t n, uint32_t crc, uint32_t* c
         r->tag = r->tag == 0xffffffffu ? 1u : r->tag + 1u;
         tag = r->tag;
         memset(r->h, 0, 8);
-        rc = extend_device_long(p, n, crc, static_cast<uint32_t*>(r->d), r->st, cus, tag);
+        rc = extend_device_big(dev, p, n, crc, static_cast<uint32_t*>(r->d), r->st, cus, tag);
     }
     if (!rc) {
         uint32_t x = 0;
-        rc = wait_tagged(r, tag, 1, &x, 1, n, "crc32c_long_kernel (routed)");
+        rc = wait_tagged(r, tag, 1, &x, 1, n, "crc32c mid/long kernel (routed)");
         if (!rc) {
             *crc_out = x;
         } else {
@@ -2103,11 +2177,11 @@ int routed_long64(int dev, const uint8_t* p, uint64_t n, uint64_t crc, uint64_t*
         r->tag = r->tag == 0xffffffffu ? 1u : r->tag + 1u;
         tag = r->tag;
         memset(r->h, 0, 16);
-        rc = extend64_device_long(p, n, crc, static_cast<uint64_t*>(r->d), r->st, cus, tag);
+        rc = extend64_device_big(dev, p, n, crc, static_cast<uint64_t*>(r->d), r->st, cus, tag);
     }
     if (!rc) {
         uint32_t x[2] = {0, 0};
-        rc = wait_tagged(r, tag, 1, x, 2, n, "crc64_long_kernel (routed)");
+        rc = wait_tagged(r, tag, 1, x, 2, n, "crc64 mid/long kernel (routed)");
         if (rc) {
             const volatile uint64_t* w = static_cast<const volatile uint64_t*>(r->h);
             char buf[128];
@@ -2135,7 +2209,7 @@ int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* cr
         sa.tag = r->tag;
         sa.slots = static_cast<uint64_t*>(r->d);
         memset(r->h, 0, 16ull * sgrid);  // as routed_small
-        hipLaunchKernelGGL(crc64_small_kernel, dim3(sgrid), dim3(256), 0, r->st, sa);
+        hipLaunchKernelGGL((crc64_small_kernel<kSmallLanes, kSmallRows>), dim3(sgrid), dim3(256), 0, r->st, sa);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) rc = hip_fail(e, "crc64_small_kernel launch");
     }

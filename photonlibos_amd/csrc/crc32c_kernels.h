@@ -1176,10 +1176,78 @@ __device__ __forceinline__ void long_reduce_word(T v, T* state, T* out, F fin, u
     }
 }
 
+// The one-round-trip word as a two-level tree (round 5, the default,
+// PCRC_LONG_REDUCE_TREE): device-scope atomics on ONE word serialise at the
+// memory side, ≈12 ns each, so a flat word costs a launch of G workgroups
+// about 2 G x 12 ns -- 10 µs at 512 workgroups, 3-4 µs at 256
+// (repo:scripts/probe_atomics.hip, repo:profiles/r05m_probe_atomics.jsonl:
+// 512 workgroups 13.3 µs per launch on one word, 3.0 µs spread over 16 words,
+// 2.9 µs with no atomic). Workgroup b counts on group word i = (base + b) mod
+// 16 (16 words, each on a 128-byte line of its own; the same {count, XOR}
+// form); the group's last member (its add returns count_i - 1, count_i = the
+// members of i among all workgroups of the state so far, a closed form in
+// base + grid) zeroes the group's XOR and adds {m_i, XOR} to the top word
+// (m_i = the group's members in this launch), whose count therefore ends at
+// base + grid as the flat word's did; the add that reaches it is the last
+// group's and writes the result. Both halves' words advance on every launch
+// (a CRC32C value's high half is 0), so one state serves both CRCs.
+#ifndef PCRC_LONG_REDUCE_TREE
+#define PCRC_LONG_REDUCE_TREE 1
+#endif
+constexpr uint32_t kTreeGroups = 16, kTreeLine = 16;  // group i's words at state + 16 (1 + i) (8-byte words)
+template <typename T, typename F>
+__device__ __forceinline__ void long_reduce_tree(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
+                                                 uint32_t tag = 0) {
+    constexpr uint32_t kHalves = sizeof(T) / 4;
+    const uint32_t grid = gridDim.x, lane = threadIdx.x & 63u;
+    if (grid == 1) {
+        long_reduce_word(v, state, out, fin, base, reset, tag);
+        return;
+    }
+    const uint64_t v0 = (uint64_t)__shfl((unsigned long long)(uint64_t)v, 0);  // v is valid on lane 0
+    if (lane < 2) {
+        unsigned long long* words = reinterpret_cast<unsigned long long*>(state);
+        const uint64_t end = base + grid;  // the state's workgroups after this launch
+        const uint32_t i = (uint32_t)((base + blockIdx.x) % kTreeGroups);
+        auto members = [&](uint64_t below) {  // workgroups g < below of the state with g mod 16 = i
+            return below > i ? (below - 1 - i) / kTreeGroups + 1 : 0ull;
+        };
+        const uint64_t ci = members(end), mi = ci - members(base);
+        unsigned long long* g = words + kTreeLine * (1 + i) + lane;
+        const uint32_t half = lane < kHalves ? (uint32_t)(v0 >> (32 * lane)) : 0u;
+        (void)__hip_atomic_fetch_xor(g, (unsigned long long)half, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long old = __hip_atomic_fetch_add(g, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(old >> 32) == (uint32_t)(ci - 1)) {  // the group's last member in this launch
+            __hip_atomic_store(g, reset ? 0ull : (unsigned long long)(uint32_t)ci << 32, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long* t = words + lane;
+            (void)__hip_atomic_fetch_xor(t, (unsigned long long)(uint32_t)old, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long top = __hip_atomic_fetch_add(t, (unsigned long long)mi << 32, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(top >> 32) + (uint32_t)mi == (uint32_t)end) {  // the last group: the result
+                if (lane < kHalves) {
+                    const uint32_t r =
+                        (uint32_t)((uint64_t)fin((T)((uint64_t)(uint32_t)top << (32 * lane))) >> (32 * lane));
+                    if (tag)
+                        __hip_atomic_store(reinterpret_cast<uint64_t*>(out) + lane, (uint64_t)tag << 32 | r,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    else
+                        reinterpret_cast<uint32_t*>(out)[lane] = r;
+                }
+                __hip_atomic_store(t, reset ? 0ull : (unsigned long long)(uint32_t)end << 32, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
 template <typename T, typename F, bool FENCED = false>
 __device__ __forceinline__ void long_reduce(T v, T* state, T* out, F fin, uint64_t base, uint32_t reset,
                                             uint32_t tag = 0) {
-    if constexpr (PCRC_LONG_REDUCE_WORD && !FENCED)
+    if constexpr (PCRC_LONG_REDUCE_WORD && PCRC_LONG_REDUCE_TREE && !FENCED)
+        long_reduce_tree(v, state, out, fin, base, reset, tag);
+    else if constexpr (PCRC_LONG_REDUCE_WORD && !FENCED)
         long_reduce_word(v, state, out, fin, base, reset, tag);
     else
         long_reduce_slots<T, F, FENCED>(v, state, out, fin, base, reset, tag);
@@ -1414,13 +1482,23 @@ constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of bloc
 // seed's cover (the reference's 128 KiB at buf+1 is 8193 blocks) is one row.
 constexpr uint32_t kSmallWg = 33, kSmallLanes = kSmallWg * 256;  // V = 8448 virtual lanes
 constexpr uint32_t kSmallRows = (kSmallBlocks + 1 + kSmallLanes - 1) / kSmallLanes;  // 2
+// The MID layout (photon_crc32c_extend_device and routed calls over 256 KiB
+// up to 32 MiB, where the long kernel's fixed cost -- ≈12 µs of table
+// prologue, ramp-up and drain -- is most of the call): the same code with
+// kMidWg = 512 workgroups (two per CU), V = 131,072 virtual lanes and up to
+// kMidRows rows per thread.
+constexpr uint32_t kMidWg = 512, kMidLanes = kMidWg * 256, kMidRows = 16;
+constexpr uint32_t kMidBlocks = kMidRows * kMidLanes;         // 2,097,152 blocks: 32 MiB
 constexpr uint32_t kNib = 512;                                // bytes of one nibble-sliced multiplier
 // D_j: x^(32 j), j = 1..3 (a block's lagged CRC in ONE table step, not three
-// dependent ones), S: one row, A_dl, B_dh: the lane's finish.
-constexpr uint32_t kSmD = 0, kSmS = 3 * kNib, kSmA = 4 * kNib, kSmB = kSmA + 8 * kNib;
-constexpr uint32_t kSmLds = kSmB + 7 * kNib;                  // 9728 B of tables in LDS
-constexpr uint32_t kSmWave = kSmLds;  // 4 kSmallWg x 32 words: basis of x^(8192 (4 kSmallWg - 1 - wave))
-constexpr uint32_t kSmTail = kSmWave + 4u * kSmallWg * 32u * 4u;  // 32 x 32 words: basis of x^(-8 k), k < 32
+// dependent ones), S: one row of the small layout, A_dl, B_dh: the lane's
+// finish, S2: one row of the mid layout.
+constexpr uint32_t kSmD = 0, kSmS = 3 * kNib, kSmA = 4 * kNib, kSmB = kSmA + 8 * kNib, kSmS2 = kSmB + 7 * kNib;
+constexpr uint32_t kSmLds = kSmS2 + kNib;                     // 10,240 B of tables in LDS
+// 4 kMidWg x 32 words: basis of x^(8192 d), d = the waves after this one in
+// its layout (4 kSmallWg - 1 - wave, or 4 kMidWg - 1 - wave)
+constexpr uint32_t kSmWave = kSmLds;
+constexpr uint32_t kSmTail = kSmWave + 4u * kMidWg * 32u * 4u;  // 32 x 32 words: basis of x^(-8 k), k < 32
 constexpr uint32_t kSmImage = kSmTail + 32u * 32u * 4u;       // bytes of the device image
 
 struct SmallArgs {
@@ -1474,7 +1552,7 @@ __device__ __forceinline__ uint32_t small_lag(const SmallArgs& a, const uint32_t
 
 // Q -> the wave's value: x^(32 + 128 dl), then x^(1024 dh) (d = 63 - lane:
 // Q -> P and the shift to the end of the wave), the 64-lane XOR and the
-// wave's factor x^(8192 (4 kSmallWg - 1 - (4 wg + wave))) (bw_wave).
+// wave's factor x^(8192 (V / 64 - 1 - (4 wg + wave))) (bw_wave).
 template <typename Stamp>
 __device__ __forceinline__ uint32_t small_finish(const uint32_t* lds, uint32_t q, uint32_t bw_wave, Stamp stamp) {
     const uint32_t lane = threadIdx.x & 63u, l32 = lane & 31u;
@@ -1492,9 +1570,9 @@ __device__ __forceinline__ uint32_t small_finish(const uint32_t* lds, uint32_t q
 // Steps 2-3 of one wave's share (blocks w[] loaded for virtual lane vt, the
 // tables at lds): the column, the shift to the end of the wave and the
 // wave's factor (bw_wave): the wave's value, on every lane.
-__device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const uint32_t* lds,
-                                                     const uint4 (&w)[kSmallRows], uint32_t vt, uint32_t bw_wave,
-                                                     uint64_t* ts = nullptr) {
+template <uint32_t V, int R>
+__device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const uint32_t* lds, const uint4 (&w)[R],
+                                                     uint32_t vt, uint32_t bw_wave, uint64_t* ts = nullptr) {
     auto stamp = [&](int i, uint32_t dep) {  // bench-only builds (PCRC_SVC_STAMP): time after `dep` is known
         if (PCRC_SVC_STAMP && ts) {
             asm volatile("" ::"v"(dep));
@@ -1502,24 +1580,25 @@ __device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const u
         }
     };
     // uniform (a scalar branch below): rows past the last are not computed
-    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
-    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;  // this thread's block in row 0
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + V - 1) / V);
+    const int first = (int)a.nb - (int)(rows * V) + (int)vt;  // this thread's block in row 0
     // 2. The column: lagged blocks (independent per row) and the row shift.
     // A wave64 VALU instruction takes 4 cycles on a SIMD16: at 1-3 rows per
     // thread the column is most of a small call's device time, so a row that
     // does not exist costs nothing (PCRC_SVC_STAMP probe: 1.0 µs for 3 rows).
-    uint32_t c[kSmallRows];
+    uint32_t c[R];
 #pragma unroll
-    for (int r = 0; r < (int)kSmallRows; ++r) {
+    for (int r = 0; r < R; ++r) {
         c[r] = 0;
         if ((uint32_t)r >= rows) continue;
-        c[r] = small_lag(a, lds, w[r], first + r * (int)kSmallLanes);
+        c[r] = small_lag(a, lds, w[r], first + r * (int)V);
     }
-    stamp(8, c[0] ^ c[kSmallRows - 1]);
+    stamp(8, c[0] ^ c[R - 1]);
+    constexpr uint32_t kRow = (V == kSmallLanes ? kSmS : kSmS2) / 4;  // the row shift x^(128 V)
     uint32_t q = c[0];
 #pragma unroll
-    for (int r = 1; r < (int)kSmallRows; ++r)
-        if ((uint32_t)r < rows) q = nib_mul(lds + kSmS / 4, q) ^ c[r];
+    for (int r = 1; r < R; ++r)
+        if ((uint32_t)r < rows) q = nib_mul(lds + kRow, q) ^ c[r];
     stamp(9, q);
     // 3. Q -> P, the shift to the end of the wave, the wave's factor.
     return small_finish(lds, q, bw_wave, stamp);
@@ -1527,11 +1606,12 @@ __device__ __forceinline__ uint32_t small_wave_value(const SmallArgs& a, const u
 
 // The workgroup's value (small_wave_value of its 4 waves XORed, times the
 // tail factor bw_tail), valid on wave 0 (every lane); one barrier.
-__device__ __forceinline__ uint32_t small_value(const SmallArgs& a, const uint32_t* lds, const uint4 (&w)[kSmallRows],
+template <uint32_t V, int R>
+__device__ __forceinline__ uint32_t small_value(const SmallArgs& a, const uint32_t* lds, const uint4 (&w)[R],
                                                 uint32_t vt, uint32_t bw_wave, uint32_t bw_tail, uint32_t* red,
                                                 uint64_t* ts = nullptr) {
     const uint32_t lane = threadIdx.x & 63u, wave = wave_id(), l32 = lane & 31u;
-    const uint32_t v = small_wave_value(a, lds, w, vt, bw_wave, ts);
+    const uint32_t v = small_wave_value<V, R>(a, lds, w, vt, bw_wave, ts);
     if (lane == 0) red[wave] = v;
     __syncthreads();
     uint32_t u = 0;
@@ -1552,61 +1632,22 @@ __device__ __forceinline__ uint4 load16_coherent(const uint8_t* p) {
     return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-// The service's form for calls of up to kSvcRows rows (≈2 MiB; the small
-// kernel's layout, more rows per thread): every row's block of this thread
-// loaded at once (agent-scope loads), then the column, the finish and the
-// workgroup's value as small_value.
+// The service takes calls of up to kSvcRows rows of its layout (≈2 MiB).
 constexpr uint32_t kSvcRows = 16;
 constexpr uint32_t kSvcMaxBlocks = kSvcRows * kSmallLanes;  // 135,168 blocks (2.06 MiB)
-
-// This thread's blocks of every row (as small_load<true>, kSvcRows rows; the
-// rows past the call's are not read).
-template <typename A>
-__device__ __forceinline__ void svc_load_rows(const A& a, uint32_t vt, uint4 (&w)[kSvcRows]) {
-    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
-    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
-#pragma unroll
-    for (int r = 0; r < (int)kSvcRows; ++r) {
-        w[r] = make_uint4(0, 0, 0, 0);
-        const int b = first + r * (int)kSmallLanes;
-        if ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) w[r] = load16_coherent(a.a0 + 16 * (uint32_t)b);
-    }
-}
-__device__ __forceinline__ uint32_t small_value_rows(const SmallArgs& a, const uint32_t* lds, uint32_t vt,
-                                                     uint32_t bw_wave, uint32_t bw_tail, uint32_t* red) {
-    const uint32_t lane = threadIdx.x & 63u, wave = wave_id(), l32 = lane & 31u;
-    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
-    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
-    uint4 w[kSvcRows];
-    svc_load_rows(a, vt, w);
-    uint32_t q = 0;
-#pragma unroll
-    for (int r = 0; r < (int)kSvcRows; ++r) {
-        if ((uint32_t)r < rows) {  // uniform
-            const uint32_t c = small_lag(a, lds, w[r], first + r * (int)kSmallLanes);
-            q = r ? nib_mul(lds + kSmS / 4, q) ^ c : c;
-        }
-    }
-    const uint32_t v = small_finish(lds, q, bw_wave, [](int, uint32_t) {});
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    uint32_t u = 0;
-    if (wave == 0) u = mul_lanes(red[0] ^ red[1] ^ red[2] ^ red[3], bw_tail, l32);
-    return u;
-}
 
 // This thread's blocks: only blocks that overlap the data are read (a block
 // at or past the end -- the seed's cover, n = 0 -- is all masked bytes, and
 // may lie on an unmapped page). COHERENT: agent-scope loads that
 // skip the CU's L1 (the resident service below reads buffers that other
 // launches rewrite between its requests); else nontemporal loads.
-template <bool COHERENT, typename A>
-__device__ __forceinline__ void small_load(const A& a, uint32_t vt, uint4 (&w)[kSmallRows]) {
-    const uint32_t rows = (a.nb + kSmallLanes - 1) / kSmallLanes;
-    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
+template <bool COHERENT, uint32_t V, int R, typename A>
+__device__ __forceinline__ void small_load(const A& a, uint32_t vt, uint4 (&w)[R]) {
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + V - 1) / V);
+    const int first = (int)a.nb - (int)(rows * V) + (int)vt;
 #pragma unroll
-    for (int r = 0; r < (int)kSmallRows; ++r) {
-        const int b = first + r * (int)kSmallLanes;
+    for (int r = 0; r < R; ++r) {
+        const int b = first + r * (int)V;
         w[r] = make_uint4(0, 0, 0, 0);
         if ((uint32_t)r < rows && b >= 0 && 16u * (uint32_t)b < a.eoff) {
             const uint8_t* p = a.a0 + 16 * (uint32_t)b;
@@ -1619,6 +1660,10 @@ __device__ __forceinline__ void small_load(const A& a, uint32_t vt, uint4 (&w)[k
     }
 }
 
+// V = kSmallLanes, R = kSmallRows: the small layout; V = kMidLanes, R =
+// kMidRows: the mid layout (the same steps; 512 workgroups, a row shift of its
+// own, long_reduce over up to 512 workgroup values).
+template <uint32_t V, int R>
 __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSmLds / 4];
     __shared__ uint32_t red[4];
@@ -1627,16 +1672,17 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
     const uint32_t vt = wg * 256u + tid;                   // virtual lane
     // 1. The table copy first (vmcnt counts in issue order), then the payload
     //    rows, then the basis words this thread needs at the end.
-    constexpr uint32_t kVec = kSmLds / 16;  // 608 16-byte pieces
+    constexpr uint32_t kVec = kSmLds / 16;  // 640 16-byte pieces
+    static_assert(kVec <= 3 * 256, "table copy: 3 pieces per thread");
     u32x4 tv[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const uint32_t j = (uint32_t)i * 256u + tid;
         tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
     }
-    uint4 w[kSmallRows];
-    small_load<false>(a, vt, w);
-    const uint32_t bw_wave = a.image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
+    uint4 w[R];
+    small_load<false, V>(a, vt, w);
+    const uint32_t bw_wave = a.image[kSmWave / 4 + (V / 64u - 1u - (wg * 4u + wave)) * 32u + l32];
     const uint32_t bw_tail = a.image[kSmTail / 4 + a.k * 32u + l32];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -1644,7 +1690,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
         if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
     }
     lds_barrier();
-    const uint32_t u = small_value(a, lds, w, vt, bw_wave, bw_tail, red);
+    const uint32_t u = small_value<V, R>(a, lds, w, vt, bw_wave, bw_tail, red);
     if (wave == 0) {
         if (a.slots) {
             if (lane == 0) {
@@ -1655,7 +1701,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
                     a.slots[blockIdx.x] = u;
             }
         } else {
-            long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset);
+            long_reduce(u, a.acc, a.out, [](uint32_t x) { return x; }, a.tbase, a.treset, a.tag);
         }
     }
 }
@@ -1796,7 +1842,7 @@ __global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s
         *reinterpret_cast<u32x4*>(lds + 4 * j) = *((const g_u32x4*)image + j);
     for (uint32_t j = tid; j < 32u * 32u / 4u; j += 256u)
         *reinterpret_cast<u32x4*>(lds + kSmLds / 4 + 4 * j) = *((const g_u32x4*)(image + kSmTail / 4) + j);
-    const uint32_t bw_wave = image[kSmWave / 4 + (wg * 4u + wave) * 32u + l32];
+    const uint32_t bw_wave = image[kSmWave / 4 + (4u * kSmallWg - 1u - (wg * 4u + wave)) * 32u + l32];
     __syncthreads();
     uint64_t st[16] = {};  // PCRC_SVC_STAMP builds: 0-7 service_loop / below, 8-12 inside small_wave_value
     service_loop(s, cmd, PCRC_SVC_STAMP ? st : nullptr, [&](const SvcReq& r) {
@@ -1810,16 +1856,19 @@ __global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s
         if (PCRC_SVC_STAMP) st[2] = __builtin_amdgcn_s_memrealtime();
         const uint32_t bw_tail = lds[kSmLds / 4 + a.k * 32u + l32];
         uint32_t u;
-        if (a.nb > kSmallRows * kSmallLanes) {  // uniform: a mid-size call (up to kSvcRows rows)
-            u = small_value_rows(a, lds, vt, bw_wave, bw_tail, red);
+        if (a.nb > kSmallRows * kSmallLanes) {  // uniform: a call of up to kSvcRows rows
+            uint4 w[kSvcRows];
+            small_load<true, kSmallLanes>(a, vt, w);
+            u = small_value<kSmallLanes, kSvcRows>(a, lds, w, vt, bw_wave, bw_tail, red);
         } else {
             uint4 w[kSmallRows];
-            small_load<true>(a, vt, w);
+            small_load<true, kSmallLanes>(a, vt, w);
             if (PCRC_SVC_STAMP) {
                 __builtin_amdgcn_s_waitcnt(0);
                 st[3] = __builtin_amdgcn_s_memrealtime();
             }
-            u = small_value(a, lds, w, vt, bw_wave, bw_tail, red, PCRC_SVC_STAMP ? st : nullptr);
+            u = small_value<kSmallLanes, kSmallRows>(a, lds, w, vt, bw_wave, bw_tail, red,
+                                                     PCRC_SVC_STAMP ? st : nullptr);
         }
         if (PCRC_SVC_STAMP && wave == 0) {
             asm volatile("" ::"v"(u));

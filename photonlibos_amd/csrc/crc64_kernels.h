@@ -855,10 +855,15 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
 // lanes read position t's 16 entries: 128 contiguous bytes, no conflicts.
 // The reference times crc64ecma on 128 KiB at buf+1 (test_checksum.cpp:204-216).
 constexpr uint32_t kNib64 = 2048;
+// The mid layout at 64 bits takes up to 8 rows (16 MiB): past that the long
+// kernel is faster (repo:profiles/r05n_probe_mid.jsonl: 32 MiB 20.1 µs per
+// call queued against 16.2; 16 MiB 13.7 against 16.0).
+constexpr uint32_t kMid64Rows = 8, kMid64Blocks = kMid64Rows * kMidLanes;
 constexpr uint32_t kSm64D = 0, kSm64S = kNib64, kSm64A = 2 * kNib64, kSm64B = kSm64A + 8 * kNib64;
-constexpr uint32_t kSm64Lds = kSm64B + 7 * kNib64;                      // 34 KiB of tables in LDS
-constexpr uint32_t kSm64Wave = kSm64Lds;                                // 128 x 64 words: x^(8192 (127 - wave))
-constexpr uint32_t kSm64Tail = kSm64Wave + 4u * kSmallWg * 64u * 8u;    // 32 x 64 words: x^(-8 k), k < 32
+constexpr uint32_t kSm64S2 = kSm64B + 7 * kNib64;                       // the mid layout's row shift
+constexpr uint32_t kSm64Lds = kSm64S2 + kNib64;                         // 36 KiB of tables in LDS
+constexpr uint32_t kSm64Wave = kSm64Lds;  // 4 kMidWg x 64 words: x^(8192 d), d = waves after this one
+constexpr uint32_t kSm64Tail = kSm64Wave + 4u * kMidWg * 64u * 8u;      // 32 x 64 words: x^(-8 k), k < 32
 constexpr uint32_t kSm64Image = kSm64Tail + 32u * 64u * 8u;
 
 struct Small64Args {
@@ -899,12 +904,12 @@ __device__ __forceinline__ uint64_t tail_word64(uint64_t w, int off, int eoff) {
 // Steps 2-3 of one workgroup's share (blocks w[] loaded for virtual lane vt):
 // the column, the shift to the end of the wave, the wave's factor, the XOR
 // over the 4 waves and the tail factor; the value on wave 0, one barrier.
-template <int R>
+template <uint32_t V, int R>
 __device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const uint32_t* lds, const uint4 (&w)[R],
                                                   uint32_t vt, uint64_t bw_wave, uint64_t bw_tail, uint64_t* red) {
     const uint32_t lane = threadIdx.x & 63u, wave = wave_id();
-    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + kSmallLanes - 1) / kSmallLanes);
-    const int first = (int)a.nb - (int)(rows * kSmallLanes) + (int)vt;
+    const uint32_t rows = __builtin_amdgcn_readfirstlane((a.nb + V - 1) / V);
+    const int first = (int)a.nb - (int)(rows * V) + (int)vt;
     // 2. The column: lagged blocks and the row shift (rows that do not exist
     //    cost nothing: crc32c_kernels.h small_wave_value).
     uint64_t c[R];
@@ -912,7 +917,7 @@ __device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const ui
     for (int r = 0; r < R; ++r) {
         c[r] = 0;
         if ((uint32_t)r >= rows) continue;
-        const int b = first + r * (int)kSmallLanes;
+        const int b = first + r * (int)V;
         uint64_t lo = ((uint64_t)w[r].y << 32) | w[r].x, hi = ((uint64_t)w[r].w << 32) | w[r].z;
         if (b <= 1 || b >= (int)a.nb - 2) {  // the head's and the tail's blocks: masks + init
             const int off = b * 16;
@@ -925,7 +930,7 @@ __device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const ui
     uint64_t q = c[0];
 #pragma unroll
     for (int r = 1; r < R; ++r)
-        if ((uint32_t)r < rows) q = nib_mul64_pos(lds, kSm64S, q) ^ c[r];
+        if ((uint32_t)r < rows) q = nib_mul64_pos(lds, V == kSmallLanes ? kSm64S : kSm64S2, q) ^ c[r];
     // 3. Q -> P and the shift to the end of the wave, the wave's and the tail's factors.
     const uint32_t d = 63u - lane, dh = d >> 3;
     const uint64_t x = nib_mul64_pos(lds, kSm64A + (d & 7u) * kNib64, q);
@@ -942,6 +947,7 @@ __device__ __forceinline__ uint64_t small64_value(const Small64Args& a, const ui
     return u;
 }
 
+template <uint32_t V, int R>  // the small or the mid layout (crc32c_small_kernel)
 __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSm64Lds / 4];
     __shared__ uint64_t red[4];
@@ -949,7 +955,7 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
     const uint32_t wg = a.wg0 + blockIdx.x;
     const uint32_t vt = wg * 256u + tid;
     // 1. Table copy first, then the payload rows, then the basis words.
-    constexpr uint32_t kVec = kSm64Lds / 16;  // 2176 16-byte pieces: up to 9 per thread
+    constexpr uint32_t kVec = kSm64Lds / 16;  // 2304 16-byte pieces: 9 per thread
     constexpr uint32_t kPer = (kVec + 255) / 256;
     u32x4 tv[kPer];
 #pragma unroll
@@ -957,9 +963,9 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
         const uint32_t j = i * 256u + tid;
         tv[i] = j < kVec ? *((const g_u32x4*)a.image + j) : u32x4{0, 0, 0, 0};
     }
-    uint4 w[kSmallRows];
-    small_load<false>(a, vt, w);  // as crc32c_small_kernel: only blocks that overlap the data
-    const uint64_t bw_wave = a.image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
+    uint4 w[R];
+    small_load<false, V>(a, vt, w);  // as crc32c_small_kernel: only blocks that overlap the data
+    const uint64_t bw_wave = a.image[kSm64Wave / 8 + (V / 64u - 1u - (wg * 4u + wave)) * 64u + lane];
     const uint64_t bw_tail = a.image[kSm64Tail / 8 + a.k * 64u + lane];
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
@@ -967,7 +973,7 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
         if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
     }
     lds_barrier();
-    const uint64_t u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+    const uint64_t u = small64_value<V, R>(a, lds, w, vt, bw_wave, bw_tail, red);
     if (wave == 0) {
         if (a.slots) {  // routed: the host XORs the workgroups' raw values and inverts
             if (lane == 0) {
@@ -977,7 +983,7 @@ __global__ __launch_bounds__(256) void crc64_small_kernel(Small64Args a) {
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         } else {
-            long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset);  // crc.cpp:119-122
+            long_reduce(u, a.acc, a.out, [](uint64_t x) { return ~x; }, a.tbase, a.treset, a.tag);  // crc.cpp:119-122
         }
     }
 }
@@ -996,7 +1002,7 @@ __global__ __launch_bounds__(256) void crc64_small_service_kernel(ServiceArgs s)
     const uint64_t* image = static_cast<const uint64_t*>(s.image);
     for (uint32_t j = tid; j < kSm64Lds / 16; j += 256u)
         *reinterpret_cast<u32x4*>(lds + 4 * j) = *((const g_u32x4*)image + j);
-    const uint64_t bw_wave = image[kSm64Wave / 8 + (wg * 4u + wave) * 64u + lane];
+    const uint64_t bw_wave = image[kSm64Wave / 8 + (4u * kSmallWg - 1u - (wg * 4u + wave)) * 64u + lane];
     __syncthreads();
     service_loop(s, cmd, nullptr, [&](const SvcReq& r) {
         Small64Args a{};
@@ -1008,14 +1014,14 @@ __global__ __launch_bounds__(256) void crc64_small_service_kernel(ServiceArgs s)
         a.init = r.seed;
         const uint64_t bw_tail = image[kSm64Tail / 8 + a.k * 64u + lane];  // L2-resident: 16 KiB for all k
         uint64_t u;
-        if (a.nb > kSmallRows * kSmallLanes) {  // uniform: a mid-size call (crc32c_kernels.h small_value_rows)
+        if (a.nb > kSmallRows * kSmallLanes) {  // uniform: a call of up to kSvcRows rows
             uint4 w[kSvcRows];
-            svc_load_rows(a, vt, w);
-            u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+            small_load<true, kSmallLanes>(a, vt, w);
+            u = small64_value<kSmallLanes, kSvcRows>(a, lds, w, vt, bw_wave, bw_tail, red);
         } else {
             uint4 w[kSmallRows];
-            small_load<true>(a, vt, w);
-            u = small64_value(a, lds, w, vt, bw_wave, bw_tail, red);
+            small_load<true, kSmallLanes>(a, vt, w);
+            u = small64_value<kSmallLanes, kSmallRows>(a, lds, w, vt, bw_wave, bw_tail, red);
         }
         if (wave == 0 && lane < 2)
             __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg + lane,

@@ -200,13 +200,24 @@ def test_extend_device_reference_perf_shape(torch_dev, oracle, n):
     del d
 
 
-def test_extend_device_plan_edges(torch_dev, oracle):
+@pytest.mark.parametrize("mid", [True, False])
+def test_extend_device_plan_edges(torch_dev, oracle, mid):
     # Chunk-plan edges: one chunk, the one-workgroup limit (256 KiB, 16
     # chunks) and one byte past it, T at multiples of 16 waves +- 1, the
     # 16-KiB-chunk limit of a full grid (64 MiB) +- a few bytes, odd sizes;
     # offsets 0, 1, 15; seeds; CRC-32C and CRC-64. Each call also leaves its
-    # accumulator state zeroed for the next one (repeated calls agree).
+    # accumulator state zeroed for the next one (repeated calls agree). With
+    # the mid kernel on (the default) spans up to 32 MiB take the mid layout;
+    # off, every span over 256 KiB takes the long kernel.
     torch = torch_dev
+    ck.set_mid_kernel(mid)
+    try:
+        _plan_edges(torch, oracle)
+    finally:
+        ck.set_mid_kernel(True)
+
+
+def _plan_edges(torch, oracle):
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     big = 16 * cus * (16 << 10)
     sizes = [0, 1, 15, 64, 4095, 4096, 4097, 65536 + 3, (256 << 10) - 1, 256 << 10, (256 << 10) + 1,
@@ -318,6 +329,56 @@ def test_extend64_device_small_path_edges(torch_dev, oracle):
             assert int(got[k]) == oracle.crc64ecma(host[off:off + n], seed), (off - base, n, hex(seed))
 
 
+MID_LANES = 512 * 256  # crc32c_kernels.h kMidWg * 256
+
+
+@pytest.mark.parametrize("crc64", [False, True])
+def test_extend_device_mid_path_edges(torch_dev, oracle, crc64):
+    """The mid layout (crc32c_small_kernel / crc64_small_kernel over 512
+    workgroups, spans over 256 KiB up to 32 MiB, CRC-64 16 MiB): one byte
+    over the small limit, every row count at its boundaries (+-1 block, at
+    offsets 0, 1, 15), the span limit and one byte past it (the long kernel),
+    random sizes and seeds; calls queued back to back on one stream (one
+    reduce state), all against the oracle."""
+    torch = torch_dev
+    row = MID_LANES * 16
+    rows_max = 8 if crc64 else 16  # crc64_kernels.h kMid64Rows: the long kernel past 16 MiB
+    cap = rows_max * row + 64
+    d = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix(d, cap, cap, 1, 0x5EED0E00 + crc64)
+    host = d.cpu().numpy()
+    base = (-d.data_ptr()) % 16
+    cover = 8 if crc64 else 4
+    cases = [(base + 1, (256 << 10), 1), (base, (256 << 10) + 1, 2), (base + 15, row - 15, 3),
+             (base, rows_max * row, 4), (base + 1, rows_max * row - 1, 5), (base + 3, rows_max * row - 2, 6),
+             (base, rows_max * row + 1, 7), (base + 9, 3 * row + 12345, 8)]
+    for k in range(1, rows_max):
+        for off, dn in ((0, 0), (1, 1), (15, -15), (0, 16), (7, -16 - 7)):
+            cases.append((base + off, k * row + dn, k * 0x9E3779B1 + off))
+    rng = np.random.default_rng(0x5EED0E01 + crc64)
+    for _ in range(24):
+        cases.append((base + int(rng.integers(0, 16)), int(rng.integers(256 << 10, rows_max * row - 16)),
+                      int(rng.integers(0, 1 << 62))))
+    cases = [(o, n, s) for o, n, s in cases if o + max(n, cover) <= cap - 16]
+    if crc64:
+        out = torch.zeros(len(cases), dtype=torch.int64, device="cuda")
+        for k, (off, n, seed) in enumerate(cases):
+            ck.extend64_device(d.data_ptr() + off, n, out[k:k + 1], seed=seed)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64)
+        for k, (off, n, seed) in enumerate(cases):
+            assert int(got[k]) == oracle.crc64ecma(host[off:off + n], seed), (off - base, n, hex(seed))
+    else:
+        out = torch.zeros(len(cases), dtype=torch.int32, device="cuda")
+        for k, (off, n, seed) in enumerate(cases):
+            ck.extend_device(d.data_ptr() + off, n, seed & 0xFFFFFFFF, out[k:k + 1])
+        torch.cuda.synchronize()
+        got = _u32(out)
+        for k, (off, n, seed) in enumerate(cases):
+            assert int(got[k]) == oracle.crc32c(host[off:off + n], seed & 0xFFFFFFFF), (off - base, n, seed)
+    del d
+
+
 def test_extend_device_thousand_back_to_back_launches(torch_dev, oracle):
     """the fence-free cross-workgroup reduce (long_reduce)
     reused by 1,000 back-to-back full-grid launches on ONE stream (one state:
@@ -356,7 +417,8 @@ def test_extend_device_thousand_back_to_back_launches(torch_dev, oracle):
     del bufs
 
 
-def test_extend_device_graph_capture(torch_dev, oracle):
+@pytest.mark.parametrize("mid", [True, False])
+def test_extend_device_graph_capture(torch_dev, oracle, mid):
     """every extend_device call captures into a HIP graph -- a
     one-workgroup call, a multi-workgroup small-kernel call (128 KiB) and a
     full-grid long-kernel call (1 MiB) -- each multi-workgroup launch with a
@@ -365,6 +427,14 @@ def test_extend_device_graph_capture(torch_dev, oracle):
     state again after the capture, and destroying the graph hands the states
     back for the next capture."""
     torch = torch_dev
+    ck.set_mid_kernel(mid)  # the 1 MiB span: the mid layout's 256 workgroups, or the long kernel
+    try:
+        _graph_capture(torch, oracle)
+    finally:
+        ck.set_mid_kernel(True)
+
+
+def _graph_capture(torch, oracle):
     d = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, d.numel(), d.numel(), 1, 0x5EED0C00)
     spans = ((3, 3000), (3, 128 << 10), (3, (1 << 20) - 64))
@@ -455,6 +525,7 @@ def test_extend_device_aligned_grid_edges(torch_dev, oracle, shape):
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     lanes, rounds = shape
     ck.set_long_shape(lanes, rounds)
+    ck.set_mid_kernel(False)  # the long kernel's plan for every span over 256 KiB
     try:
         full = 16 * cus * (64 // (lanes or 64)) * (rounds or 1)  # lane-group slots of a full grid
         n_full = 16384 * full  # the 16 KiB chunk floor of a full grid (64 MiB at 64 x 1)
@@ -478,6 +549,7 @@ def test_extend_device_aligned_grid_edges(torch_dev, oracle, shape):
         del d
     finally:
         ck.set_long_shape(0, 0)
+        ck.set_mid_kernel(True)
 
 
 def test_extend_spans_one_buffer_over_devices(torch_dev, oracle):

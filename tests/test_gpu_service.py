@@ -213,7 +213,7 @@ def test_mid_sizes_served(torch_dev, oracle, kind):
     every row boundary and the span limit at every offset class, random
     sizes and seeds, a buffer rewritten by a kernel and by a host copy in
     between: every call equal to the oracle and served by the service; one
-    block past the limit takes the long kernel (not served) and is exact."""
+    block past the limit takes the launch path (not served) and is exact."""
     torch = torch_dev
     cap = SVC_MAX_BLOCKS * 16 + 64
     rng = np.random.default_rng(0x3D1 + (kind == "crc64"))
@@ -251,7 +251,7 @@ def test_mid_sizes_served(torch_dev, oracle, kind):
         got, want = one(off, n, seed)
         assert got == want, (kind, off, n, seed)
     _check_served(st0, len(cases))
-    # one block past the span: the launch path (the long kernel), still exact
+    # one block past the span: the launch path (the mid layout), still exact
     s1 = _served()
     for off, n in ((0, SVC_MAX_BLOCKS * 16 + 1), (5, SVC_MAX_BLOCKS * 16 - 4)):
         got, want = one(off, n, 77)
