@@ -1,5 +1,6 @@
 """Soak of the resident small-buffer services (bench-only):
-for SECONDS, routed crc32c_extend / crc64ecma_extend calls of random size,
+for SECONDS, routed crc32c_extend / crc64ecma_extend calls of random size
+(up to 4 MiB: the service's small and rows forms, the mid layout),
 offset and seed on device buffers that are rewritten between calls (a fill
 kernel, a device-to-device copy on another stream, a host-to-device copy),
 beside CRC32C and CRC-64 batch launches on another stream (the CRC-64 ones
@@ -45,7 +46,7 @@ def main():
 
     def worker(t):
         rng = random.Random(1000 + t)
-        cap = (256 << 10) + 64
+        cap = (4 << 20) + 64  # the small service (<= 256 KiB), its rows form (<= 2 MiB), the mid layout
         buf = torch.zeros(cap, dtype=torch.uint8, device="cuda")
         src = torch.zeros(cap, dtype=torch.uint8, device="cuda")
         stream = torch.cuda.Stream()
@@ -65,7 +66,8 @@ def main():
             host = buf.cpu().numpy()
             for _ in range(rng.randrange(1, 6)):
                 off = rng.randrange(16)
-                n = rng.choice([rng.randrange(1, 64), rng.randrange(1, 8192), rng.randrange(1, cap - 64)])
+                n = rng.choice([rng.randrange(1, 64), rng.randrange(1, 8192), rng.randrange(1, 256 << 10),
+                                rng.randrange(1, cap - 64)])
                 seed = rng.getrandbits(64)
                 if rng.randrange(2):
                     got = ck.crc32c_extend_at(buf.data_ptr() + off, n, seed & 0xFFFFFFFF)
