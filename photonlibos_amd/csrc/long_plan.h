@@ -6,7 +6,8 @@
 //
 // The cut (round 4). A = the first 4 KiB boundary at or after the data start;
 // the HEAD [data, A) (0..4095 bytes) carries the seed; the BODY [A, end) is
-// cut into T chunks of `chunk` bytes (a 1 KiB multiple, >= 16 KiB), the last
+// cut into T chunks of `chunk` bytes (a 1 KiB multiple, >= 16 KiB; >= 8 KiB
+// under 128 MiB), the last
 // one of L bytes (0 < L <= chunk). The grid has S lane groups and R rounds:
 // R*S virtual slots v = 0 .. R*S-1, slot v belongs to group v % S in round
 // v / S, and body chunk t sits in slot v = t + D with D = R*S - T: the
@@ -29,6 +30,14 @@
 
 #include "crc64_kernels.h"
 #include "gf2.h"
+
+// A/B switches of the cut under 128 MiB (the round-4 cut: 16384 and 0).
+#ifndef PCRC_LONG_MID_FLOOR
+#define PCRC_LONG_MID_FLOOR 8192
+#endif
+#ifndef PCRC_LONG_R1_MIB
+#define PCRC_LONG_R1_MIB 64
+#endif
 
 namespace pcrc {
 
@@ -62,6 +71,15 @@ inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t sh
     //    0.1771, 64x1 0.1882 (0.1668)
     //  up to 256 KiB (CRC-64 only: CRC-32C has its small kernel): 1 round of
     //  chunks of >= 4 KiB, one workgroup
+    //  under 128 MiB (round 5, repo:profiles/r05p_ab_long_chunk_floor.jsonl;
+    //    the mid layout takes CRC-32C spans up to 32 MiB, CRC-64 16 MiB): 16 KiB
+    //    chunks fill only 64-128 of 256 CUs; 8 KiB: 64 MiB 64x2 0.0215 vs
+    //    0.0232, 32 MiB 64x1 0.0160 vs 64x2/16 KiB 0.0225; 128 MiB 16 KiB stays
+    //    best (0.0325 vs 0.0334). The rule, A/B against the 16 KiB cut
+    //    (repo:profiles/r05p_ab_floor8_vs_16.jsonl, ms medians): CRC-32C 33 MiB
+    //    0.0166 vs 0.0231, 48 MiB 0.0188 vs 0.0234, 64 MiB 0.0218 vs 0.0240,
+    //    127 MiB 0.0325 vs 0.0328; CRC-64 17 MiB 0.0159 vs 0.0182, 33 MiB
+    //    0.0180 vs 0.0191, 48-127 MiB equal
     const bool small = n <= (256u << 10);
     const uint64_t mib = n >> 20;
     const int lanes = (shape & 0xff) ? (int)(shape & 0xff)
@@ -69,7 +87,7 @@ inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t sh
     uint64_t rounds = (shape >> 8) ? shape >> 8
                     : small ? 1
                     : crc64 ? (mib < 512 ? 1 : mib < 1536 ? 2 : mib < 3072 ? 4 : 2)
-                            : (mib < 1536 ? 2 : mib < 3072 ? 4 : 2);
+                            : (mib < PCRC_LONG_R1_MIB ? 1 : mib < 1536 ? 2 : mib < 3072 ? 4 : 2);
     const uint64_t gpw = 64 / (uint64_t)lanes;
     const uint64_t maxgrid = (uint64_t)cus < kLongMaxFt ? (uint64_t)cus : kLongMaxFt;
     LongPlan p{};
@@ -81,7 +99,7 @@ inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t sh
     const uint64_t m = n - head;  // 0 only when the whole buffer lies before A (then the head is all of it)
     const uint64_t slots = 16ull * maxgrid * gpw * rounds;
     uint64_t chunk = ((m + slots - 1) / slots + 1023) / 1024 * 1024;  // whole rows, 1 KiB aligned
-    const uint64_t lo = small ? 4096 : 16384;
+    const uint64_t lo = small ? 4096 : mib < 128 ? PCRC_LONG_MID_FLOOR : 16384;
     if (chunk < lo) chunk = lo;
     if (force_chunk) chunk = force_chunk;
     p.head = head;

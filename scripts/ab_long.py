@@ -14,6 +14,8 @@ Bench-only.
             strided batch kernel over the same bytes as 64 KiB pieces from an
             aligned base) and "read" (the read-only grid-stride stream)
   SIZES_MIB buffer sizes (at base+1, test_checksum.cpp:125-168)
+  MID       1 (default) / 0: photon_crc_set_mid_kernel in every build (0: the
+            long kernel for spans of up to 32 MiB too)
   LAUNCHES  back-to-back launches per variant per round, ROUNDS rounds (after
             WARM untimed interleaved rounds: under rocprofv3 every kernel then
             starts past the fill's DVFS dip, so the kernels' stats compare)
@@ -40,6 +42,8 @@ for item in os.environ.get("LIBS", "new=" + os.path.join(REPO, "photonlibos_amd/
     lib.photon_crc32c_extend_device.restype = ci
     lib.photon_crc_set_long_shape.argtypes = [ci, ci]
     lib.photon_crc_set_long_shape.restype = ci
+    if hasattr(lib, "photon_crc_set_mid_kernel"):  # MID=0: spans <= 32 MiB on the long kernel too
+        lib.photon_crc_set_mid_kernel(int(os.environ.get("MID", "1")))
     libs[name] = lib
 VARIANTS = os.environ.get("VARIANTS", "new:0/0,batch64k,read").split(",")
 OFF = int(os.environ.get("OFF", "1"))  # buffer start offset from a 2 MiB-aligned allocation
