@@ -559,7 +559,10 @@ def run_extend(args, stream):
     d = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, n + 64, n + 64, 1, 0x5EED0900, stream=stream)
     out = torch.zeros(64, dtype=torch.int32, device="cuda")
-    for label, nbytes, steps in (("1GiB", n, max(10, min(args.steps, 50))), ("128KiB", 128 << 10, 200)):
+    # 1 MiB and 8 MiB: the mid layout (the small kernel's code over 512
+    # workgroups); 64 MiB: the long kernel's smallest full-chip cut
+    for label, nbytes, steps in (("1GiB", n, max(10, min(args.steps, 50))), ("128KiB", 128 << 10, 200),
+                                 ("1MiB", 1 << 20, 200), ("8MiB", 8 << 20, 200), ("64MiB", 64 << 20, 100)):
         ms = []
         for k in range(steps + 5):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -2281,6 +2281,33 @@ void service_end_all() {
     }
 }
 
+// At process exit (atexit): stop every running launch and wait, bounded, for
+// each workgroup's exit word -- no HIP call, since a profiler's or the
+// runtime's own exit hooks may already have run (rocprofv3 aborted in one:
+// "get_stream_stack() must be non nullptr" inside hipStreamSynchronize).
+void service_end_at_exit() {
+    std::lock_guard<std::mutex> lk(g_svc_list_mu);
+    for (SmallService* s : g_svc_list) {
+        std::lock_guard<std::mutex> l2(s->mu);
+        if (!s->live) continue;
+        volatile uint64_t* h = s->h;
+        if (!h[kSvcQuit]) {
+            bell_put(s, kSvcStop, 1ull);
+            bell_flush();
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t b = 0; b < kSmallWg;) {
+            if (h[kSvcSlots + kSvcSlotStride * b + kSvcExitWord]) {
+                ++b;
+                continue;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+            cpu_relax();
+        }
+        set_live(s, false);
+    }
+}
+
 int service_get(int dev, int kind, SmallService** out) {
     return g_svc[kind].get(dev, out, [kind](int, SmallService*& slot) {
         auto* s = new SmallService;
@@ -2328,7 +2355,7 @@ int service_get(int dev, int kind, SmallService** out) {
             s->bell_d = s->d;
         }
         std::lock_guard<std::mutex> lk(g_svc_list_mu);
-        if (g_svc_list.empty()) atexit(service_end_all);  // after HIP's init: runs before its teardown
+        if (g_svc_list.empty()) atexit(service_end_at_exit);  // after HIP's init: runs before its teardown
         g_svc_list.push_back(s);
         slot = s;
         return 0;
@@ -2397,6 +2424,8 @@ int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0
         bell_put(s, kSvcQuit, 0ull);
         bell_flush();
         __atomic_store_n(&s->h[kSvcQuit], 0ull, __ATOMIC_RELAXED);
+        for (uint32_t b = 0; b < kSmallWg; ++b)  // the last launch's waves have all left (stream synchronised)
+            __atomic_store_n(&s->h[kSvcSlots + kSvcSlotStride * b + kSvcExitWord], 0ull, __ATOMIC_RELAXED);
         ServiceArgs a{img, s->bell_d, s->d, s->seq, 100u * (uint32_t)idle_us, kSvcLifeTicks};
         const hipError_t e = relaxed_capture([&] {
             if (kind == 0)

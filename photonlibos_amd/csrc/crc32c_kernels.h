@@ -1735,7 +1735,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
 //        workgroups and in the pinned area's word 7 for the host, which then
 //        starts a new launch for later calls.
 // Pinned area: word 7 quit (above); 16 + 8 b: slot of workgroup b, {seq,
-// value} (CRC-64: {seq, low}, {seq, high}).
+// value} (CRC-64: {seq, low}, {seq, high}); 16 + 8 b + 3: workgroup b left.
 // Every wave exits: workgroup 0 on stop / idle / life, the others on stop,
 // quit or 2 x life by their own clock (a workgroup 0 that never became
 // resident cannot keep them alive). The decision is per workgroup (wave 0's,
@@ -1744,6 +1744,7 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
 // with agent-scope loads (small_load<true>): a buffer rewritten by another
 // launch since this one last read it must not come from this CU's L1.
 constexpr uint32_t kSvcStop = 6, kSvcQuit = 7, kSvcSlots = 16, kSvcSlotStride = 8;  // one 64-byte line per slot
+constexpr uint32_t kSvcExitWord = 3;  // word 3 of a workgroup's slot line: set as the workgroup leaves
 constexpr uint32_t kSvcWords = kSvcSlots + kSvcSlotStride * kSmallWg;
 constexpr uint32_t kSvcLds = kSmLds + 32u * 32u * 4u;  // the tables, then the tail basis words
 
@@ -1829,6 +1830,11 @@ __device__ __forceinline__ void service_loop(const ServiceArgs& s, uint32_t (&cm
         if (wg < r.wg0) continue;  // no data in this workgroup's part of the layout
         work(r);
     }
+    // the host's process-exit path waits for these instead of the stream (no
+    // HIP call at exit: a profiler's exit hooks may have run before it)
+    if (wave == 0 && lane == 0)
+        __hip_atomic_store(s.area + kSvcSlots + kSvcSlotStride * wg + kSvcExitWord, 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(256) void crc32c_small_service_kernel(ServiceArgs s) {
