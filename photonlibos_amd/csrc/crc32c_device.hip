@@ -146,6 +146,8 @@ std::mutex g_mu;
 std::vector<DeviceInfo> g_dev;
 thread_local int g_fail_next = 0;  // photon_crc_test_fail_next (tuning.h)
 
+void table_images_init();  // (below) the device's table-prologue images
+
 // Resolve the current device; only gfx950 is supported (no other code path).
 // Every device entry point passes through here before it enqueues anything.
 int current_device(int* cus) {
@@ -167,6 +169,7 @@ int current_device(int* cus) {
         di.cus = prop.multiProcessorCount;
         di.probed = true;
         if (!di.ok) g_err = std::string("device is ") + prop.gcnArchName + ", need gfx950";
+        if (di.ok) table_images_init();
     }
     if (!di.ok) return fail(-ENODEV, "photon_crc: no gfx950 device (got other arch)");
     *cus = di.cus;
@@ -608,6 +611,46 @@ hipError_t relaxed_capture(F f) {
     const hipError_t e = f();
     if (ex == hipSuccess) (void)hipThreadExchangeStreamCaptureMode(&m);
     return e;
+}
+
+// The table-prologue images of the current device (crc32c_kernels.h
+// load_tables): table_image_kernel<G> writes what build_tables<G> leaves in
+// LDS, for every G, into one device buffer, and g_table_image points the
+// kernels at it. Once per device, on its first call (current_device), on a
+// private stream in relaxed capture mode. A failure leaves the slots null:
+// the kernels then build their tables as before (same results).
+void table_images_init() {
+    (void)relaxed_capture([&] {
+        constexpr uint64_t kB[5] = {lds_bytes_for<4>(), lds_bytes_for<8>(), lds_bytes_for<16>(), lds_bytes_for<32>(),
+                                    lds_bytes_for<64>()};
+        uint64_t off[5], total = 0;
+        for (int i = 0; i < 5; ++i) {
+            off[i] = total;
+            total += (kB[i] + 255) & ~255ull;
+        }
+        hipStream_t s = nullptr;
+        char* base = nullptr;
+        hipError_t r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (r == hipSuccess) r = hipMalloc(reinterpret_cast<void**>(&base), total);
+        const uint32_t* img[5] = {};
+        for (int i = 0; i < 5; ++i) img[i] = reinterpret_cast<const uint32_t*>(base + off[i]);
+        auto w = [&](int i) { return const_cast<uint32_t*>(img[i]); };
+        if (r == hipSuccess) {
+            hipLaunchKernelGGL(table_image_kernel<4>, dim3(1), dim3(kBlock), 0, s, lane_consts(4), w(0));
+            hipLaunchKernelGGL(table_image_kernel<8>, dim3(1), dim3(kBlock), 0, s, lane_consts(8), w(1));
+            hipLaunchKernelGGL(table_image_kernel<16>, dim3(1), dim3(kBlock), 0, s, lane_consts(16), w(2));
+            hipLaunchKernelGGL(table_image_kernel<32>, dim3(1), dim3(kBlock), 0, s, lane_consts(32), w(3));
+            hipLaunchKernelGGL(table_image_kernel<64>, dim3(1), dim3(kBlock), 0, s, lane_consts(64), w(4));
+            r = hipGetLastError();
+        }
+        if (r == hipSuccess) r = hipStreamSynchronize(s);  // the images are written before any kernel sees them
+        if (r == hipSuccess)
+            r = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_table_image), img, sizeof img, 0, hipMemcpyHostToDevice, s);
+        if (r == hipSuccess) r = hipStreamSynchronize(s);
+        if (r != hipSuccess && base) (void)hipFree(base);
+        if (s) (void)hipStreamDestroy(s);
+        return r;
+    });
 }
 
 // A multi-workgroup launch captured into a HIP graph cannot use the stream's

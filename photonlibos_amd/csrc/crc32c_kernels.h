@@ -306,8 +306,15 @@ __device__ __forceinline__ void lds_barrier() {
 // each table per thread).
 // FG = 0: R_k lane-combine tables; FG = 4 or 8: F_d finish tables for G = FG;
 // FG >= 16: the A_dl / B_dh finish tables for G = FG.
+#ifndef PCRC_ABL_NO_PROLOGUE
+#define PCRC_ABL_NO_PROLOGUE 0  // A/B builds only: skip the table build (wrong CRCs; the prologue's cost)
+#endif
 template <int FG = 0>
 __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc) {
+    if (PCRC_ABL_NO_PROLOGUE) {
+        lds_barrier();
+        return;
+    }
     const uint32_t tid = threadIdx.x;
     const uint32_t t = tid >> 8, b = tid & 255u;
     if constexpr (FG >= 16) {
@@ -358,6 +365,61 @@ __device__ __forceinline__ void build_tables(uint32_t* lds, const LaneConsts& kc
         lds[base + kSOff / 4 + r] = sv;
     }
     lds_barrier();
+}
+
+// The table prologue from a per-device IMAGE (round 5): build_tables costs
+// ≈4.7 µs of VALU at the start of every launch (repo:scripts/probe_long_times.py,
+// prologue_us_med), ≈0.6 points of C2 and 2.6 % of the 1 GiB long kernel
+// (an A/B build that skips it, repo:profiles/r05r_ab_noprol_*). Each device
+// keeps the LDS contents build_tables<G> leaves, written once by
+// table_image_kernel<G> (the same code, so the image is exact by
+// construction); a launch copies them into LDS with 16-byte loads instead
+// (L2-resident: one image per G, read by every workgroup). Slot by G: 4, 8,
+// 16, 32, 64 -> 0..4; a null slot (no image yet, or an A/B build with
+// PCRC_TABLE_BUILD) builds as before.
+#ifndef PCRC_TABLE_BUILD
+#define PCRC_TABLE_BUILD 0
+#endif
+static __device__ const uint32_t* g_table_image[5];
+template <int G>
+constexpr int table_slot() {
+    return G == 4 ? 0 : G == 8 ? 1 : G == 16 ? 2 : G == 32 ? 3 : 4;
+}
+
+template <int G>
+__device__ __forceinline__ void copy_tables(uint32_t* lds, const uint32_t* img) {
+    constexpr uint32_t kVec = lds_bytes_for<G>() / 16, kPer = (kVec + kBlock - 1) / kBlock;
+    const uint32_t tid = threadIdx.x;
+    u32x4 v[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t j = i * kBlock + tid;
+        v[i] = j < kVec ? *((const g_u32x4*)img + j) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t j = i * kBlock + tid;
+        if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = v[i];
+    }
+    lds_barrier();
+}
+
+template <int G>
+__device__ __forceinline__ void load_tables(uint32_t* lds, const LaneConsts& kc) {
+    const uint32_t* img = PCRC_TABLE_BUILD ? nullptr : g_table_image[table_slot<G>()];
+    if (img)
+        copy_tables<G>(lds, img);
+    else
+        build_tables<G>(lds, kc);
+}
+
+// Writes the image of G (once per device; crc32c_device.hip table_images).
+template <int G>
+__global__ __launch_bounds__(kBlock) void table_image_kernel(LaneConsts kc, uint32_t* img) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
+    build_tables<G>(lds, kc);
+    for (uint32_t j = threadIdx.x; j < lds_bytes_for<G>() / 16; j += kBlock)
+        *reinterpret_cast<u32x4*>(img + 4 * j) = *reinterpret_cast<const u32x4*>(lds + 4 * j);
 }
 
 __device__ __forceinline__ LaneAddr lane_addr(uint32_t lane) {
@@ -682,7 +744,7 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
 template <int G, int U = 4, int MSG = 0>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
-    build_tables<G>(lds, kc);
+    load_tables<G>(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
     const uint32_t lane = threadIdx.x & 63u;
@@ -1382,7 +1444,7 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
         t0 = __builtin_amdgcn_s_memrealtime();
         c0 = __builtin_amdgcn_s_memtime();
     }
-    build_tables<G>(lds, kc);
+    load_tables<G>(lds, kc);
     if constexpr (STAMP) t_tab = __builtin_amdgcn_s_memrealtime();
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
