@@ -614,17 +614,19 @@ hipError_t relaxed_capture(F f) {
 }
 
 // The table-prologue images of the current device (crc32c_kernels.h
-// load_tables): table_image_kernel<G> writes what build_tables<G> leaves in
-// LDS, for every G, into one device buffer, and g_table_image points the
-// kernels at it. Once per device, on its first call (current_device), on a
+// load_tables, crc64_kernels.h load_tables64): table_image_kernel<G> /
+// table_image64_kernel<G> write what build_tables<G> / build_tables64<G> leave
+// in LDS, for every G, into one device buffer, and g_table_image /
+// g_table_image64 point the kernels at it. Once per device, on its first call (current_device), on a
 // private stream in relaxed capture mode. A failure leaves the slots null:
 // the kernels then build their tables as before (same results).
 void table_images_init() {
     (void)relaxed_capture([&] {
-        constexpr uint64_t kB[5] = {lds_bytes_for<4>(), lds_bytes_for<8>(), lds_bytes_for<16>(), lds_bytes_for<32>(),
-                                    lds_bytes_for<64>()};
-        uint64_t off[5], total = 0;
-        for (int i = 0; i < 5; ++i) {
+        constexpr uint64_t kB[10] = {lds_bytes_for<4>(),  lds_bytes_for<8>(),  lds_bytes_for<16>(), lds_bytes_for<32>(),
+                                     lds_bytes_for<64>(), lds64_used<4>(),     lds64_used<8>(),     lds64_used<16>(),
+                                     lds64_used<32>(),    lds64_used<64>()};
+        uint64_t off[10], total = 0;
+        for (int i = 0; i < 10; ++i) {
             off[i] = total;
             total += (kB[i] + 255) & ~255ull;
         }
@@ -633,19 +635,31 @@ void table_images_init() {
         hipError_t r = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
         if (r == hipSuccess) r = hipMalloc(reinterpret_cast<void**>(&base), total);
         const uint32_t* img[5] = {};
-        for (int i = 0; i < 5; ++i) img[i] = reinterpret_cast<const uint32_t*>(base + off[i]);
+        const uint32_t* img64[5] = {};
+        for (int i = 0; i < 5; ++i) {
+            img[i] = reinterpret_cast<const uint32_t*>(base + off[i]);
+            img64[i] = reinterpret_cast<const uint32_t*>(base + off[5 + i]);
+        }
         auto w = [&](int i) { return const_cast<uint32_t*>(img[i]); };
+        auto w64 = [&](int i) { return const_cast<uint32_t*>(img64[i]); };
         if (r == hipSuccess) {
             hipLaunchKernelGGL(table_image_kernel<4>, dim3(1), dim3(kBlock), 0, s, lane_consts(4), w(0));
             hipLaunchKernelGGL(table_image_kernel<8>, dim3(1), dim3(kBlock), 0, s, lane_consts(8), w(1));
             hipLaunchKernelGGL(table_image_kernel<16>, dim3(1), dim3(kBlock), 0, s, lane_consts(16), w(2));
             hipLaunchKernelGGL(table_image_kernel<32>, dim3(1), dim3(kBlock), 0, s, lane_consts(32), w(3));
             hipLaunchKernelGGL(table_image_kernel<64>, dim3(1), dim3(kBlock), 0, s, lane_consts(64), w(4));
+            hipLaunchKernelGGL(table_image64_kernel<4>, dim3(1), dim3(kBlock), 0, s, lane_consts64(4), w64(0));
+            hipLaunchKernelGGL(table_image64_kernel<8>, dim3(1), dim3(kBlock), 0, s, lane_consts64(8), w64(1));
+            hipLaunchKernelGGL(table_image64_kernel<16>, dim3(1), dim3(kBlock), 0, s, lane_consts64(16), w64(2));
+            hipLaunchKernelGGL(table_image64_kernel<32>, dim3(1), dim3(kBlock), 0, s, lane_consts64(32), w64(3));
+            hipLaunchKernelGGL(table_image64_kernel<64>, dim3(1), dim3(kBlock), 0, s, lane_consts64(64), w64(4));
             r = hipGetLastError();
         }
         if (r == hipSuccess) r = hipStreamSynchronize(s);  // the images are written before any kernel sees them
         if (r == hipSuccess)
             r = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_table_image), img, sizeof img, 0, hipMemcpyHostToDevice, s);
+        if (r == hipSuccess)
+            r = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_table_image64), img64, sizeof img64, 0, hipMemcpyHostToDevice, s);
         if (r == hipSuccess) r = hipStreamSynchronize(s);
         if (r != hipSuccess && base) (void)hipFree(base);
         if (s) (void)hipStreamDestroy(s);

@@ -386,9 +386,9 @@ constexpr int table_slot() {
     return G == 4 ? 0 : G == 8 ? 1 : G == 16 ? 2 : G == 32 ? 3 : 4;
 }
 
-template <int G>
+template <uint32_t BYTES>
 __device__ __forceinline__ void copy_tables(uint32_t* lds, const uint32_t* img) {
-    constexpr uint32_t kVec = lds_bytes_for<G>() / 16, kPer = (kVec + kBlock - 1) / kBlock;
+    constexpr uint32_t kVec = BYTES / 16, kPer = (kVec + kBlock - 1) / kBlock;
     const uint32_t tid = threadIdx.x;
     u32x4 v[kPer];
 #pragma unroll
@@ -408,7 +408,7 @@ template <int G>
 __device__ __forceinline__ void load_tables(uint32_t* lds, const LaneConsts& kc) {
     const uint32_t* img = PCRC_TABLE_BUILD ? nullptr : g_table_image[table_slot<G>()];
     if (img)
-        copy_tables<G>(lds, img);
+        copy_tables<lds_bytes_for<G>()>(lds, img);
     else
         build_tables<G>(lds, kc);
 }

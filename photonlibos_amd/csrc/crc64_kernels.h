@@ -286,6 +286,29 @@ __device__ __forceinline__ void build_tables64(uint32_t* lds, const LaneConsts64
     __syncthreads();
 }
 
+// The CRC-64 prologue from a per-device image (crc32c_kernels.h load_tables):
+// the bytes build_tables64<G> writes (D, S, the finish tables of G), copied.
+static __device__ const uint32_t* g_table_image64[5];
+template <int G>
+constexpr uint32_t lds64_used() {
+    return k64FBase + (8u + (G > 8 ? G / 8 - 1 : 0)) * 2048u;
+}
+template <int G>
+__device__ __forceinline__ void load_tables64(uint32_t* lds, const LaneConsts64& kc) {
+    const uint32_t* img = PCRC_TABLE_BUILD ? nullptr : g_table_image64[table_slot<G>()];
+    if (img)
+        copy_tables<lds64_used<G>()>(lds, img);
+    else
+        build_tables64<G>(lds, kc);
+}
+template <int G>
+__global__ __launch_bounds__(kBlock) void table_image64_kernel(LaneConsts64 kc, uint32_t* img) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
+    build_tables64<G>(lds, kc);
+    for (uint32_t j = threadIdx.x; j < lds64_used<G>() / 16; j += kBlock)
+        *reinterpret_cast<u32x4*>(img + 4 * j) = *reinterpret_cast<const u32x4*>(lds + 4 * j);
+}
+
 // p * x^(128*d) for d < 2^LOG2 (basis multiplies on the bits of d).
 template <int LOG2>
 __device__ __forceinline__ uint64_t shift64(uint64_t pc, uint32_t d, const uint32_t* lds) {
@@ -456,7 +479,7 @@ __device__ __forceinline__ void crc64_batch_run(const Batch64Args& args, const L
                                                 uint64_t* t) {
     uint64_t ts[5] = {0, 0, 0, 0, 0};
     if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memrealtime();
-    build_tables64<G>(lds, kc);
+    load_tables64<G>(lds, kc);
     if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gl = lane & (G - 1);
@@ -546,7 +569,7 @@ __device__ __forceinline__ void load_step64(uint4 (&w)[U], const uint8_t* p) {
 template <int G, int U, bool XB>
 __global__ __launch_bounds__(kBlock) void crc64_full_kernel(Batch64Args args, LaneConsts64 kc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[k64FLdsBytes / 4];
-    build_tables64<G>(lds, kc);
+    load_tables64<G>(lds, kc);
     constexpr int GPW = 64 / G;
     constexpr uint32_t kStep = 16u * G * U;  // bytes of one step of a lane group
     const uint32_t lane = threadIdx.x & 63u;
@@ -754,7 +777,7 @@ __device__ __forceinline__ void crc64_long_run(const Long64Args& a, const LaneCo
                                                uint64_t* red, uint64_t* t) {
     uint64_t ts[5] = {0, 0, 0, 0, 0};
     if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memrealtime();
-    build_tables64<G>(lds, kc);
+    load_tables64<G>(lds, kc);
     if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memrealtime();
     constexpr int GPW = 64 / G;
     const uint32_t lane = threadIdx.x & 63u;
