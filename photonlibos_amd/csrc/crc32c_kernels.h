@@ -741,10 +741,21 @@ __device__ __forceinline__ uint32_t buffer_crc(const uint32_t* lds, const uint8_
 // with per-segment CRCs + fold (separate instantiations: the two message
 // forms in one kernel shared one register allocation, and each is faster
 // compiled alone).
+// PCRC_BATCH_OVERLAP (buffer batches): the table image's loads, then the
+// wave's first buffer's rows, then the LDS writes -- vmcnt counts in issue
+// order, so the writes wait for the image only and the first rows stay in
+// flight across the barrier ("Table prologue from a per-device
+// image").
+#ifndef PCRC_BATCH_OVERLAP
+#define PCRC_BATCH_OVERLAP 1
+#endif
 template <int G, int U = 4, int MSG = 0>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
-    load_tables<G>(lds, kc);
+    // (A/B, repo:profiles/r05t_ab_overlap_c2_c3_c4.jsonl: C2 +0.1 point 3 of 3 rounds,
+    // C3 at G = 16 -0.1, C4 +-0; U = 8 spills)
+    constexpr bool kOverlap = MSG == 0 && G >= 32 && U <= 4 && PCRC_BATCH_OVERLAP && !PCRC_TABLE_BUILD;
+    if constexpr (!kOverlap) load_tables<G>(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
     const uint32_t lane = threadIdx.x & 63u;
@@ -879,22 +890,73 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
     // (Measured and dropped: software-pipelining the wave's buffers -- the
     // next buffer's descriptor and first rows issued before the current
     // buffer's finish -- 127 instead of 106 VGPRs, C2 -1 point, C3 -0.6.)
+    auto item = [&](uint64_t wv, const uint8_t** p, uint64_t* n, uint32_t* seed) {
+        const uint64_t bi = wv * GPW + grp;
+        *p = nullptr;
+        *n = 0;
+        *seed = args.seed0;
+        if (bi < args.count) {
+            if (args.iov) {
+                *p = static_cast<const uint8_t*>(args.iov[bi].base);
+                *n = args.iov[bi].len;
+            } else {
+                *p = args.base + bi * args.stride;
+                *n = args.nbytes;
+            }
+            if (args.seeds) *seed = args.seeds[bi];
+        }
+    };
+    if constexpr (kOverlap) {
+        constexpr uint32_t kVec = lds_bytes_for<G>() / 16, kPer = (kVec + kBlock - 1) / kBlock;
+        const uint32_t* img = g_table_image[table_slot<G>()];
+        const uint32_t tid = threadIdx.x;
+        u32x4 tv[kPer];
+        if (img) {
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t j = i * kBlock + tid;
+                tv[i] = j < kVec ? *((const g_u32x4*)img + j) : u32x4{0, 0, 0, 0};
+            }
+        }
+        uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave;
+        const uint8_t* p;
+        uint64_t n;
+        uint32_t seed;
+        item(wv, &p, &n, &seed);
+        BufGeo g = buf_geo<G>(p, n, gl);
+        BufPre<U, PCRC_BATCH_LEAD> pre;
+        if (wv * GPW < args.count) buf_preload<G, U, PCRC_BATCH_LEAD>(g, gl, pre);  // wave-uniform
+        if (img) {
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t j = i * kBlock + tid;
+                if (j < kVec) *reinterpret_cast<u32x4*>(lds + 4 * j) = tv[i];
+            }
+            lds_barrier();
+        } else {
+            build_tables<G>(lds, kc);
+        }
+        for (bool first = true; wv * GPW < args.count; wv += nwaves, first = false) {
+            if (!first) {
+                item(wv, &p, &n, &seed);
+                g = buf_geo<G>(p, n, gl);
+                buf_preload<G, U, PCRC_BATCH_LEAD>(g, gl, pre);
+            }
+            const uint32_t s = args.shift_init ? 0u : seed;
+            const uint32_t pc = buf_body<G, U, PCRC_BATCH_LEAD>(lds, g, pre, s, gl, la, !args.shift_init);
+            const uint32_t crc = buf_finish<G>(lds, g, pc, p, n, s, gl, la);
+            const uint64_t bi = wv * GPW + grp;
+            if (bi < args.count && gl == 0) args.out[bi] = crc ^ args.init_shift;  // init_shift is 0 unless shift_init
+        }
+        return;
+    }
     for (uint64_t wv = (uint64_t)blockIdx.x * kWaves + wave; wv * GPW < args.count; wv += nwaves) {
         const uint64_t bi = wv * GPW + grp;
         const bool active = bi < args.count;
-        const uint8_t* p = nullptr;
-        uint64_t n = 0;
-        uint32_t seed = args.seed0;
-        if (active) {
-            if (args.iov) {
-                p = static_cast<const uint8_t*>(args.iov[bi].base);
-                n = args.iov[bi].len;
-            } else {
-                p = args.base + bi * args.stride;
-                n = args.nbytes;
-            }
-            if (args.seeds) seed = args.seeds[bi];
-        }
+        const uint8_t* p;
+        uint64_t n;
+        uint32_t seed;
+        item(wv, &p, &n, &seed);
         const uint32_t crc = buffer_crc<G, U, PCRC_BATCH_LEAD>(lds, p, n, args.shift_init ? 0u : seed, gl, la,
                                                                !args.shift_init);
         if (active && gl == 0) args.out[bi] = crc ^ args.init_shift;  // init_shift is 0 unless shift_init
