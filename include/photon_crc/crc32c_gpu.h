@@ -25,6 +25,11 @@
  * descriptor arrays must be device-accessible (hipMalloc'd or registered /
  * pinned host memory).
  *
+ * Per device, the library keeps ≈1.3 MiB of constant table images for the
+ * life of the process (the LDS tables every batch / long kernel copies
+ * instead of building them, written on the device's first call) and, for
+ * the small and mid kernels, ≈1.3 MiB more on the first call that needs them.
+ *
  * Return value: 0 on success, a negative errno-style code otherwise
  * (-ENODEV no usable gfx950 device, -EINVAL bad arguments, -EIO HIP runtime
  * error; photon_crc_last_error() has the text). There is NO silent CPU
