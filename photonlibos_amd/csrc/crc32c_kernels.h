@@ -1506,6 +1506,11 @@ __device__ __forceinline__ void long_run(const LongArgs& a, const LaneConsts& kc
         t0 = __builtin_amdgcn_s_memrealtime();
         c0 = __builtin_amdgcn_s_memtime();
     }
+    // (Measured and dropped: the batch kernel's overlap here -- the first
+    // round's rows issued between the image loads and the LDS writes -- took
+    // the long kernel from 99 to 128 VGPRs and was slower at every size: 1 GiB
+    // 0.1695 vs 0.1654 ms, 256 MiB 0.0549 vs 0.0530,
+    // repo:profiles/r05v_ab_long_overlap.jsonl.)
     load_tables<G>(lds, kc);
     if constexpr (STAMP) t_tab = __builtin_amdgcn_s_memrealtime();
     constexpr int GPW = 64 / G;
