@@ -45,15 +45,15 @@ int photon_crc_set_msg_mode(int mode);
 /* Rows per step of the one-kernel message form (tuning): 2 (default) or 4. */
 int photon_crc_set_msg_rows(int rows_per_step);
 
-/* Buffers over 256 KiB up to 32 MiB (block span <= 2,097,152 16-byte blocks;
- * CRC-64 16 MiB) of photon_crc32c_extend_device / photon_crc64ecma_extend_device
- * and of the routed calls: 1 (default) = the mid layout (the small kernel's code over 512
- * workgroups, no table prologue: 1 MiB in about a third of the long kernel's
- * time), 0 = the long kernel (tests of its plan). DESIGN.md §4.0. */
+/* Buffers over 256 KiB up to 16 MiB (block span <= 1,048,576 16-byte blocks)
+ * of photon_crc32c_extend_device / photon_crc64ecma_extend_device
+ * and of the routed calls: 1 (default) = the mid layout (the small kernel's
+ * code over 512 workgroups: 1 MiB in 5.1 µs per call queued against 8.3 for
+ * the long kernel), 0 = the long kernel (tests of its plan). DESIGN.md §4.0. */
 int photon_crc_set_mid_kernel(int on);
 
 /* One long buffer (photon_crc32c_extend_device / photon_crc64ecma_extend_device,
- * buffers over 32 MiB, or over 256 KiB with the mid kernel off): lanes per chunk (32 or 64) and chunks per lane
+ * buffers over 16 MiB, or over 256 KiB with the mid kernel off): lanes per chunk (32 or 64) and chunks per lane
  * group of the full grid (rounds, 1..64); 0 = automatic, by buffer size and
  * CRC width (photonlibos_amd/csrc/long_plan.h long_plan_for, which lists the
  * measurements behind each step): CRC-32C 64 lanes x 2 rounds, 32 x 2 from

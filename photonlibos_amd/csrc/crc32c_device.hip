@@ -1000,7 +1000,7 @@ bool small_args(const void* p, uint64_t n, uint32_t seed, SmallArgs* a, uint32_t
 }
 
 // The mid layout (crc32c_kernels.h kMidWg): spans over kSmallBlocks up to
-// kMidBlocks (32 MiB; CRC-64 kMid64Blocks, 16 MiB) while
+// kMidBlocks (16 MiB, both CRCs) while
 // photon_crc_set_mid_kernel is on, else false (the long kernel's case).
 std::atomic<int> g_mid_kernel{1};
 
@@ -1591,7 +1591,7 @@ int photon_crc64ecma_extend_device(const void* d_data, uint64_t nbytes, uint64_t
 }  // extern "C"
 
 namespace pcrc {
-// A span over the small kernel's: the mid layout up to 32 MiB, else the long
+// A span over the small kernel's: the mid layout up to 16 MiB, else the long
 // kernel (tag: as extend64_device_long).
 int extend64_device_big(int dev, const void* d_data, uint64_t nbytes, uint64_t seed, uint64_t* d_out, hipStream_t st,
                         int cus, uint32_t tag) {
@@ -1728,7 +1728,7 @@ int photon_crc32c_extend_device(const void* d_data, uint64_t nbytes, uint32_t se
 }  // extern "C"
 
 namespace pcrc {
-// A span over the small kernel's: the mid layout up to 32 MiB, else the long
+// A span over the small kernel's: the mid layout up to 16 MiB, else the long
 // kernel (tag: as extend_device_long).
 int extend_device_big(int dev, const void* d_data, uint64_t nbytes, uint32_t seed, uint32_t* d_out, hipStream_t st,
                       int cus, uint32_t tag) {

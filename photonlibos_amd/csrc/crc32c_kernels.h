@@ -1612,12 +1612,14 @@ constexpr uint32_t kSmallBlocks = 16384;                      // 256 KiB of bloc
 constexpr uint32_t kSmallWg = 33, kSmallLanes = kSmallWg * 256;  // V = 8448 virtual lanes
 constexpr uint32_t kSmallRows = (kSmallBlocks + 1 + kSmallLanes - 1) / kSmallLanes;  // 2
 // The MID layout (photon_crc32c_extend_device and routed calls over 256 KiB
-// up to 32 MiB, where the long kernel's fixed cost -- ≈12 µs of table
-// prologue, ramp-up and drain -- is most of the call): the same code with
-// kMidWg = 512 workgroups (two per CU), V = 131,072 virtual lanes and up to
-// kMidRows rows per thread.
-constexpr uint32_t kMidWg = 512, kMidLanes = kMidWg * 256, kMidRows = 16;
-constexpr uint32_t kMidBlocks = kMidRows * kMidLanes;         // 2,097,152 blocks: 32 MiB
+// up to 16 MiB): the same code with kMidWg = 512 workgroups (two per CU), V =
+// 131,072 virtual lanes and up to kMidRows rows per thread. Past 16 MiB the
+// long kernel (with its table image and 8 KiB chunks) is as fast or faster
+// (repo:profiles/r05v_probe_mid.jsonl, µs per call queued: 16 MiB 9.18 vs
+// 9.32, 32 MiB 13.33 vs 10.03; CRC-64 16 MiB 10.79 vs 10.74); before the
+// image it had ≈17 µs of fixed cost (r05n: 1 MiB 19.1 µs against 5.2).
+constexpr uint32_t kMidWg = 512, kMidLanes = kMidWg * 256, kMidRows = 8;
+constexpr uint32_t kMidBlocks = kMidRows * kMidLanes;         // 1,048,576 blocks: 16 MiB
 constexpr uint32_t kNib = 512;                                // bytes of one nibble-sliced multiplier
 // D_j: x^(32 j), j = 1..3 (a block's lagged CRC in ONE table step, not three
 // dependent ones), S: one row of the small layout, A_dl, B_dh: the lane's

@@ -878,10 +878,8 @@ __global__ __launch_bounds__(kBlock) void crc64_long_kernel(Long64Args a, LaneCo
 // lanes read position t's 16 entries: 128 contiguous bytes, no conflicts.
 // The reference times crc64ecma on 128 KiB at buf+1 (test_checksum.cpp:204-216).
 constexpr uint32_t kNib64 = 2048;
-// The mid layout at 64 bits takes up to 8 rows (16 MiB): past that the long
-// kernel is faster (repo:profiles/r05n_probe_mid.jsonl: 32 MiB 20.1 µs per
-// call queued against 16.2; 16 MiB 13.7 against 16.0).
-constexpr uint32_t kMid64Rows = 8, kMid64Blocks = kMid64Rows * kMidLanes;
+// The mid layout at 64 bits: the same 8 rows (16 MiB) as CRC-32C.
+constexpr uint32_t kMid64Rows = kMidRows, kMid64Blocks = kMid64Rows * kMidLanes;
 constexpr uint32_t kSm64D = 0, kSm64S = kNib64, kSm64A = 2 * kNib64, kSm64B = kSm64A + 8 * kNib64;
 constexpr uint32_t kSm64S2 = kSm64B + 7 * kNib64;                       // the mid layout's row shift
 constexpr uint32_t kSm64Lds = kSm64S2 + kNib64;                         // 36 KiB of tables in LDS

@@ -72,7 +72,7 @@ inline LongPlan long_plan_for(const void* data, uint64_t n, int cus, uint32_t sh
     //  up to 256 KiB (CRC-64 only: CRC-32C has its small kernel): 1 round of
     //  chunks of >= 4 KiB, one workgroup
     //  under 128 MiB (round 5, repo:profiles/r05p_ab_long_chunk_floor.jsonl;
-    //    the mid layout takes CRC-32C spans up to 32 MiB, CRC-64 16 MiB): 16 KiB
+    //    the mid layout takes spans up to 16 MiB): 16 KiB
     //    chunks fill only 64-128 of 256 CUs; 8 KiB: 64 MiB 64x2 0.0215 vs
     //    0.0232, 32 MiB 64x1 0.0160 vs 64x2/16 KiB 0.0225; 128 MiB 16 KiB stays
     //    best (0.0325 vs 0.0334). The rule, A/B against the 16 KiB cut

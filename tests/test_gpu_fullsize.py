@@ -207,7 +207,7 @@ def test_extend_device_plan_edges(torch_dev, oracle, mid):
     # 16-KiB-chunk limit of a full grid (64 MiB) +- a few bytes, odd sizes;
     # offsets 0, 1, 15; seeds; CRC-32C and CRC-64. Each call also leaves its
     # accumulator state zeroed for the next one (repeated calls agree). With
-    # the mid kernel on (the default) spans up to 32 MiB take the mid layout;
+    # the mid kernel on (the default) spans up to 16 MiB take the mid layout;
     # off, every span over 256 KiB takes the long kernel.
     torch = torch_dev
     ck.set_mid_kernel(mid)
@@ -335,14 +335,14 @@ MID_LANES = 512 * 256  # crc32c_kernels.h kMidWg * 256
 @pytest.mark.parametrize("crc64", [False, True])
 def test_extend_device_mid_path_edges(torch_dev, oracle, crc64):
     """The mid layout (crc32c_small_kernel / crc64_small_kernel over 512
-    workgroups, spans over 256 KiB up to 32 MiB, CRC-64 16 MiB): one byte
+    workgroups, spans over 256 KiB up to 16 MiB): one byte
     over the small limit, every row count at its boundaries (+-1 block, at
     offsets 0, 1, 15), the span limit and one byte past it (the long kernel),
     random sizes and seeds; calls queued back to back on one stream (one
     reduce state), all against the oracle."""
     torch = torch_dev
     row = MID_LANES * 16
-    rows_max = 8 if crc64 else 16  # crc64_kernels.h kMid64Rows: the long kernel past 16 MiB
+    rows_max = 8  # crc32c_kernels.h kMidRows: the long kernel past 16 MiB
     cap = rows_max * row + 64
     d = torch.empty(cap, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, cap, cap, 1, 0x5EED0E00 + crc64)
