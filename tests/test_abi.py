@@ -102,6 +102,12 @@ def test_argument_validation():
     assert e.value.code == -22
     with pytest.raises(ck.CrcError):
         ck.batch_strided(None, 4096, 4096, 4, None)
+    # tuning knobs added in round 5 (no GPU needed): ranges are checked
+    from photonlibos_amd._native import lib
+    assert lib().photon_crc_set_mid_kernel(2) == -22
+    assert lib().photon_crc_set_mid_kernel(1) == 0
+    assert lib().photon_crc_set_small_service(-1) == -22
+    assert lib().photon_crc_set_small_service(2000000) == -22
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
