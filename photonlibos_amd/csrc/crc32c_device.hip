@@ -656,12 +656,15 @@ void table_images_init() {
             r = hipGetLastError();
         }
         if (r == hipSuccess) r = hipStreamSynchronize(s);  // the images are written before any kernel sees them
-        if (r == hipSuccess)
+        bool published = false;  // once a slot may point into `base`, it is never freed
+        if (r == hipSuccess) {
+            published = true;
             r = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_table_image), img, sizeof img, 0, hipMemcpyHostToDevice, s);
+        }
         if (r == hipSuccess)
             r = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_table_image64), img64, sizeof img64, 0, hipMemcpyHostToDevice, s);
         if (r == hipSuccess) r = hipStreamSynchronize(s);
-        if (r != hipSuccess && base) (void)hipFree(base);
+        if (r != hipSuccess && base && !published) (void)hipFree(base);
         if (s) (void)hipStreamDestroy(s);
         return r;
     });
