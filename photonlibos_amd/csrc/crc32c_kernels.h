@@ -386,10 +386,36 @@ constexpr int table_slot() {
     return G == 4 ? 0 : G == 8 ? 1 : G == 16 ? 2 : G == 32 ? 3 : 4;
 }
 
+// PCRC_TABLE_DMA (A/B builds): the copy as LDS-DMA loads
+// (global_load_lds_dwordx4: no VGPR round trip, no ds_write; one wave
+// instruction fills 1 KiB of LDS at a wave-uniform base, the image being
+// lane-linear), then vmcnt(0) -- nothing else is in flight at a kernel's
+// start. Measured neutral against the register copy (C3, C5, CRC-64 C2/C3
+// shapes within 0.1 point, 1 GiB long kernel 0.1699 vs 0.1693 ms, 430 GPU
+// tests green on it; repo:profiles/r05y_ab_dma_vs_regcopy.jsonl), so the
+// register copy stays the default.
+#ifndef PCRC_TABLE_DMA
+#define PCRC_TABLE_DMA 0
+#endif
 template <uint32_t BYTES>
 __device__ __forceinline__ void copy_tables(uint32_t* lds, const uint32_t* img) {
     constexpr uint32_t kVec = BYTES / 16, kPer = (kVec + kBlock - 1) / kBlock;
     const uint32_t tid = threadIdx.x;
+    if constexpr (PCRC_TABLE_DMA) {
+        static_assert(kVec % 64 == 0, "whole 1 KiB wave pieces");
+        typedef __attribute__((address_space(1))) const void g_void;
+        typedef __attribute__((address_space(3))) void l_void;
+        const uint32_t lane = tid & 63u, w64 = tid & ~63u;
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t j0 = i * kBlock + w64;  // wave-uniform
+            if (j0 < kVec)
+                __builtin_amdgcn_global_load_lds((g_void*)(img + 4 * (j0 + lane)), (l_void*)(lds + 4 * j0), 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA writes have landed
+        lds_barrier();
+        return;
+    }
     u32x4 v[kPer];
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
