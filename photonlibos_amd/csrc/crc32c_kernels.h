@@ -779,7 +779,9 @@ template <int G, int U = 4, int MSG = 0>
 __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, LaneConsts kc, PowTable pt) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[lds_bytes_for<G>() / 4];
     // (A/B, repo:profiles/r05t_ab_overlap_c2_c3_c4.jsonl: C2 +0.1 point 3 of 3 rounds,
-    // C3 at G = 16 -0.1, C4 +-0; U = 8 spills)
+    // C3 at G = 16 -0.1, C4 +-0; U = 8 spills. At G = 16 the same overlap with
+    // the copy as LDS-DMA -- no VGPRs held, a counted vmcnt before the barrier --
+    // measured neutral, 4 rounds: repo:profiles/r05z_ab_dma_overlap_c3.jsonl.)
     constexpr bool kOverlap = MSG == 0 && G >= 32 && U <= 4 && PCRC_BATCH_OVERLAP && !PCRC_TABLE_BUILD;
     if constexpr (!kOverlap) load_tables<G>(lds, kc);
 
