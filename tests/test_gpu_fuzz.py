@@ -272,3 +272,40 @@ def test_fuzz_extend_device(dev_pool, oracle, round_):
         torch.cuda.synchronize()
         assert int(out32.cpu().numpy().view(np.uint32)[0]) == oracle.crc32c(host[o:o + n], s32), (o, n)
         assert int(out64.cpu().numpy().view(np.uint64)[0]) == oracle.crc64ecma(host[o:o + n], s64), (o, n)
+
+
+@pytest.mark.parametrize("mid", [True, False])
+def test_fuzz_extend_device_mixed_spans_one_stream(oracle, mid):
+    """Small (33 workgroups), mid (up to 512) and long (up to 256) launches of
+    both CRCs queued back to back on ONE stream, so they share its reduce
+    state: the two-level tree's group and top counts (closed forms in the
+    state's running workgroup count) must stay exact across launches of
+    every grid size (crc32c_kernels.h long_reduce_tree). 48 random spans of
+    0 B-20 MiB at random offsets and seeds, checked after one sync."""
+    import torch
+    pool = 24 << 20
+    host = datagen.stream_bytes(0xF0E1 + mid, pool)
+    d = torch.from_numpy(host.copy()).cuda()
+    rnd = random.Random(9100 + mid)
+    st = torch.cuda.Stream()
+    out32 = torch.zeros(48, dtype=torch.int32, device="cuda")
+    out64 = torch.zeros(48, dtype=torch.int64, device="cuda")
+    cases = []
+    ck.set_mid_kernel(mid)
+    try:
+        torch.cuda.synchronize()
+        for k in range(48):
+            n = rnd.choice([rnd.randrange(0, 300000), rnd.randrange(300000, 16 << 20), rnd.randrange(16 << 20, 20 << 20)])
+            o = rnd.randrange(0, pool - n)
+            s32, s64 = rnd.getrandbits(32), rnd.getrandbits(64)
+            ck.extend_device(d.data_ptr() + o, n, s32, out32[k:k + 1], stream=st)
+            ck.extend64_device(d.data_ptr() + o, n, out64[k:k + 1], seed=s64, stream=st)
+            cases.append((o, n, s32, s64))
+        st.synchronize()
+    finally:
+        ck.set_mid_kernel(True)
+    g32 = out32.cpu().numpy().view(np.uint32)
+    g64 = out64.cpu().numpy().view(np.uint64)
+    for k, (o, n, s32, s64) in enumerate(cases):
+        assert int(g32[k]) == oracle.crc32c(host[o:o + n], s32), (k, o, n)
+        assert int(g64[k]) == oracle.crc64ecma(host[o:o + n], s64), (k, o, n)
