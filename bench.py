@@ -106,6 +106,7 @@ def parse(argv=None):
     ap.add_argument("--no-c4-leg", action="store_true",
                     help="skip the C4 (BASELINE configs[3]) shard leg timed after the C2 leg")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--device", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (profiles/*.json) giving HBM bytes per launch (fallback when no live pass)")
     return ap.parse_args(argv)
@@ -389,7 +390,7 @@ def load_traffic(path, config):
     return int(v) if v else None
 
 
-def live_traffic(config, timeout=150):
+def live_traffic(config, device=0, timeout=150):
     """HBM read bytes per launch of the config's main kernel, measured now: a
     child `rocprofv3 --pmc FETCH_SIZE` pass (counters only, no tracing) over
     `bench.py --pmc-child` (3 launches of the same workload), FETCH_SIZE KiB
@@ -404,8 +405,15 @@ def live_traffic(config, timeout=150):
         cmd = [prof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--config", config, "--steps", "3", "--warmup", "1",
                "--pmc-child"]
+        # The child is a fresh 1-process run on this rank's device: drop the
+        # torch.distributed.run variables so it does not join the job's
+        # rendezvous, and pin it to the device this rank timed.
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                            "ROLE_WORLD_SIZE", "GROUP_WORLD_SIZE", "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=d)
+            r = subprocess.run(cmd + ["--device", str(device)], capture_output=True, text=True, timeout=timeout,
+                               cwd=d, env=env)
         except subprocess.TimeoutExpired:
             return None
         if r.returncode != 0:
@@ -420,6 +428,44 @@ def live_traffic(config, timeout=150):
         return None
     name = max(per, key=lambda k: float(np.mean(per[k])))
     return {"bytes": int(round(float(np.mean(per[name])) * 1024 * 2)), "kernel": name, "launches": len(per[name])}
+
+
+def rank0_tail(args, cfg, rank, world, dist, gpu=True, device=0):
+    """What `north_star` asks for "in the same run" beside the throughput, at
+    EVERY N: after the last timed leg and its barrier, rank 0 (a) takes live
+    FETCH_SIZE of the config's kernel on its own device in a child rocprofv3
+    process (a subprocess, never an exec of this GPU-initialised process) and
+    (b) times Photon's own CPU checksum (crc.cpp:339-358) on its host cores,
+    while the other ranks wait in a barrier, so the GPU ranks are idle and
+    the timed legs are untouched. The traffic is per launch of ONE rank's
+    shard (each rank runs the same per-GPU workload). Returns the fields for
+    the line; every rank returns after the barrier."""
+    tail = {"traffic": None, "traffic_source": None,
+            "traffic_scope": f"per launch on rank 0's device (device {device}); every rank runs the same "
+                             "per-GPU workload" if world > 1 else "per launch"}
+    if rank == 0:
+        if gpu and not args.no_live_pmc:
+            lt = live_traffic(args.config, device)
+            if lt is not None:
+                tail["traffic"] = lt["bytes"]
+                tail["traffic_source"] = (f"live rocprofv3 --pmc FETCH_SIZE x1024x2, {lt['launches']} launches, "
+                                          "child process after the timed legs")
+        if tail["traffic"] is None:
+            tail["traffic"] = load_traffic(args.traffic_json, args.config)
+            tail["traffic_source"] = (f"committed, not this run: profiles/pmc_{args.config}.json (an earlier "
+                                      "rocprofv3 --pmc FETCH_SIZE pass of this config on one GPU)"
+                                      if tail["traffic"] else "none: no live pass and no committed profile")
+        if not args.no_cpu_baseline:
+            base = cpu_baseline(cfg, args.cpu_seconds)
+            base["measured_by"] = (f"rank 0 of {world}, after the timed legs, other ranks idle in a barrier"
+                                   if world > 1 else "the bench process, after the timed legs")
+            tail["cpu_baseline"] = base
+            c1 = cpu_reference_c1(min(2.0, args.cpu_seconds))
+            if c1:
+                tail["cpu_reference_c1"] = c1
+    if dist is not None:
+        dist.barrier()
+    return tail
 
 
 # ------------------------------------------------------------- host-memory modes
@@ -864,6 +910,8 @@ def run_cpu_rehearsal(args, rank, world, dist):
               "value": round(aggregate_gibps(n4 * cnt4, args.steps, world, el4), 3), "unit": "GiB/s",
               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el4 / args.steps * 1e3, 4),
               "per_rank": r4, "rehearsal_step": f"{cnt4} x {n4} B host buffers per rank, crc32c() drop-in"}
+    tail = rank0_tail(args, CONFIGS[args.config], rank, world, dist, gpu=False)
+    extra = {k: tail[k] for k in ("cpu_baseline", "cpu_reference_c1") if k in tail}
     if rank == 0:
         print(json.dumps({"metric": "GiB/s CRC32C host rehearsal of the N-rank bench path (no GPU)",
                           "value": round(aggregate_gibps(n * cnt, args.steps, world, elapsed), 3), "unit": "GiB/s",
@@ -873,7 +921,11 @@ def run_cpu_rehearsal(args, rank, world, dist):
                           "rehearsal_step": f"{cnt} x {n} B host buffers per rank, crc32c() drop-in",
                           "config": {"workload": CONFIGS[args.config]["workload"], "config": args.config,
                                      "parallelism": f"shard-per-gpu x{world}"},
-                          **({"config_c4": c4} if c4 else {})}), flush=True)
+                          "roofline": {"bound": "hbm", "traffic": tail["traffic"],
+                                       "traffic_source": tail["traffic_source"],
+                                       "traffic_scope": tail["traffic_scope"],
+                                       "note": "rehearsal: no kernel was timed, only the tail's plumbing"},
+                          **extra, **({"config_c4": c4} if c4 else {})}), flush=True)
 
 
 # ----------------------------------------------------------------------- main
@@ -906,7 +958,7 @@ def main(argv=None):
     if visible < 1 or (world > visible and not args.share_gpus):
         print(f"bench.py: rank {rank}: {visible} GPU(s) visible for {world} ranks", file=sys.stderr)
         return 2
-    device = local % visible
+    device = args.device if args.device is not None else local % visible
     torch.cuda.set_device(device)
     ck.set_lanes_per_buffer(args.lanes)
     stream = torch.cuda.current_stream()
@@ -968,15 +1020,8 @@ def main(argv=None):
         c4 = c4_leg(args, rank, world, device, stream, dist)
         all_ok = all_ok and c4["self_check"]
 
-    traffic, traffic_src = None, None
-    if rank == 0 and world == 1 and not args.no_live_pmc:
-        lt = live_traffic(args.config)
-        if lt is not None:
-            traffic, traffic_src = lt["bytes"], f"live rocprofv3 --pmc FETCH_SIZE x1024x2, {lt['launches']} launches"
-    if traffic is None:
-        traffic = load_traffic(args.traffic_json, args.config)
-        traffic_src = (f"committed, not this run: profiles/pmc_{args.config}.json (an earlier rocprofv3 --pmc "
-                       "FETCH_SIZE pass of this config on one GPU)") if traffic else None
+    tail = rank0_tail(args, cfg, rank, world, dist, gpu=True, device=device)
+    traffic, traffic_src = tail["traffic"], tail["traffic_source"]
 
     if rank == 0:
         steady = bytes_step / (float(np.median([r["launch_ms"]["median"] for r in ranks])) * 1e-3) / 1e9
@@ -1018,9 +1063,10 @@ def main(argv=None):
             res["north_star_shape_g64"] = shape64
         if c4:
             res["config_c4"] = c4
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-            res["cpu_reference_c1"] = cpu_reference_c1(min(2.0, args.cpu_seconds))
+        res["roofline"]["traffic_scope"] = tail["traffic_scope"]
+        for k in ("cpu_baseline", "cpu_reference_c1"):
+            if k in tail:
+                res[k] = tail[k]
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -77,6 +77,8 @@ def test_bench_defaults():
 
 
 def _run_bench(*argv, timeout=240):
+    if "--cpu-seconds" not in argv:  # rank 0's CPU baseline leg, kept short on CPU
+        argv = (*argv, "--cpu-seconds", "0.2")
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
@@ -167,3 +169,45 @@ def test_two_rank_line_carries_c4_leg():
 def oracle_crc(data):
     from tests import _oracle
     return _oracle.crc32c(data)
+
+
+def test_two_rank_line_carries_cpu_baseline_and_traffic():
+    """an N>1 line carries what `north_star` asks for "in the
+    same run" -- Photon's CPU checksum timed on the host cores (rank 0, after
+    the timed legs, the other ranks idle in a barrier) and the HBM traffic of
+    the config's kernel with its source and scope (rank 0's device). Before
+    round 6 both were gated on world == 1."""
+    r = _run_bench("--gpus", "2", "--cpu-rehearsal", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3")
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    base = res["cpu_baseline"]
+    assert base["value"] > 0 and base["unit"] == "GiB/s" and base["cores"] >= 1
+    assert base["kind"] in ("reference", "port") and "rank 0 of 2" in base["measured_by"]
+    roof = res["roofline"]
+    assert roof["traffic_source"] and "rank 0" in roof["traffic_scope"]
+    # the committed C2 profile is what a rehearsal (no rocprofv3 child) reads
+    assert roof["traffic"] == bench.load_traffic(None, "c2")
+    # --no-cpu-baseline drops the leg at any N
+    r0 = _run_bench("--gpus", "2", "--cpu-rehearsal", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+                    "--no-c4-leg")
+    assert "cpu_baseline" not in json.loads([ln for ln in r0.stdout.splitlines() if ln.startswith("{")][0])
+
+
+def test_pmc_child_env_leaves_the_rendezvous(monkeypatch):
+    """The live FETCH_SIZE child of an N>1 rank must not join the job's
+    rendezvous: live_traffic strips the torch.distributed.run variables and
+    pins the child to the rank's device."""
+    seen = {}
+
+    def fake_run(cmd, **kw):
+        seen["cmd"], seen["env"] = cmd, kw["env"]
+        raise subprocess.TimeoutExpired(cmd, 1)
+    monkeypatch.setattr(bench.shutil, "which", lambda _: sys.executable)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    assert bench.live_traffic("c2", device=3) is None
+    assert not {"WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"} & set(seen["env"])
+    assert seen["cmd"][-2:] == ["--device", "3"] and "--pmc-child" in seen["cmd"]
