@@ -215,7 +215,15 @@ int photon_crc32c_extend_spans(const photon_crc_span* spans, int nspans, uint32_
  * errno is set to EIO, and the bytes are copied to the host and checksummed
  * by the host engine (same result as the reference); if even that copy fails
  * the process aborts with a message. Returns 0, or -EIO if a routed call
- * failed since the last switch (photon_crc_dispatch_fallbacks() counts them). */
+ * failed since the last switch (photon_crc_dispatch_fallbacks() counts them).
+ * Ordering: like the reference's crc32c_extend (crc32c.h:30-33), a routed
+ * call checksums the bytes that exist when it is called. It takes no stream
+ * and orders against none of the caller's: the caller must have COMPLETED
+ * every write to the buffer (kernel, copy, vDMA, peer write) before the call,
+ * e.g. hipStreamSynchronize / hipEventSynchronize on the producer's stream.
+ * A write still in flight may or may not be seen. For stream-ordered work use
+ * photon_crc32c_extend_device / photon_crc64ecma_extend_device on the
+ * producer's stream instead. */
 int photon_crc_set_device_dispatch(int on);
 /* Number of routed calls so far whose device work failed and that were
  * recomputed on the host (0 in a healthy process; tests assert it). */

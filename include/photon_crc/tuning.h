@@ -90,17 +90,39 @@ int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
  * first request). Default 200 (or the environment variable
  * PHOTON_CRC_SMALL_SERVICE at load); 0 = off, a launch per call; turning it
  * off ends running launches. crc64ecma_extend has a service of its own (34
- * KiB of LDS per workgroup). A library launch whose workgroups could not
- * share a CU with a service's (the CRC-64 batch and long kernels, 158 KiB of
- * LDS) ends the running services first. One call at a time uses it; concurrent
- * calls take the launch path. While it runs, hipDeviceSynchronize() and
- * anything else that waits for every stream of the device wait until it ends
- * (at most idle_us after the last call), and the 33 workgroups hold their
- * CUs' resources beside other kernels. DESIGN.md §4.0 has the latency. */
+ * KiB of LDS per workgroup). Every batch, message or long launch of this
+ * library ends the running services of its device first, and no routed call
+ * starts a service launch while one is queued or running (it takes the launch
+ * path), so those kernels never run beside them. One call at a time uses it; concurrent calls take
+ * the launch path. While it runs, hipDeviceSynchronize() and anything else
+ * that waits for every stream of the device wait until it ends: at most
+ * idle_us after the last call, and at most the launch's life (below) under
+ * steady traffic; the library ends it before its own hipFree calls. An idle
+ * launch naps between doorbell polls after 20 us without a request. DESIGN.md
+ * §4.0 has the latency. */
 int photon_crc_set_small_service(int idle_us);
+/* Life of one service launch, 100..1000000 us (default 2000): under steady
+ * routed traffic a launch ends after it and the next call starts another, so
+ * it bounds how long a device-wide wait can stall behind the service. */
+int photon_crc_set_small_service_life(int life_us);
+/* The service's doorbell: 1 (default) = device memory the host writes through
+ * the PCIe BAR, used only when the device reports a large BAR and the host
+ * mapping was verified at creation (fault-free probe: the kernel copies the
+ * words to and from a pipe, EFAULT if unmapped); 0 = the pinned host area
+ * (also PHOTON_CRC_SVC_DOORBELL=host in the environment at load). Ends
+ * running launches; the next launch uses the new doorbell. */
+int photon_crc_set_service_doorbell(int bar);
+/* The doorbell the current device's service of `kind` (0 CRC-32C, 1 CRC-64)
+ * rings: 1 BAR, 0 pinned host memory, -ENOENT if it was never started. */
+int photon_crc_small_service_doorbell(int kind);
 /* Routed small calls served by the service, launches of it, and calls that
  * found it ending and took the launch path (tests). */
 int photon_crc_small_service_stats(uint64_t* served, uint64_t* starts, uint64_t* missed);
+/* Routed small calls that would have started a service launch while a batch,
+ * message or long launch of this library was still queued or running on the
+ * device, and took the launch path instead (the two never share the chip:
+ * their workgroups do not fit on one CU together). */
+uint64_t photon_crc_small_service_deferred(void);
 
 /* Lanes per buffer the engine picks for buffers of typical length n (the
  * lane-group table of DESIGN.md §4, or the override when one is set). */

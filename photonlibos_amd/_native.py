@@ -71,6 +71,10 @@ def _declare(L):
     fn("photon_crc_set_small_service", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_set_mid_kernel", ctypes.c_int, ctypes.c_int)
     fn("photon_crc_small_service_stats", ctypes.c_int, vp, vp, vp)
+    fn("photon_crc_set_small_service_life", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc_set_service_doorbell", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc_small_service_doorbell", ctypes.c_int, ctypes.c_int)
+    fn("photon_crc_small_service_deferred", u64)
     fn("photon_crc64_set_full_rows", ctypes.c_int, ctypes.c_int, ctypes.c_int)
     fn("photon_crc_host_register", ctypes.c_int, vp, u64)
     fn("photon_crc_stream_create", ctypes.c_int, ctypes.POINTER(vp))

@@ -534,6 +534,36 @@ def set_small_service(idle_us):
     _check(lib().photon_crc_set_small_service(int(idle_us)))
 
 
+def set_small_service_life(life_us):
+    """Life of one service launch (default 2000 us): the bound on how long a
+    device-wide wait stalls behind it under steady routed traffic (tuning)."""
+    _check(lib().photon_crc_set_small_service_life(int(life_us)))
+
+
+def set_service_doorbell(bar):
+    """The service's doorbell: True = device memory through the PCIe BAR (the
+    default, when the host mapping was verified), False = pinned host memory.
+    Ends running launches (tuning)."""
+    _check(lib().photon_crc_set_service_doorbell(1 if bar else 0))
+
+
+def small_service_doorbell(kind=0):
+    """'bar' or 'pinned': the doorbell the current device's service of `kind`
+    (0 CRC-32C, 1 CRC-64) rings; None if that service was never started."""
+    r = lib().photon_crc_small_service_doorbell(int(kind))
+    if r == -2:  # -ENOENT
+        return None
+    _check(r if r < 0 else 0)
+    return "bar" if r == 1 else "pinned"
+
+
+def small_service_deferred():
+    """Routed small calls that took the launch path because a batch / long
+    launch of the library was in flight when they would have started a
+    service launch (tests)."""
+    return int(lib().photon_crc_small_service_deferred())
+
+
 def small_service_stats():
     """(served, starts, missed): routed small calls the service served, its
     launches, calls that found it ending (tests)."""

@@ -194,6 +194,7 @@ struct photon_crc_msg_batch {
 namespace {
 
 void free_batch(photon_crc_msg_batch* b) {
+    pcrc::services_end_before_free();
     if (b->done_ev) (void)hipEventDestroy(b->done_ev);
     for (void* p : {(void*)b->h_iov, (void*)b->h_start, (void*)b->h_expect, (void*)b->h_out})
         if (p) (void)hipHostFree(p);

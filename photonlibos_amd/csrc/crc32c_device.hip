@@ -33,11 +33,13 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <fcntl.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
 #include <sys/prctl.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <chrono>
@@ -107,13 +109,47 @@ int svc_idle_from_env() {
     return v < 0 ? 0 : v > 1000000 ? 1000000 : (int)v;
 }
 std::atomic<int> g_svc_idle_us{svc_idle_from_env()};
-std::atomic<uint64_t> g_svc_served{0}, g_svc_starts{0}, g_svc_missed{0};
+// Life of one service launch in µs (photon_crc_set_small_service_life): under
+// steady traffic a launch ends after it and the next call starts another, so a
+// caller's device-wide wait (hipDeviceSynchronize, hipFree) stalls at most
+// this long behind it. 2 ms: one relaunch (~10 µs) per 2 ms of traffic.
+std::atomic<int> g_svc_life_us{2000};
+// The doorbell: 1 = device memory written through the PCIe BAR when the host
+// mapping was verified (the default), 0 = the pinned host area (also with
+// PHOTON_CRC_SVC_DOORBELL=host at load); photon_crc_set_service_doorbell.
+int svc_bell_from_env() {
+    const char* e = getenv("PHOTON_CRC_SVC_DOORBELL");
+    return e && (!strcmp(e, "host") || !strcmp(e, "pinned") || !strcmp(e, "0")) ? 0 : 1;
+}
+std::atomic<int> g_svc_bell{svc_bell_from_env()};
+std::atomic<uint64_t> g_svc_served{0}, g_svc_starts{0}, g_svc_missed{0}, g_svc_deferred{0};
+std::atomic<int> g_svc_made{0};  // services created in this process (HeavyLaunch's fast path)
 void service_end_all();  // (below) end every running service launch
-// (below) before a launch that needs `lds` bytes of LDS per workgroup: end
-// the running small-buffer services whose workgroups would keep it off
-// their CUs (their LDS + lds > 160 KiB)
-void svc_yield(uint32_t lds);
-constexpr uint32_t kWholeCu = 160u * 1024u;  // the CRC-64 batch / long kernels (158 KiB)
+// (below) before a batch, message or long launch of this library: end the
+// running small-buffer services of the current device, so the launch never
+// waits for their idle time
+void svc_yield();
+// (below) after such a launch: note it in the device's ring of heavy-launch
+// events, which a routed call reads before it starts a service launch
+void heavy_mark(hipStream_t st);
+
+// A batch / message / long launch and the resident services never share the
+// chip. Its workgroups (4 waves per SIMD at up to 120 VGPRs, 100-158 KiB of
+// LDS) and a service's (100-126 VGPRs a wave) do not fit on one CU together,
+// so a service beside a persistent one-workgroup-per-CU grid holds 33 of its
+// workgroups off their CUs: C2 measured 0.83-0.97 ms per launch beside an idle
+// service against 0.62-0.65 alone (repo:profiles/r06b_power_coresident.jsonl).
+// So the launch ends the services first (svc_yield), and marks itself in the
+// ring (heavy_mark) that keeps routed calls from starting a new service launch
+// until it has finished -- those calls take the launch path meanwhile.
+struct HeavyLaunch {
+    hipStream_t st;
+    explicit HeavyLaunch(hipStream_t s) : st(s) { svc_yield(); }
+    ~HeavyLaunch() { heavy_mark(st); }
+};
+// (below) 1 = the device's service of this kind rings a BAR doorbell, 0 =
+// the pinned one, -ENOENT = no service created yet
+int service_doorbell_of(int dev, int kind);
 
 int fail(int code, const std::string& what) {
     g_err = what;
@@ -277,6 +313,7 @@ int64_t scratch_trim_locked(bool all) {
         uint64_t& kept = idle_dev[b->dev & 63];
         if (idle && (all || b->cap > kScratchKeep || kept + b->cap > kScratchMaxIdle)) {
             (void)hipEventDestroy(b->last);
+            services_end_before_free();
             (void)hipFree(b->p);
             freed += (int64_t)b->cap;
             delete b;
@@ -419,15 +456,6 @@ int batch_rows(int g) {
     return u >= 0 ? u : g == 16 ? 2 : 4;
 }
 
-uint32_t lds_for_lanes(int g) {
-    switch (g) {
-        case 64: return lds_bytes_for<64>();
-        case 32: return lds_bytes_for<32>();
-        case 16: return lds_bytes_for<16>();
-        case 8: return lds_bytes_for<8>();
-        default: return lds_bytes_for<4>();
-    }
-}
 
 // lanes: 0 = by typical_len (batch_lanes), else the lane-group size.
 int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, int lanes = 0) {
@@ -443,7 +471,7 @@ int launch_batch(const BatchArgs& a, uint64_t typical_len, hipStream_t stream, i
     if (const int cap = g_grid_cap.load(std::memory_order_relaxed)) grid = grid > (uint64_t)cap ? (uint64_t)cap : grid;
     const int rows_per_step = batch_rows(g);
     const LaneConsts& kc = lane_consts(g);
-    svc_yield(lds_for_lanes(g));
+    HeavyLaunch heavy(stream);
 #define LB(GG, UU) \
     hipLaunchKernelGGL((crc32c_batch_kernel<GG, UU>), dim3(grid), dim3(kBlock), 0, stream, a, kc, pow_table())
 #define LBG(UU)                    \
@@ -500,7 +528,7 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     uint64_t grid = (waves + kWaves - 1) / kWaves;
     if (grid > (uint64_t)cus) grid = cus;
     const LaneConsts64& kc = lane_consts64(g);
-    svc_yield(kWholeCu);
+    HeavyLaunch heavy(stream);
     // Whole-step uniform batches: the full-row kernel (crc64_kernels.h).
     const uint32_t full = g_full64.load(std::memory_order_relaxed);
     const int fu = (int)(full >> 4);
@@ -1173,6 +1201,28 @@ int photon_crc_set_small_service(int idle_us) {
     return 0;
 }
 
+int photon_crc_set_small_service_life(int life_us) {
+    if (life_us < 100 || life_us > 1000000) return fail(-EINVAL, "service life must be 100..1000000 us");
+    g_svc_life_us.store(life_us, std::memory_order_relaxed);
+    return 0;
+}
+
+int photon_crc_set_service_doorbell(int bar) {
+    if (bar != 0 && bar != 1) return fail(-EINVAL, "doorbell must be 0 (pinned host) or 1 (device BAR)");
+    service_end_all();  // launches from now on pick the doorbell
+    g_svc_bell.store(bar, std::memory_order_relaxed);
+    return 0;
+}
+
+int photon_crc_small_service_doorbell(int kind) {
+    if (kind != 0 && kind != 1) return fail(-EINVAL, "kind must be 0 (CRC-32C) or 1 (CRC-64)");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(-ENODEV, "no device");
+    return service_doorbell_of(dev, kind);
+}
+
+uint64_t photon_crc_small_service_deferred(void) { return g_svc_deferred.load(std::memory_order_relaxed); }
+
 int photon_crc_small_service_stats(uint64_t* served, uint64_t* starts, uint64_t* missed) {
     if (served) *served = g_svc_served.load(std::memory_order_relaxed);
     if (starts) *starts = g_svc_starts.load(std::memory_order_relaxed);
@@ -1254,6 +1304,7 @@ int host_batch_impl(const void* h_base, uint64_t stride, uint64_t nbytes, uint64
     hipError_t e;
     const uint64_t bytes = count * sizeof(T);
     if (p->out_cap < bytes) {
+        services_end_before_free();
         if (p->d_out) (void)hipFree(p->d_out);
         if (p->d_seeds) (void)hipFree(p->d_seeds);
         p->d_out = p->d_seeds = nullptr;
@@ -1424,7 +1475,7 @@ int pcrc::batch_msg_lanes(const photon_crc_iovec* d_iov, const uint64_t* d_msg_s
         uint64_t grid = ((nmsg + gpw - 1) / gpw + kWaves - 1) / kWaves;
         if (grid > (uint64_t)cus) grid = cus;
         const LaneConsts& kc = lane_consts(g);
-        svc_yield(lds_for_lanes(g));
+        HeavyLaunch heavy(st);
 #define LM(GG, UU)                                                                                            \
     do {                                                                                                      \
         if (a.out)                                                                                            \
@@ -1622,7 +1673,7 @@ int extend64_device_long(const void* d_data, uint64_t nbytes, uint64_t seed, uin
     Long64Args a{};
     long_args64(&a, lp, pw, d_data, seed, d_out);
     a.out_tag = tag;
-    svc_yield(kWholeCu);
+    HeavyLaunch heavy(st);
     return long_launch(st, lp.grid, "crc64_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint64_t*>(state);
         a.tbase = base;
@@ -1760,7 +1811,7 @@ int extend_device_long(const void* d_data, uint64_t nbytes, uint32_t seed, uint3
     LongArgs a{};
     long_args(&a, lp, pw, d_data, seed, d_out);
     a.out_tag = tag;
-    svc_yield(lds_for_lanes(lp.lanes));
+    HeavyLaunch heavy(st);
     return long_launch(st, lp.grid, "crc32c_long_kernel launch", [&](void* state, uint64_t base, uint32_t reset) {
         a.acc = static_cast<uint32_t*>(state);
         a.tbase = base;
@@ -2286,7 +2337,7 @@ int routed_small64(int dev, const Small64Args& sa0, uint32_t sgrid, uint64_t* cr
 
 // The resident small-buffer services (crc32c_kernels.h
 // crc32c_small_service_kernel, crc64_kernels.h crc64_small_service_kernel;
-// opt-in, photon_crc_set_small_service). One per device and CRC width, each
+// on by default, photon_crc_set_small_service). One per device and CRC width, each
 // started by the first routed call of its width: a non-blocking stream, the
 // doorbell, the pinned slot area, the last seq posted. One call at a time
 // uses a service (try-lock: a call that finds it busy, or not running, takes
@@ -2298,10 +2349,12 @@ struct SmallService {
     hipStream_t st = nullptr;
     uint64_t* h = nullptr;     // host view of the pinned area (quit, slots)
     uint64_t* d = nullptr;     // its device view
-    uint64_t* bell = nullptr;  // the doorbell: uncached device memory (large BAR: the host writes it
-                               // through the BAR at the same address) or the pinned area (h / d)
+    uint64_t* vram = nullptr;  // uncached device memory the host writes through the BAR at the same
+                               // address (large BAR, mapping verified by bar_host_rw), else null
+    // the doorbell of the current launch: vram, or the pinned area (h / d);
+    // chosen at each launch, read without the lock by svc_yield
+    std::atomic<uint64_t*> bell{nullptr};
     uint64_t* bell_d = nullptr;
-    bool bar = false;
     uint32_t seq = 0;          // last seq posted (never 0)
     std::atomic<bool> live{false};  // a launch that has not been seen to end
 };
@@ -2312,12 +2365,41 @@ void set_live(SmallService* s, bool on) {
 
 // Doorbell words from the host; the BAR mapping is write-combined: the
 // stores leave the CPU at the sfence.
-inline void bell_put(SmallService* s, uint32_t i, uint64_t v) { __atomic_store_n(&s->bell[i], v, __ATOMIC_RELAXED); }
+inline void bell_put(SmallService* s, uint32_t i, uint64_t v) {
+    __atomic_store_n(s->bell.load(std::memory_order_relaxed) + i, v, __ATOMIC_RELAXED);
+}
 inline void bell_flush() { __builtin_ia32_sfence(); }
 PerDevice<SmallService*> g_svc[2];
 std::mutex g_svc_list_mu;
 std::vector<SmallService*> g_svc_list;
-constexpr uint32_t kSvcLifeTicks = 10000000u;  // 100 ms of the 100 MHz clock, then a new launch
+
+// Does the host reach device memory p (8 bytes) at the same address, for
+// reads and writes? hipDeviceAttributeIsLargeBar does not prove it (a VF or a
+// container may leave the VRAM unmapped for the CPU), and a plain access to an
+// unmapped address would fault inside a drop-in call that has no error
+// channel. The kernel's copy to and from a pipe touches p instead: an
+// unmapped p gives EFAULT, never a signal. A device-side write is
+// read back by the host, a host write by the device.
+bool bar_host_rw(uint64_t* p, hipStream_t st) {
+    int fd[2];
+    if (pipe2(fd, O_CLOEXEC) != 0) return false;
+    bool ok = false;
+    do {
+        uint64_t got = 0, back = 0;
+        const uint64_t dev_word = 0xA5A5A5A5A5A5A5A5ull, host_word = 0x5AC3C3A55AC3C3A5ull;
+        if (hipMemsetAsync(p, 0xA5, 8, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) break;
+        if (write(fd[1], p, 8) != 8 || read(fd[0], &got, 8) != 8 || got != dev_word) break;
+        if (write(fd[1], &host_word, 8) != 8 || read(fd[0], p, 8) != 8) break;
+        bell_flush();
+        if (hipMemcpyAsync(&back, p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess || back != host_word)
+            break;
+        ok = true;
+    } while (false);
+    close(fd[0]);
+    close(fd[1]);
+    return ok;
+}
 
 // Tell a live service to end and wait for its waves (caller holds s->mu).
 void service_end(SmallService* s) {
@@ -2391,35 +2473,40 @@ int service_get(int dev, int kind, SmallService** out) {
             if (r == hipSuccess) r = hipGetDevice(&dev);
             if (r == hipSuccess && hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) == hipSuccess &&
                 large_bar == 1 &&
-                hipExtMallocWithFlags(reinterpret_cast<void**>(&s->bell), 4096, hipDeviceMallocUncached) == hipSuccess) {
-                s->bar = true;  // host stores through the BAR at the device address
-                s->bell_d = s->bell;
-                r = hipMemsetAsync(s->bell, 0, 4096, s->st);  // complete before the host writes it
+                hipExtMallocWithFlags(reinterpret_cast<void**>(&s->vram), 4096, hipDeviceMallocUncached) == hipSuccess) {
+                if (!bar_host_rw(s->vram, s->st)) {  // not mapped for the host here: the pinned doorbell
+                    (void)hipFree(s->vram);
+                    s->vram = nullptr;
+                }
+                if (s->vram) r = hipMemsetAsync(s->vram, 0, 4096, s->st);  // complete before the host writes it
                 if (r == hipSuccess) r = hipStreamSynchronize(s->st);
-            } else {
-                (void)hipGetLastError();
-                s->bell = nullptr;
             }
+            (void)hipGetLastError();
             return r;
         });
         if (e != hipSuccess) {
-            if (s->bell) (void)hipFree(s->bell);
+            if (s->vram) (void)hipFree(s->vram);
             if (s->h) (void)hipHostFree(s->h);
             if (s->st) (void)hipStreamDestroy(s->st);
             delete s;
             return hip_fail(e, "small-buffer service");
         }
         memset(s->h, 0, bytes);
-        if (!s->bar) {
-            s->bell = s->h;
-            s->bell_d = s->d;
-        }
+        s->bell.store(s->h, std::memory_order_relaxed);  // until the first launch picks its doorbell
+        s->bell_d = s->d;
         std::lock_guard<std::mutex> lk(g_svc_list_mu);
         if (g_svc_list.empty()) atexit(service_end_at_exit);  // after HIP's init: runs before its teardown
         g_svc_list.push_back(s);
+        g_svc_made.fetch_add(1, std::memory_order_relaxed);
         slot = s;
         return 0;
     });
+}
+
+int service_doorbell_of(int dev, int kind) {
+    SmallService* s = g_svc[kind].peek(dev);
+    if (!s) return -ENOENT;
+    return s->bell.load(std::memory_order_relaxed) == s->h ? 0 : 1;
 }
 
 void services_end_on_impl(int dev) {
@@ -2432,16 +2519,15 @@ void services_end_on_impl(int dev) {
     }
 }
 
-// LDS per workgroup of the two services (the kernels' tables, command words
-// and reduce words, rounded up to 1 KiB).
-constexpr uint32_t kSvcLdsBytes[2] = {14u * 1024u, 35u * 1024u};
-
-void svc_yield(uint32_t lds) {
+// Every batch / message / mid / long launch ends the services first (VERDICT
+// r5 #2): deciding co-residency by LDS alone ignored VGPRs and wave
+// slots, and a resident launch beside a streaming kernel on a power-bound
+// chip is not free. A routed call after the launch starts a new service.
+void svc_yield() {
     if (g_svc_live.load(std::memory_order_relaxed) == 0) return;
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) return;
     for (int kind = 0; kind < 2; ++kind) {
-        if (lds + kSvcLdsBytes[kind] <= kWholeCu) continue;
         SmallService* s = g_svc[kind].peek(dev);
         if (!s || !s->live.load()) continue;
         // no lock: a call in flight sees quit, waits for the stream and takes
@@ -2450,6 +2536,64 @@ void svc_yield(uint32_t lds) {
         bell_flush();
         __atomic_store_n(&s->h[kSvcQuit], 1ull, __ATOMIC_RELAXED);
     }
+}
+
+// The ring of a device's last kHeavyEvents heavy launches (HeavyLaunch),
+// kept only once a service exists in the process (a process without routed
+// calls pays nothing). Launches captured into a graph are not marked.
+constexpr int kHeavyEvents = 8;
+struct HeavyRing {
+    std::mutex mu;
+    hipEvent_t ev[kHeavyEvents] = {};
+    bool pending[kHeavyEvents] = {};
+    uint32_t next = 0;
+};
+PerDevice<HeavyRing*> g_heavy;
+
+void heavy_mark(hipStream_t st) {
+    if (g_svc_made.load(std::memory_order_relaxed) == 0) return;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    HeavyRing* r = nullptr;
+    if (g_heavy.get(dev, &r, [](int, HeavyRing*& slot) {
+            auto* h = new HeavyRing;
+            const hipError_t e = relaxed_capture([&] {
+                hipError_t x = hipSuccess;
+                for (int i = 0; i < kHeavyEvents && x == hipSuccess; ++i)
+                    x = hipEventCreateWithFlags(&h->ev[i], hipEventDisableTiming);
+                return x;
+            });
+            if (e != hipSuccess) {
+                for (hipEvent_t ev : h->ev)
+                    if (ev) (void)hipEventDestroy(ev);
+                delete h;
+                return -EIO;
+            }
+            slot = h;
+            return 0;
+        }))
+        return;
+    std::lock_guard<std::mutex> lk(r->mu);
+    const uint32_t i = r->next++ % kHeavyEvents;
+    r->pending[i] = hipEventRecord(r->ev[i], st) == hipSuccess;
+}
+
+// Is a heavy launch marked on `dev` still queued or running?
+bool heavy_in_flight(int dev) {
+    HeavyRing* r = g_heavy.peek(dev);
+    if (!r) return false;
+    std::lock_guard<std::mutex> lk(r->mu);
+    bool busy = false;
+    for (int i = 0; i < kHeavyEvents; ++i) {
+        if (!r->pending[i]) continue;
+        if (hipEventQuery(r->ev[i]) == hipErrorNotReady)
+            busy = true;
+        else
+            r->pending[i] = false;
+    }
+    return busy;
 }
 
 // Serve one routed small call through the service of its width: 0 = the
@@ -2470,6 +2614,10 @@ int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0
         set_live(s, false);
     }
     if (!s->live) {
+        if (heavy_in_flight(dev)) {  // a batch / long launch holds the CUs: the launch path
+            g_svc_deferred.fetch_add(1, std::memory_order_relaxed);
+            return 1;
+        }
         const void* img = nullptr;
         if (kind == 0) {
             const uint32_t* i32 = nullptr;
@@ -2480,13 +2628,20 @@ int service_small(int dev, int kind, const uint8_t* a0, uint32_t nb, uint32_t s0
             if (small64_image(dev, &i64)) return 1;
             img = i64;
         }
+        // this launch's doorbell; its request words carry the last seq posted
+        // (never taken as fresh), whichever doorbell the last launch used
+        const bool bar = s->vram && g_svc_bell.load(std::memory_order_relaxed);
+        s->bell.store(bar ? s->vram : s->h, std::memory_order_relaxed);
+        s->bell_d = bar ? s->vram : s->d;
+        for (uint32_t i = 0; i < kSvcStop; ++i) bell_put(s, i, (uint64_t)s->seq << 32);
         bell_put(s, kSvcStop, 0ull);
         bell_put(s, kSvcQuit, 0ull);
         bell_flush();
         __atomic_store_n(&s->h[kSvcQuit], 0ull, __ATOMIC_RELAXED);
         for (uint32_t b = 0; b < kSmallWg; ++b)  // the last launch's waves have all left (stream synchronised)
             __atomic_store_n(&s->h[kSvcSlots + kSvcSlotStride * b + kSvcExitWord], 0ull, __ATOMIC_RELAXED);
-        ServiceArgs a{img, s->bell_d, s->d, s->seq, 100u * (uint32_t)idle_us, kSvcLifeTicks};
+        const uint32_t life = 100u * (uint32_t)g_svc_life_us.load(std::memory_order_relaxed);
+        ServiceArgs a{img, s->bell_d, s->d, s->seq, 100u * (uint32_t)idle_us, life};
         const hipError_t e = relaxed_capture([&] {
             if (kind == 0)
                 hipLaunchKernelGGL(crc32c_small_service_kernel, dim3(kSmallWg), dim3(256), 0, s->st, a);
@@ -2713,3 +2868,6 @@ extern "C" void* photon_crc_test_service_area(void) {
 
 // internal.h: for the vDMA initiator's device-wide fence (vdma_hip.cpp).
 void pcrc::services_end_on(int dev) { services_end_on_impl(dev); }
+void pcrc::services_end_before_free() {
+    if (pcrc::g_svc_live.load(std::memory_order_relaxed)) pcrc::service_end_all();
+}

@@ -1865,9 +1865,9 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
     }
 }
 
-// The resident small-buffer service (routed drop-in calls of <= 256 KiB,
-// opt-in: photon_crc_set_small_service; CRC-64: crc64_kernels.h
-// crc64_small_service_kernel). A launch of kSmallWg workgroups that stays on
+// The resident small-buffer service (routed drop-in calls of up to 2 MiB,
+// on by default once device dispatch is on, photon_crc_set_small_service;
+// CRC-64: crc64_kernels.h crc64_small_service_kernel). A launch of kSmallWg workgroups that stays on
 // the chip between calls: the tables and the basis words are loaded ONCE,
 // and a call costs no launch -- the host writes the request into the
 // doorbell, wave 0 of every workgroup polls it and hands it to its
@@ -1895,6 +1895,10 @@ __global__ __launch_bounds__(256) void crc32c_small_kernel(SmallArgs a) {
 //        starts a new launch for later calls.
 // Pinned area: word 7 quit (above); 16 + 8 b: slot of workgroup b, {seq,
 // value} (CRC-64: {seq, low}, {seq, high}); 16 + 8 b + 3: workgroup b left.
+// A poll finds nothing for kSvcNapTicks: wave 0 sleeps ~0.3 µs (s_sleep)
+// before each further poll until the next request, so an idle launch neither
+// streams doorbell reads nor keeps its SIMD's issue port busy (a request after
+// such a pause is seen at most one nap later).
 // Every wave exits: workgroup 0 on stop / idle / life, the others on stop,
 // quit or 2 x life by their own clock (a workgroup 0 that never became
 // resident cannot keep them alive). The decision is per workgroup (wave 0's,
@@ -1906,6 +1910,7 @@ constexpr uint32_t kSvcStop = 6, kSvcQuit = 7, kSvcSlots = 16, kSvcSlotStride = 
 constexpr uint32_t kSvcExitWord = 3;  // word 3 of a workgroup's slot line: set as the workgroup leaves
 constexpr uint32_t kSvcWords = kSvcSlots + kSvcSlotStride * kSmallWg;
 constexpr uint32_t kSvcLds = kSmLds + 32u * 32u * 4u;  // the tables, then the tail basis words
+constexpr uint64_t kSvcNapTicks = 2000;  // 20 µs of the 100 MHz clock without a request: nap between polls
 
 struct ServiceArgs {
     const void* image;  // the small kernel's image (tables, wave and tail basis words)
@@ -1932,9 +1937,11 @@ __device__ __forceinline__ void service_loop(const ServiceArgs& s, uint32_t (&cm
     uint32_t last = s.last;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t tl = t0;
+    bool nap = false;  // wave 0: the last poll found nothing for kSvcNapTicks
     for (uint32_t round = 0;; ++round) {
         uint32_t* c = cmd[round & 1u];
         if (wave == 0) {
+            if (nap) __builtin_amdgcn_s_sleep(10);  // 640 cycles
             const uint64_t t_issue = __builtin_amdgcn_s_memrealtime();
             const uint64_t v = lane <= kSvcQuit ? __hip_atomic_load(s.bell + lane, __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_SYSTEM)
@@ -1958,6 +1965,7 @@ __device__ __forceinline__ void service_loop(const ServiceArgs& s, uint32_t (&cm
                     cm = 2u;
                 }
             }
+            nap = !fresh && now - tl > kSvcNapTicks;
             if (fresh) {
                 last = seq;
                 tl = now;

@@ -267,6 +267,7 @@ int photon_crc_device_alloc(void** ptr, uint64_t nbytes) {
 
 int photon_crc_device_free(void* ptr) {
     if (!ptr) return 0;
+    pcrc::services_end_before_free();
     hipError_t e = hipFree(ptr);
     return e == hipSuccess ? 0 : report_hip_error(e, "hipFree");
 }

@@ -29,4 +29,8 @@ void forget_registration(const void* p);
 // for their waves), so that a device-wide synchronise that follows does not
 // wait for their idle time (the next routed call starts them again).
 void services_end_on(int dev);
+// The same on every device that has one running: before the library's own
+// hipFree (which waits for the device's streams), so it does not wait for a
+// service's idle time or life.
+void services_end_before_free();
 }  // namespace pcrc

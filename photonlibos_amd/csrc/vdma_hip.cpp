@@ -107,6 +107,7 @@ public:
         for (auto& kv : registered_)
             if (kv.second->host_pinned()) (void)hipHostUnregister(kv.second->address());
         registered_.clear();
+        pcrc::services_end_before_free();
         if (base_) (void)hipFree(base_);
         if (!name_.empty()) shm_unlink(name_.c_str());
     }

@@ -23,7 +23,10 @@ Phases are separated by IDLE_S seconds of idle GPU. One JSON line per phase.
    c3: CRC-32C on the same 4 GiB as 1 Mi x 4 KiB buffers; c3_64 / c2_64: CRC-64/ECMA on
    4 KiB / 64 KiB buffers with the generic batch kernel, c3_64full / c2_64full: with the
    full-row kernel, cross-buffer prefetch, 2 rows per step; c4: CRC-32C on 4 Ki x 1 MiB; readp: the
-   product's read-only row-pattern kernel, read_stream_kernel)
+   product's read-only row-pattern kernel, read_stream_kernel; crcsvc: the product kernel with a
+   resident small-buffer service beside it -- after each group of launches is queued, one routed
+   4 KiB call starts a service (1 s idle and life) that then idles, napping, beside the rest of
+   the group; the next group's first launch ends it)
 """
 import ctypes
 import json
@@ -165,6 +168,21 @@ def launch(kernel, k):
     assert rc == 0, rc
 
 
+small = torch.zeros(8192, dtype=torch.uint8, device="cuda")
+SVC = any(k.startswith("crcsvc") for k in KERNELS)
+if SVC:
+    ck.set_device_dispatch(True)
+    ck.set_small_service(1000000)
+    ck.set_small_service_life(1000000)
+
+
+def svc_kick(kernel):
+    """crcsvc: one routed call after the group is queued, so the service
+    launch is resident beside the group's remaining launches."""
+    if kernel == "crcsvc":
+        ck.crc32c_extend_at(small.data_ptr() + 1, 4096, 0)
+
+
 def clocks(k_count):
     """In-kernel clock (GHz) per launch of the window from the wave stamps."""
     res = []
@@ -196,7 +214,8 @@ def phase(kernel, label):
         ev[k][0].record(st)
         launch(kernel, k)
         ev[k][1].record(st)
-    torch.cuda.synchronize()
+    svc_kick(kernel)
+    st.synchronize()  # the launch stream only: a device-wide wait would wait out a live service
     e1, t1 = board.energy_uj(), time.perf_counter()
     ms = [round(a.elapsed_time(b), 4) for a, b in ev]
     clk = clocks(WINDOW) if (kernel in ("read", "rows") or STAMPS) else None
@@ -206,8 +225,9 @@ def phase(kernel, label):
     while time.perf_counter() - t2 < STEADY_S:
         for k in range(20):
             launch(kernel, k)
+        svc_kick(kernel)
         launches += 20
-        torch.cuda.synchronize()
+        st.synchronize()
     e3, t3 = board.energy_uj(), time.perf_counter()
     rows = smp.stop()
 
@@ -235,6 +255,10 @@ def phase(kernel, label):
                       **seg(e2, e3, t2, t3, launches)}}
     if clk:
         res["window"]["clock_ghz"] = clk
+    if SVC:
+        res["service_stats_served_starts_missed"] = ck.small_service_stats()
+        ck.set_small_service(0)  # ends a live service before the next phase
+        ck.set_small_service(1000000)
     if board.err:
         res["board_note"] = board.err
     print(json.dumps(res), flush=True)

@@ -476,6 +476,47 @@ def _graph_capture(torch, oracle):
             assert int(got[k]) == oracle.crc64ecma(host[off + 2:off + 2 + n], 11 + k), k
 
 
+def test_two_live_graphs_replay_concurrently(torch_dev, oracle):
+    """a captured multi-workgroup launch owns a reduce state through
+    a graph user object, handed back when the graph is destroyed; torch
+    destroys the hipGraph_t right after instantiation, so the executable graph
+    must keep its own reference. Two graphs stay alive -- the second captured
+    after the first's hipGraph_t is gone -- and replay at the same time on two
+    streams, many times, over spans that take many workgroups (small 128 KiB,
+    mid / long 1 MiB): a shared state would mix their tickets and slots and
+    give wrong CRCs."""
+    torch = torch_dev
+    bufs = [torch.empty(1 << 20, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for i, b in enumerate(bufs):
+        ck.fill_splitmix(b, b.numel(), b.numel(), 1, 0x6A0 + i)
+    torch.cuda.synchronize()
+    spans = ((3, 128 << 10), (3, (1 << 20) - 64), (1, 200000))
+    outs = [torch.zeros(len(spans), dtype=torch.int32, device="cuda") for _ in range(2)]
+    graphs = []
+    for i in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            st = torch.cuda.current_stream()
+            for k, (off, n) in enumerate(spans):
+                ck.extend_device(bufs[i].data_ptr() + off, n, 40 + k, outs[i][k:k + 1], stream=st)
+        graphs.append(g)
+    hosts = [b.cpu().numpy() for b in bufs]
+    want = [[oracle.crc32c(h[off:off + n], 40 + k) for k, (off, n) in enumerate(spans)] for h in hosts]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    for rep in range(150):
+        for i in range(2):
+            outs[i].zero_()
+        torch.cuda.synchronize()
+        for i in range(2):
+            with torch.cuda.stream(streams[i]):
+                graphs[i].replay()
+        torch.cuda.synchronize()
+        for i in range(2):
+            got = [int(x) for x in _u32(outs[i])]
+            assert got == want[i], (rep, i, got, want[i])
+
+
 def test_first_small_call_inside_capture(torch_dev):
     """the small kernels' table images are built lazily on
     a device's first small call; when that first call is made while the
