@@ -1942,7 +1942,7 @@ namespace {
 
 std::mutex g_dispatch_mu;
 std::atomic<int> g_dispatch_err{0};
-bool g_dispatch_on = false;
+std::atomic<bool> g_dispatch_on{false};  // written under g_dispatch_mu; read by heavy_mark
 uint32_t (*g_host_crc)(const uint8_t*, size_t, uint32_t) = nullptr;
 uint64_t (*g_host_crc64)(const uint8_t*, size_t, uint64_t) = nullptr;
 void (*g_host_series)(const uint8_t*, uint32_t, uint32_t, uint32_t*) = nullptr;
@@ -2539,8 +2539,9 @@ void svc_yield() {
 }
 
 // The ring of a device's last kHeavyEvents heavy launches (HeavyLaunch),
-// kept only once a service exists in the process (a process without routed
-// calls pays nothing). Launches captured into a graph are not marked.
+// kept only while device dispatch is on or once a service exists (a process
+// without routed calls pays nothing). Launches captured into a graph are not
+// marked.
 constexpr int kHeavyEvents = 8;
 struct HeavyRing {
     std::mutex mu;
@@ -2551,7 +2552,7 @@ struct HeavyRing {
 PerDevice<HeavyRing*> g_heavy;
 
 void heavy_mark(hipStream_t st) {
-    if (g_svc_made.load(std::memory_order_relaxed) == 0) return;
+    if (!g_dispatch_on.load(std::memory_order_relaxed) && g_svc_made.load(std::memory_order_relaxed) == 0) return;
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
