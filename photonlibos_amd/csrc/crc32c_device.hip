@@ -1852,9 +1852,11 @@ int extend_spans(const photon_crc_span* spans, int nspans, T seed, T* h_result, 
             return launch(sp.d_data, sp.nbytes, static_cast<T*>(outs[i]));
         },
         &issued);
-    // ...then collected (and every lease returned, even after a failure), each on its device.
+    // ...then collected (and every lease returned, even after a failure --
+    // a device that refuses the switch included: the later spans' leases are
+    // still returned on their own devices), each on its device.
     int first = 0;  // the first collection error; the loop goes on so that every lease is returned
-    const int set_rc = run_on_devices(
+    const int set_rc = run_on_every_device(
         rt, issued, [&](int i) { return spans[i].device; },
         [&](int i) {
             if (!outs[i]) return 0;
@@ -1865,8 +1867,7 @@ int extend_spans(const photon_crc_span* spans, int nspans, T seed, T* h_result, 
             const int frc = scratch_free(outs[i], nullptr);
             if (!first) first = frc;
             return 0;
-        },
-        nullptr);
+        });
     if (!rc) rc = first ? first : set_rc;
     if (rc) return rc;
     T acc = seed;

@@ -121,4 +121,23 @@ int run_on_devices(RT& rt, int n, Dev device, Body body, int* ran) {
     return rc;
 }
 
+// The same, but it never stops: body(i) runs for every i whose device could
+// be made current (a failed switch skips only that body), so a cleanup pass
+// still reaches every later index (extend_spans returns every scratch lease
+// on its own device even when one device refuses the switch).
+// Returns 0 or the first nonzero code, switch errors included.
+template <typename RT, typename Dev, typename Body>
+int run_on_every_device(RT& rt, int n, Dev device, Body body) {
+    int prev = -1;
+    if (int rc = rt.get(&prev)) return rc;
+    int first = 0;
+    for (int k = 0; k < n; ++k) {
+        int rc = rt.set(device(k));
+        if (!rc) rc = body(k);
+        if (rc && !first) first = rc;
+    }
+    (void)rt.set(prev);
+    return first;
+}
+
 }  // namespace pcrc

@@ -178,12 +178,57 @@ static void test_sequential() {
     CHECK(rc == -19 && seen.size() == 1 && t_cur == 3);
 }
 
+// extend_spans' collection pass (run_on_every_device): a device that refuses
+// the switch in the middle skips only its own body; every later index still
+// runs on its device, the first error is returned, the caller's device is
+// restored.
+struct FlakyRT : FakeRT {
+    int refuse = -1;  // a device id whose next switch fails once
+    int set(int d) {
+        if (d == refuse) {
+            refuse = -1;
+            return -5;  // -EIO
+        }
+        return FakeRT::set(d);
+    }
+};
+
+static void test_every_device() {
+    FlakyRT rt;
+    t_cur = 4;
+    const int devs[] = {0, 7, 2, 6, 5, 1};
+    std::vector<int> freed;
+    rt.refuse = 2;  // index 2's switch fails
+    int rc = run_on_every_device(
+        rt, 6, [&](int i) { return devs[i]; },
+        [&](int i) {
+            int cur = -1;
+            rt.get(&cur);
+            CHECK(cur == devs[i]);  // each lease returned on its own device
+            freed.push_back(i);
+            return 0;
+        });
+    CHECK(rc == -5 && freed == std::vector<int>({0, 1, 3, 4, 5}) && t_cur == 4);
+    // a failing body does not stop the pass either; the first code wins
+    freed.clear();
+    rc = run_on_every_device(
+        rt, 6, [&](int i) { return devs[i]; },
+        [&](int i) {
+            freed.push_back(i);
+            return i == 1 ? -22 : i == 4 ? -12 : 0;
+        });
+    CHECK(rc == -22 && freed.size() == 6 && t_cur == 4);
+    // all good: 0
+    CHECK(run_on_every_device(rt, 6, [&](int i) { return devs[i]; }, [](int) { return 0; }) == 0);
+}
+
 int main() {
     test_plan();
     for (int nd = 1; nd <= kDev; ++nd)
         for (uint64_t count : {1ull, 5ull, 8ull, 1000ull, 65537ull}) test_threaded(count, nd);
     test_threaded_failure();
     test_sequential();
+    test_every_device();
     if (g_fail) {
         fprintf(stderr, "multi_device_test: %d check(s) failed\n", g_fail);
         return 1;
