@@ -30,8 +30,7 @@ int photon_crc_set_batch_grid(int workgroups);
 /* Batch kernel variant (testing / tuning): -1 (default) = rows per step by
  * lane-group size (2 for 16-lane groups, else 4); 2, 4 or 8 = the generic
  * kernel with that many rows per step. (The fused and streaming kernels of
- * earlier rounds measured slower and now live only in the bench probes,
- * photonlibos_amd/csrc/stream_kernels.h.) */
+ * earlier rounds measured slower and were deleted in round 6.) */
 int photon_crc_set_generic_rows(int rows_per_step);
 
 /* Message batches (photon_crc32c_batch_msg[_n], the CheckedMessage batch),

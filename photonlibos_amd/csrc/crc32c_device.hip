@@ -28,8 +28,8 @@
 // bytes of the first aligned block are masked to 0 and the seed is XORed into
 // the first four data bytes (init-value linearity), so every load is an
 // aligned 16-byte load. Ragged tails (<16 B) are finished byte-serially.
-// (The streaming and fused variants that measured slower live in
-// stream_kernels.h, built only into the bench probes.)
+// (The streaming and fused variants of rounds 1-4 measured slower and were
+// deleted in round 6; DESIGN.md §4 keeps their numbers.)
 #include <hip/hip_runtime.h>
 
 #include <errno.h>

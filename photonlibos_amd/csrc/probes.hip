@@ -11,7 +11,6 @@
 #include "crc32c_kernels.h"
 #include "crc64_kernels.h"
 #include "long_plan.h"
-#include "stream_kernels.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
@@ -377,61 +376,6 @@ int probe_read_gridstride(const void* p, uint64_t nbytes, uint32_t* sink, int bl
         if (unroll == 4) GS(4, false); else if (unroll == 16) GS(16, false); else GS(8, false);
     }
 #undef GS
-    return hipGetLastError() == hipSuccess ? 0 : -5;
-}
-
-// The uniform CRC kernel (G=32, B=1, U=4, D=3) with parts of the arithmetic
-// removed (see crc32c_kernels.h ABL): which resource bounds the kernel?
-int probe_crc_ablate(const void* base, uint64_t nbytes, uint64_t count, uint32_t* out, int abl, int cus,
-                     void* stream) {
-    using namespace pcrc;
-    constexpr int G = 32;
-    LaneConsts kc;
-    kc.kshift = xpow(8ull * 16ull * G);
-    mul_basis(kc.kshift, kc.sbasis);
-    for (int k = 0; k < 6; ++k) mul_basis(xpow(128ull << k), kc.basis[k]);
-    UniformArgs a{static_cast<const uint8_t*>(base), nbytes, nbytes / (16ull * G), count, out};
-    const uint64_t waves = (count + 1) / 2;
-    uint64_t grid = (waves + 15) / 16;
-    if (grid > (uint64_t)cus) grid = cus;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-#define AB(X) hipLaunchKernelGGL((crc32c_uniform_kernel<G, 1, 4, 3, X>), dim3(grid), dim3(kBlock), 0, s, a, kc)
-    switch (abl) {
-        case 1: AB(1); break;
-        case 2: AB(2); break;
-        case 3: AB(3); break;
-        case 4: AB(4); break;
-        case 5: AB(5); break;
-        default: AB(0); break;
-    }
-#undef AB
-    return hipGetLastError() == hipSuccess ? 0 : -5;
-}
-
-// The CRC-64 streaming kernel (G=32, U=4, D=3) with parts of the arithmetic
-// removed: 1 no S lookups, 2 one D step per block, 4 no lookups (and sums).
-int probe_crc64_ablate(const void* base, uint64_t nbytes, uint64_t count, uint64_t* out, int abl, int cus,
-                       void* stream) {
-    using namespace pcrc;
-    constexpr int G = 32;
-    LaneConsts64 kc;
-    kc.kshift = xpow64(8ull * 16ull * G);
-    for (int i = 0; i < 64; ++i) kc.sbasis[i] = mulmod64(1ull << i, kc.kshift);
-    Uniform64Args a{static_cast<const uint8_t*>(base), nbytes, nbytes / (16ull * G), count, out, 0};
-    const uint64_t waves = (count + 1) / 2;
-    uint64_t grid = (waves + 15) / 16;
-    if (grid > (uint64_t)cus) grid = cus;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-#define AB64(X) hipLaunchKernelGGL((crc64_uniform_kernel<G, 4, 3, 1, 1, X>), dim3(grid), dim3(kBlock), 0, s, a, kc)
-    switch (abl) {
-        case 1: AB64(1); break;
-        case 2: AB64(2); break;
-        case 3: AB64(3); break;
-        case 4: AB64(4); break;
-        case 5: AB64(5); break;
-        default: AB64(0); break;
-    }
-#undef AB64
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

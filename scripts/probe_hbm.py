@@ -58,33 +58,7 @@ for k, ms in res.items():
     print(json.dumps({"probe": k, "ms": round(med, 4), "GBps": round(total / med / 1e6, 1),
                       "frac_of_8TBps": round(total / med / 1e6 / 8000, 4)}))
 
-# Ablations of the CRC kernel (G=32, B=1, U=4, D=3): 0 full, 1 no S lookups,
-# 2 one word step per block, 3 = 1+2, 4 no lookups, 5 = 1+4.
-P.probe_crc_ablate.argtypes = [vp, u64, u64, vp, ci, ci, vp]
-out = torch.zeros(count, dtype=torch.int32, device="cuda")
-abl = {f"crc ablate {a}": (lambda a=a: P.probe_crc_ablate(buf.data_ptr(), nbytes, count, out.data_ptr(), a, 256, s))
-       for a in range(6)}
-res = {k: [] for k in abl}
-for r in range(4):
-    for k, f in abl.items():
-        res[k].append(timed(f))
-for k, ms in res.items():
-    med = float(np.median(ms))
-    print(json.dumps({"probe": k, "ms": round(med, 4), "GBps": round(total / med / 1e6, 1),
-                      "frac_of_8TBps": round(total / med / 1e6 / 8000, 4)}))
-
-# Ablations of the CRC-64 streaming kernel (G=32, U=4, D=3): 0 full, 1 no S
-# lookups, 2 one D step per block, 3 = 1+2, 4 no lookups, 5 = 1+4.
-if "--crc64" in sys.argv or True:
-    P.probe_crc64_ablate.argtypes = [vp, u64, u64, vp, ci, ci, vp]
-    out64 = torch.zeros(count, dtype=torch.int64, device="cuda")
-    abl = {f"crc64 ablate {a}": (lambda a=a: P.probe_crc64_ablate(buf.data_ptr(), nbytes, count, out64.data_ptr(),
-                                                                   a, 256, s)) for a in range(6)}
-    res = {k: [] for k in abl}
-    for r in range(4):
-        for k, f in abl.items():
-            res[k].append(timed(f))
-    for k, ms in res.items():
-        med = float(np.median(ms))
-        print(json.dumps({"probe": k, "ms": round(med, 4), "GBps": round(total / med / 1e6, 1),
-                          "frac_of_8TBps": round(total / med / 1e6 / 8000, 4)}))
+# (The round-1 ablations of the retired streaming CRC kernels, probe_crc_ablate /
+# probe_crc64_ablate, were removed with those kernels in round 6; their numbers
+# stay in repo:profiles/r01_hbm_probes.jsonl and DESIGN.md §4 / §4.1. The
+# product kernels' ablations are PCRC_ABL / PCRC64_ABL builds, scripts/gpu.sh abn.)

@@ -40,7 +40,7 @@ MSG_MODES = [0, 1, 2]
 
 # Batch kernel variants: rows per step of the generic kernel (-1 = by
 # lane-group size, the product default). The fused and streaming kernels of
-# earlier rounds are bench-only probes now (stream_kernels.h).
+# earlier rounds measured slower and were deleted.
 VARIANTS = [-1, 2, 4, 8]
 
 
