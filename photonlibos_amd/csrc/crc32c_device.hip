@@ -518,11 +518,22 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     int dev = current_device(&cus);
     if (dev < 0) return dev;
     int g = choose_lanes(typical_len);
-    // 4-8 KiB CRC-64 buffers: 16 lanes (one-level finish + lane-parallel
-    // second level, init at the end): 80.7 vs 79.8 % and 79.2 vs 79.2 % on
-    // two boxes (repo:profiles/r04_ab_crc64_c3_lanes8_vs_16.jsonl,
-    // r04_ab_crc64_shift_init.jsonl)
-    if (!g_lanes_override.load(std::memory_order_relaxed) && typical_len >= 4096 && typical_len <= 8192) g = 16;
+    const uint32_t full = g_full64.load(std::memory_order_relaxed);
+    const int fu = (int)(full >> 4);
+    auto full_rows = [&](int gg) {  // the full-row kernel's mode for lane groups of gg, 0 = not eligible
+        const int fx = (full & 15u) == 3u ? (gg <= 16 ? 2 : 0) : (int)(full & 15u);
+        return fx && !a.iov && a.shift_init && a.nbytes % (2ull * 16ull * (uint64_t)gg * (uint64_t)fu) == 0 ? fx : 0;
+    };
+    // 4-8 KiB CRC-64 buffers: the full-row kernel takes 8 lanes (32-64 rows
+    // per lane, so the per-buffer finish -- 16 nibble lookups per lane -- is
+    // spread over twice the bytes of 16 lanes): at the board's power limit
+    // 4 KiB 0.802 vs 0.796 of 8 TB/s (0.2344 vs 0.2360 J/GiB), 8 KiB 0.817
+    // vs 0.784 (0.2297 vs 0.2404), bench C3 shape 0.795 vs 0.786
+    // (repo:profiles/r06c_power_crc64_lanes_g{16,8}.jsonl, r06c_ab_lanes_c3_crc64.jsonl).
+    // Other batches there keep 16 lanes (the generic kernel: 80.7 vs 79.8 %,
+    // repo:profiles/r04_ab_crc64_c3_lanes8_vs_16.jsonl).
+    if (!g_lanes_override.load(std::memory_order_relaxed) && typical_len >= 4096 && typical_len <= 8192)
+        g = full_rows(8) ? 8 : 16;
     const uint64_t gpw = 64 / g;
     const uint64_t waves = (a.count + gpw - 1) / gpw;
     uint64_t grid = (waves + kWaves - 1) / kWaves;
@@ -530,10 +541,7 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     const LaneConsts64& kc = lane_consts64(g);
     HeavyLaunch heavy(stream);
     // Whole-step uniform batches: the full-row kernel (crc64_kernels.h).
-    const uint32_t full = g_full64.load(std::memory_order_relaxed);
-    const int fu = (int)(full >> 4);
-    const int fx = (full & 15u) == 3u ? (g <= 16 ? 2 : 0) : (int)(full & 15u);
-    if (fx && !a.iov && a.shift_init && a.nbytes % (2ull * 16ull * (uint64_t)g * (uint64_t)fu) == 0) {
+    if (const int fx = full_rows(g)) {
 #define LF64(GG, UU)                                                                                          \
     do {                                                                                                      \
         if (fx == 2)                                                                                          \

@@ -133,12 +133,26 @@ __device__ __forceinline__ uint32_t rot32(uint32_t x, const LaneAddr& a) {
 // v_perm_b32 (result bytes {off.byte0, xr.byte i, 0, 0}; selector 0..3 = the
 // second operand's bytes, 4..7 = the first's, 12 = 0x00); TOFF selects the
 // D (0) or S (kSOff) half of the row through the instruction's offset field.
+// Bench-only energy ablations of the CRC32C lookups (-DPCRC_ABL=bits; results
+// are then NOT CRCs): 1 = no LDS lookup (the v_perm'd address
+// itself enters the XOR tree), 2 = no address v_perm (a per-lane fixed
+// address made opaque to the compiler, still dependent on x, is read), 4 = no
+// table prologue in the batch kernel. 0 in the product.
+#ifndef PCRC_ABL
+#define PCRC_ABL 0
+#endif
 #if PCRC_LANE_SEL
 // Per-lane selectors: the v_perm of lookup i takes byte (i+q)%4 of the
 // UNROTATED word (the selector is a per-lane register), so no v_alignbit per
 // table step; one VALU per lookup either way.
 template <int I, uint32_t TOFF>
 __device__ __forceinline__ uint32_t look(const uint32_t* lds, uint32_t x, const LaneAddr& a) {
+    if constexpr ((PCRC_ABL & 2) != 0) {
+        uint32_t ad = a.off[I];
+        asm volatile("" : "+v"(ad) : "v"(x));  // no instruction; keeps the read per step and its x dependence
+        return lds_word(lds, ad + TOFF);
+    }
+    if constexpr ((PCRC_ABL & 1) != 0) return __builtin_amdgcn_perm(x, a.off[I], a.sel[I]) + TOFF;
     return lds_word(lds, __builtin_amdgcn_perm(x, a.off[I], a.sel[I]) + TOFF);
 }
 #else
@@ -939,7 +953,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         const uint32_t* img = g_table_image[table_slot<G>()];
         const uint32_t tid = threadIdx.x;
         u32x4 tv[kPer];
-        if (img) {
+        if (img && !(PCRC_ABL & 4)) {
 #pragma unroll
             for (uint32_t i = 0; i < kPer; ++i) {
                 const uint32_t j = i * kBlock + tid;
@@ -954,7 +968,9 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         BufGeo g = buf_geo<G>(p, n, gl);
         BufPre<U, PCRC_BATCH_LEAD> pre;
         if (wv * GPW < args.count) buf_preload<G, U, PCRC_BATCH_LEAD>(g, gl, pre);  // wave-uniform
-        if (img) {
+        if (PCRC_ABL & 4) {
+            lds_barrier();
+        } else if (img) {
 #pragma unroll
             for (uint32_t i = 0; i < kPer; ++i) {
                 const uint32_t j = i * kBlock + tid;

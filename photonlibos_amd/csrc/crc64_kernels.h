@@ -616,11 +616,12 @@ __global__ __launch_bounds__(kBlock) void crc64_full_kernel(Batch64Args args, La
         }
         // Q * x^(64 + 128 d) (Q -> P and the lane's shift to the end), XOR over the group.
         uint64_t reg;
-        if constexpr (G == 16 && PCRC64_FIN16) {
+        if constexpr (G == 16 && PCRC64_FIN16 && !(PCRC64_ABL & 6)) {
             reg = finish_xor16(pc, d, lds, gl, lane);
         } else {
-            const uint64_t f = finish64<G>(pc, d, lds, lane);
-            reg = ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
+            const uint64_t f = (PCRC64_ABL & 2) ? u64of(pc) : finish64<G>(pc, d, lds, lane);
+            reg = (PCRC64_ABL & 4) ? f
+                                   : ((uint64_t)group_xor<G>((uint32_t)(f >> 32)) << 32) | group_xor<G>((uint32_t)f);
         }
         const uint64_t bi = wv * GPW + grp;
         if (gl == 0 && bi < args.count) args.out[bi] = ~(reg ^ args.init_shift);  // crc.cpp:119-122

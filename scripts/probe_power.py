@@ -18,10 +18,10 @@ Energy comes from amdsmi_get_energy_count (accumulator x resolution, uJ);
 without amdsmi the power sampler's mean power x time is used instead.
 Phases are separated by IDLE_S seconds of idle GPU. One JSON line per phase.
 
-  KERNELS=crc,rows,read,crc  STEADY_S=3  IDLE_S=2  python scripts/probe_power.py [--stamps]
+  KERNELS=crc,rows,read,crc  STEADY_S=3  IDLE_S=2  [LANES=G]  python scripts/probe_power.py [--stamps]
   (crc@W: the product kernel on a grid capped at W workgroups, photon_crc_set_batch_grid;
    c3: CRC-32C on the same 4 GiB as 1 Mi x 4 KiB buffers; c3_64 / c2_64: CRC-64/ECMA on
-   4 KiB / 64 KiB buffers with the generic batch kernel, c3_64full / c2_64full: with the
+   4 KiB / 64 KiB buffers with the generic batch kernel (c5_64: 8 KiB), c3_64full / c2_64full: with the
    full-row kernel, cross-buffer prefetch, 2 rows per step; c4: CRC-32C on 4 Ki x 1 MiB; readp: the
    product's read-only row-pattern kernel, read_stream_kernel; crcsvc: the product kernel with a
    resident small-buffer service beside it -- after each group of launches is queued, one routed
@@ -157,9 +157,9 @@ def launch(kernel, k):
     elif kernel == "readp":  # the product's read-only reference kernel (read_stream_kernel, row pattern)
         ck.read_stream(buf, nbytes, sink, sink.numel(), stream=st)
         rc = 0
-    elif kernel.startswith("c3_64") or kernel.startswith("c2_64"):
+    elif kernel[:5] in ("c3_64", "c5_64", "c2_64"):  # c5_64: 8 KiB buffers
         ck.set_full_rows64(2 if kernel.endswith("full") else 0, 2)
-        b = 4096 if kernel.startswith("c3") else 65536
+        b = {"c3": 4096, "c5": 8192, "c2": 65536}[kernel[:2]]
         ck.batch64_strided(buf, b, b, nbytes // b, out64, stream=st)
         rc = 0
     else:  # crc or crc@<workgroups>: the product kernel (on a capped grid)
@@ -168,6 +168,7 @@ def launch(kernel, k):
     assert rc == 0, rc
 
 
+ck.set_lanes_per_buffer(int(os.environ.get("LANES", "0")))  # LANES=8: lane groups of 8 for every batch phase
 small = torch.zeros(8192, dtype=torch.uint8, device="cuda")
 SVC = any(k.startswith("crcsvc") for k in KERNELS)
 if SVC:

@@ -50,9 +50,12 @@ def timed(fn):
 def make(v, lanes):
     if v == "read":
         return lambda: ck.read_stream(buf, total, sink, sink.numel(), stream=stream)
-    if v == "g64":
+    if v.startswith("g64"):  # g64[:MODE:ROWS]: CRC-64, full-row mode and rows per step (photon_crc64_set_full_rows)
+        mode, rows = (int(x) for x in v.split(":")[1:3]) if ":" in v else (3, 2)
+
         def f64():
             ck.set_lanes_per_buffer(lanes)
+            ck.set_full_rows64(mode, rows)
             ck.batch64_strided(buf, nbytes, nbytes, count, out64, stream=stream)
         return f64
 
@@ -74,7 +77,7 @@ for r in range(args.rounds):
         res[f"{v}/G{l}"].append(ms)
         if v != "read":
             torch.cuda.synchronize()
-            is64 = v == "g64"
+            is64 = v.startswith("g64")
             o = (out64 if is64 else out).cpu().numpy().copy()
             key = "64" if is64 else "32"
             if key not in refs:
@@ -82,6 +85,7 @@ for r in range(args.rounds):
             assert np.array_equal(o, refs[key]), f"variant {v}/G{l} disagrees"
 ck.set_generic_rows(-1)
 ck.set_lanes_per_buffer(0)
+ck.set_full_rows64(3, 2)
 rows = []
 for k, ms in res.items():
     med, best = float(np.median(ms)), float(np.min(ms))

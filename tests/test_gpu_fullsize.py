@@ -78,15 +78,16 @@ def test_full_strided_every_crc(torch_dev, oracle, cfg):
 
 def test_full_c3_crc64_every_crc(torch_dev, oracle):
     # CRC-64/ECMA (row f2) on the C3 shape at full size: the product's
-    # 16-lane path (crc64_batch_kernel<16>, 4-8 KiB buffers) and the 8-lane
-    # one (lanes override), every CRC of both against the oracle.
+    # path (crc64_full_kernel<8,2,true> since round 6: 4-8 KiB uniform
+    # batches take 8 lanes) and the 16-lane one (lanes override; the
+    # default before round 6), every CRC of both against the oracle.
     torch = torch_dev
     nbytes, count = 4096, 1 << 20
     d = torch.empty(nbytes * count, dtype=torch.uint8, device="cuda")
     ck.fill_splitmix(d, nbytes, nbytes, count, SEED_BASE)
     want = oracle.crc64ecma_strided(d.cpu().numpy(), nbytes, nbytes, count)
     assert ck.lanes_for(nbytes) in (8, 16)
-    for lanes in (0, 8):
+    for lanes in (0, 16):
         ck.set_lanes_per_buffer(lanes)
         try:
             out = torch.zeros(count, dtype=torch.int64, device="cuda")
