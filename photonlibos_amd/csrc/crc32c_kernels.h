@@ -26,9 +26,19 @@
 // copied cur <- nxt on the loop edge (the default); 1 = the compiler's unroll
 // by two (no copies; the next step's loads issued before this step's land:
 // 8 rows in flight); 2 = two register sets by hand, the next step's loads
-// issued only once this step's have landed (4 rows in flight, no copies).
+// issued only once this step's have landed (4 rows in flight, no copies);
+// 3 = one register set reloaded row by row as each row is consumed.
 #ifndef PCRC_BODY
 #define PCRC_BODY 0
+#endif
+// With PCRC_BODY 0: steps of U >= 4 rows take variant 3's rolling reload
+// (the C2 / C4 batch kernels and the long kernels; no v_mov copies on the
+// loop edge): C2 in the driver's 5 + 20 launches 0.834 vs 0.826 frac_kernel
+// over 5 alternating rounds, C4 +0.25 points, 1 GiB long kernel 0.170 vs
+// 0.174 ms; at U = 2 (C3, messages) it cost 2 points, so U < 4 keeps the
+// copies (repo:profiles/r06d_ab_roll_*.jsonl). A/B builds: -DPCRC_BODY_ROLL=0.
+#ifndef PCRC_BODY_ROLL
+#define PCRC_BODY_ROLL 1
 #endif
 // Aligned strided batches take the seed at the end (BatchArgs::shift_init;
 // A/B builds: -DPCRC_SHIFT_INIT=0).
@@ -683,6 +693,27 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
             row += U;
         }
 #else
+        if constexpr (PCRC_BODY == 3 || (PCRC_BODY == 0 && U >= 4 && PCRC_BODY_ROLL)) {
+        // Rolling reload: row u of the next step is loaded into cur[u] right
+        // after row u's lagged block is taken, so the old and new values never
+        // live together and the loop edge needs no copies; U rows stay in
+        // flight, each issued a little later than at the top of the step.
+        uint4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = pre.cur[u];
+        for (; row + 2 * U <= g.full; row += U) {
+            uint32_t c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                c[u] = lag16(lds, cur[u], la);
+                cur[u] = load16(lp + (row + U + u) * (16 * G));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) pc = sstep(lds, pc, la, c[u]);
+        }
+        pc = lag_column_step<U>(lds, pc, cur, la);
+        row += U;
+        } else {
         uint4 cur[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = pre.cur[u];
@@ -697,6 +728,7 @@ __device__ __forceinline__ uint32_t buf_body(const uint32_t* lds, const BufGeo& 
         }
         pc = lag_column_step<U>(lds, pc, cur, la);
         row += U;
+        }
 #endif
     }
     const bool part = g.full >= 1 && g.full < g.rows && g.full * G + gl < g.nb;

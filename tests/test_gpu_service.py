@@ -348,6 +348,8 @@ def test_service_beside_batch_kernels(torch_dev, oracle):
         # at once, while they run: the launch path (deferred), not a service
         assert ck.crc32c_extend_at(small.data_ptr() + 3, 5000, it) == oracle.crc32c(host[3:5003], it)
         calls += 1
+        if it % 2:
+            side.synchronize()  # odd rounds: no batch in flight any more, the calls below are served
         for j in range(5):
             host = rng.integers(0, 256, small.numel(), dtype=np.uint8)
             small.copy_(torch.from_numpy(host))
@@ -365,7 +367,10 @@ def test_service_beside_batch_kernels(torch_dev, oracle):
     served, starts, missed = (b - a for a, b in zip(st0, st1))
     deferred = d1 - d0
     assert served + starts + missed + deferred >= calls, (served, starts, missed, deferred, calls)
-    assert deferred >= 20 and served >= 40, (served, starts, missed, deferred, calls)
+    # the first call of every round finds its batches in flight; in the odd
+    # rounds the other five find none and are served (the first of them
+    # starting a launch); in the even rounds they may go either way
+    assert deferred >= 20 and served >= 80, (served, starts, missed, deferred, calls)
 
 
 def test_service_does_not_hold_other_streams(torch_dev, oracle):
