@@ -147,7 +147,8 @@ __device__ __forceinline__ uint32_t rot32(uint32_t x, const LaneAddr& a) {
 // are then NOT CRCs): 1 = no LDS lookup (the v_perm'd address
 // itself enters the XOR tree), 2 = no address v_perm (a per-lane fixed
 // address made opaque to the compiler, still dependent on x, is read), 4 = no
-// table prologue in the batch kernel. 0 in the product.
+// table prologue in the batch kernel, 8 = no segment-CRC stores in the
+// message kernel, 16 = no fold there (acc = c). 0 in the product.
 #ifndef PCRC_ABL
 #define PCRC_ABL 0
 #endif
@@ -558,6 +559,7 @@ __device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
     return k;
 }
 
+
 // -------------------------------------------------------------- generic path
 // Any pointer, any length, any seed; one group of G lanes per buffer.
 // U rows per step per lane, the next U rows' loads in flight. A buffer runs in
@@ -897,7 +899,10 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                 // issued (its DPP reduction and select-XORs then overlap them
                 // instead of delaying them).
                 auto fold = [&](uint32_t c, uint64_t n) {
-                    if constexpr (G >= 8) {
+                    if constexpr ((PCRC_ABL & 16) != 0) {
+                        acc ^= c;
+                        (void)n;
+                    } else if constexpr (G >= 8) {
                         if (n != klen) {
                             const uint32_t kn = xpow8_tab(n, pt);
 #pragma unroll
@@ -948,7 +953,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                         const uint64_t first = sg - j;
                         // Held back, two per lane, and written when a third
                         // comes or the wave ends (see HeldStores above).
-                        if (gl <= j) seg_held.put(args.out + first + gl, pend);
+                        if (gl <= j && !(PCRC_ABL & 8)) seg_held.put(args.out + first + gl, pend);
                     }
                     cprev = c;
                     nprev = n;
