@@ -99,6 +99,7 @@ def parse(argv=None):
                     help="one long device buffer at base+1 (1 GiB rate, 128 KiB latency, routed drop-in cost)")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per buffer override (0 = auto)")
     ap.add_argument("--msg-rows", type=int, default=0, help="message kernel rows per step (tuning; 0 = default)")
+    ap.add_argument("--rows", type=int, default=0, help="batch kernel rows per step (tuning; 0 = by lane count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-live-pmc", action="store_true",
@@ -964,6 +965,8 @@ def main(argv=None):
     ck.set_lanes_per_buffer(args.lanes)
     if args.msg_rows:
         ck.set_msg_rows(args.msg_rows)
+    if args.rows:
+        ck.set_generic_rows(args.rows)
     stream = torch.cuda.current_stream()
     if args.h2d or args.rpc_batch or args.rpc_latency or args.file_records or args.extend:
         if rank == 0:

@@ -24,6 +24,14 @@
 #ifndef PCRC64_ABL
 #define PCRC64_ABL 0
 #endif
+// The generic batch kernel's row loop: 1 = reload each row's registers as it
+// is consumed (no copies on the loop edge; C2 shape 0.850 vs 0.848
+// frac_kernel over 3 alternating rounds, steady 0.8516 vs 0.8495 at the
+// same J/GiB, repo:profiles/r06f_ab_roll64_c2.jsonl, r06f_power_roll64_*.jsonl),
+// 0 = the next step into a second set and copied back (A/B builds).
+#ifndef PCRC64_ROLL
+#define PCRC64_ROLL 1
+#endif
 
 namespace pcrc {
 
@@ -435,12 +443,25 @@ __device__ __forceinline__ uint64_t buffer_reg64(const uint32_t* lds, const uint
         };
         if (steps) {
             for (; row + 2 * U <= full; row += U) {
-                uint4 nxt[U];
+                if constexpr (PCRC64_ROLL) {
+                    // each row's registers reloaded as soon as its lagged
+                    // block is taken: no copies on the loop edge
+                    uint2 c[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
-                column_step(cur);
+                    for (int u = 0; u < U; ++u) {
+                        c[u] = lag16_64(lds, cur[u], la);
+                        cur[u] = load16(lp + (row + U + u) * (16 * G));
+                    }
 #pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+                    for (int u = 0; u < U; ++u) pc = sstep64(lds, pc, la, c[u]);
+                } else {
+                    uint4 nxt[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) nxt[u] = load16(lp + (row + U + u) * (16 * G));
+                    column_step(cur);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+                }
             }
             column_step(cur);
         }
