@@ -7,8 +7,10 @@ beside CRC32C and CRC-64 batch launches on another stream (the CRC-64 ones
 end the services), with random idle gaps around the services' 200 us idle
 time (their end / restart races). Every routed result is checked against the
 host engine on a host copy of the same bytes; the batches' first and last
-CRCs too. One JSON line at the end.
-Usage: python scripts/soak_service.py [--seconds 60] [--threads 1]"""
+CRCs too. --flip: a further thread flips the service's doorbell (BAR /
+pinned), its life (100 us .. 5 ms) and turns it off and on, every 2-50 ms,
+while the calls run. One JSON line at the end.
+Usage: python scripts/soak_service.py [--seconds 60] [--threads 1] [--flip]"""
 import argparse
 import json
 import os
@@ -28,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--flip", action="store_true")
     args = ap.parse_args()
     ck.set_device_dispatch(True)
     nb, count = 64 << 10, 1024
@@ -101,14 +104,40 @@ def main():
                 stats["bad_batches"] += 0 if ok else 1
             time.sleep(rng.choice([0, 1e-4, 1e-3, 5e-3]))
 
+    flips = [0]
+
+    def flipper():
+        rng = random.Random(11)
+        while time.perf_counter() < stop:
+            what = rng.randrange(4)
+            if what == 0:
+                ck.set_service_doorbell(rng.randrange(2) == 1)
+            elif what == 1:
+                ck.set_small_service_life(rng.choice([100, 500, 2000, 5000]))
+            elif what == 2:
+                ck.set_small_service(0)
+                ck.set_small_service(200)
+            else:
+                t0 = time.perf_counter()
+                torch.cuda.synchronize()  # a device-wide wait beside the routed calls
+                with lock:
+                    stats["sync_max_ms"] = max(stats.get("sync_max_ms", 0.0), (time.perf_counter() - t0) * 1e3)
+            flips[0] += 1
+            time.sleep(rng.choice([2e-3, 10e-3, 50e-3]))
+        ck.set_service_doorbell(True)
+        ck.set_small_service_life(2000)
+
     th = [threading.Thread(target=worker, args=(t,)) for t in range(args.threads)] + [threading.Thread(target=batches)]
+    if args.flip:
+        th.append(threading.Thread(target=flipper))
     for x in th:
         x.start()
     for x in th:
         x.join()
     served, starts, missed = ck.small_service_stats()
-    stats.update({"served": served, "starts": starts, "missed": missed, "fallbacks": ck.dispatch_fallbacks(),
-                  "seconds": args.seconds, "threads": args.threads})
+    stats.update({"served": served, "starts": starts, "missed": missed, "deferred": ck.small_service_deferred(),
+                  "fallbacks": ck.dispatch_fallbacks(), "seconds": args.seconds, "threads": args.threads,
+                  "flips": flips[0]})
     print(json.dumps(stats), flush=True)
     ck.set_device_dispatch(False)
     sys.exit(0 if stats["bad"] == 0 and stats["bad_batches"] == 0 and stats["fallbacks"] == 0 else 1)

@@ -108,6 +108,15 @@ def test_argument_validation():
     assert lib().photon_crc_set_mid_kernel(1) == 0
     assert lib().photon_crc_set_small_service(-1) == -22
     assert lib().photon_crc_set_small_service(2000000) == -22
+    # round 6: the service's life, its doorbell, the deferred count
+    assert lib().photon_crc_set_small_service_life(99) == -22
+    assert lib().photon_crc_set_small_service_life(1000001) == -22
+    assert lib().photon_crc_set_small_service_life(2000) == 0
+    assert lib().photon_crc_set_service_doorbell(2) == -22
+    assert lib().photon_crc_set_service_doorbell(0) == 0
+    assert lib().photon_crc_set_service_doorbell(1) == 0
+    assert lib().photon_crc_small_service_doorbell(5) == -22
+    assert lib().photon_crc_small_service_deferred() >= 0
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
