@@ -85,8 +85,8 @@ int photon_crc_set_routed_wait(int spin_us, int sleep_ahead);
  * that polls a request doorbell (device memory the host writes through the
  * PCIe BAR; pinned memory without a large BAR), so a call costs no kernel
  * launch and no table load; the launch ends after idle_us without a request
- * (and after 100 ms in any case; the next call starts a new one and is its
- * first request). Default 200 (or the environment variable
+ * (and after its life, photon_crc_set_small_service_life, 2 ms by default,
+ * in any case; the next call starts a new one and is its first request). Default 200 (or the environment variable
  * PHOTON_CRC_SMALL_SERVICE at load); 0 = off, a launch per call; turning it
  * off ends running launches. crc64ecma_extend has a service of its own (34
  * KiB of LDS per workgroup). Every batch, message or long launch of this

@@ -551,6 +551,18 @@ struct PowTable {
     uint32_t x8pow2[64];  // x^(8 * 2^i) mod P
 };
 
+// (a * b) mod P with the 32 steps as a loop (code size, not speed: for the
+// message fold's once-per-wave basis rebuild).
+__device__ __forceinline__ uint32_t mulmod_rolled(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll 1
+    for (int i = 0; i < 32; ++i, b >>= 1) r = (r >> 1) ^ ((0u - (r & 1u)) & kPoly) ^ ((0u - (b & 1u)) & a);
+    return r;
+}
+#ifndef PCRC_FOLD_COMPACT
+#define PCRC_FOLD_COMPACT 1  // A/B builds: 0 = the unrolled basis rebuild
+#endif
+
 // x^(8n) mod P: product of the x^(8*2^i) entries over the set bits of n.
 __device__ __forceinline__ uint32_t xpow8_tab(uint64_t n, const PowTable& t) {
     uint32_t k = kOne;
@@ -904,12 +916,34 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                         (void)n;
                     } else if constexpr (G >= 8) {
                         if (n != klen) {
+#if PCRC_FOLD_COMPACT
+                            // Rolled loops (runs once per wave for equal
+                            // segments; unrolled, its 4 + log2(n) 32-step
+                            // multiplies were 1,800 instructions inside the
+                            // segment loop). K = x^(8n); bit b's image is
+                            // K * x^(31-b): a chain of single x-steps.
+                            uint32_t r = kOne;
+                            uint64_t m = n;
+#pragma unroll 1
+                            for (int i = 0; m; ++i, m >>= 1)
+                                if (m & 1) r = mulmod_rolled(r, pt.x8pow2[i]);
+#pragma unroll
+                            for (int w = 0; w < kFoldW; ++w) kb[w] = 0u;
+#pragma unroll 1
+                            for (uint32_t j = 0; j < 32; ++j) {  // r = K * x^j, bit 31 - j
+#pragma unroll
+                                for (int w = 0; w < kFoldW; ++w)
+                                    kb[w] = gl * kFoldW + w == 31u - j ? r : kb[w];
+                                r = (r >> 1) ^ ((0u - (r & 1u)) & kPoly);
+                            }
+#else
                             const uint32_t kn = xpow8_tab(n, pt);
 #pragma unroll
                             for (int w = 0; w < kFoldW; ++w) {
                                 const uint32_t bit = gl * kFoldW + w;
                                 kb[w] = bit < 32 ? mulmod(1u << bit, kn) : 0u;
                             }
+#endif
                             klen = n;
                         }
                         uint32_t part = 0;
