@@ -559,8 +559,11 @@ __device__ __forceinline__ uint32_t mulmod_rolled(uint32_t a, uint32_t b) {
     for (int i = 0; i < 32; ++i, b >>= 1) r = (r >> 1) ^ ((0u - (r & 1u)) & kPoly) ^ ((0u - (b & 1u)) & a);
     return r;
 }
+// The message fold's basis rebuild as rolled loops: C5 0.853 vs 0.852 steady
+// in 3 of 3 alternating rounds, 119 -> 107 VGPRs, 2,860 -> 1,285 instructions
+// (repo:profiles/r06h_ab_c5_fold_compact.jsonl). A/B builds: 0 = unrolled.
 #ifndef PCRC_FOLD_COMPACT
-#define PCRC_FOLD_COMPACT 1  // A/B builds: 0 = the unrolled basis rebuild
+#define PCRC_FOLD_COMPACT 1
 #endif
 
 // x^(8n) mod P: product of the x^(8*2^i) entries over the set bits of n.
