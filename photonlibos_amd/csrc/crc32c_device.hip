@@ -2565,7 +2565,10 @@ void heavy_mark(hipStream_t st) {
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();  // never left for the caller's next launch check
+        return;
+    }
     HeavyRing* r = nullptr;
     if (g_heavy.get(dev, &r, [](int, HeavyRing*& slot) {
             auto* h = new HeavyRing;
@@ -2579,6 +2582,7 @@ void heavy_mark(hipStream_t st) {
                 for (hipEvent_t ev : h->ev)
                     if (ev) (void)hipEventDestroy(ev);
                 delete h;
+                (void)hipGetLastError();
                 return -EIO;
             }
             slot = h;
@@ -2588,6 +2592,7 @@ void heavy_mark(hipStream_t st) {
     std::lock_guard<std::mutex> lk(r->mu);
     const uint32_t i = r->next++ % kHeavyEvents;
     r->pending[i] = hipEventRecord(r->ev[i], st) == hipSuccess;
+    if (!r->pending[i]) (void)hipGetLastError();
 }
 
 // Is a heavy launch marked on `dev` still queued or running?
