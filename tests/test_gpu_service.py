@@ -409,12 +409,13 @@ def test_service_does_not_hold_other_streams(torch_dev, oracle):
     assert st1[0] - st0[0] >= 12, (st0, st1)
 
 
-def test_process_exit_with_live_service(torch_dev):
+def test_process_exit_with_live_service(torch_dev, _service):
     """A process that exits while a service launch is resident (1 s idle
     time) stops it at exit without any HIP call (rocprofv3's exit hooks run
     before the library's: a HIP call there aborted the process under the
     profiler) and waits for every workgroup's exit word: the child exits 0
-    well inside the idle time."""
+    well inside the idle time. The pinned case selects its doorbell with
+    PHOTON_CRC_SVC_DOORBELL=host at load."""
     import os
     import subprocess
     import sys
@@ -427,15 +428,21 @@ d = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
 torch.cuda.synchronize()
 ck.set_device_dispatch(True)
 ck.set_small_service(1000000)
+ck.set_small_service_life(1000000)  # still resident when the process exits
 for _ in range(3):
     assert ck.crc32c_extend_at(d.data_ptr() + 1, 100000, 0) == ck.crc32c_extend(bytes(100000), 0)
     ck.crc64ecma_extend_at(d.data_ptr() + 1, 5000, 0)
 assert ck.small_service_stats()[0] >= 2
+assert ck.small_service_doorbell(0) == %r, ck.small_service_doorbell(0)
 print("ok", flush=True)
 t = time.perf_counter()
-""" % (repo,)
+""" % (repo, _service)
+    env = dict(os.environ)
+    env.pop("PHOTON_CRC_SVC_DOORBELL", None)
+    if _service == "pinned":  # the environment switch at load (tuning.h)
+        env["PHOTON_CRC_SVC_DOORBELL"] = "host"
     t0 = time.perf_counter()
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=repo)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=repo, env=env)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     assert time.perf_counter() - t0 < 60
 
