@@ -2528,10 +2528,10 @@ void services_end_on_impl(int dev) {
     }
 }
 
-// Every batch / message / mid / long launch ends the services first (VERDICT
-// r5 #2): deciding co-residency by LDS alone ignored VGPRs and wave
-// slots, and a resident launch beside a streaming kernel on a power-bound
-// chip is not free. A routed call after the launch starts a new service.
+// Every batch / message / long launch ends the services first (HeavyLaunch;
+// VERDICT r5 #2): deciding co-residency by LDS alone ignored VGPRs
+// and wave slots. A routed call starts a new service once the launch has
+// finished (heavy_in_flight); until then it takes the launch path.
 void svc_yield() {
     if (g_svc_live.load(std::memory_order_relaxed) == 0) return;
     int dev = -1;
