@@ -66,8 +66,9 @@ int photon_crc_set_long_shape(int lanes, int rounds);
  * 1 = the full-row kernel (wave-uniform loop, two register sets), 2 = the
  * same with the next buffer's first rows issued before the finish, 3 = the
  * default: mode 2 for buffers that take lane groups of up to 16 lanes (up to
- * 8 KiB), the generic kernel above; rows_per_step 2 or 4 (default 2).
- * DESIGN.md §4.1 has the measurements. */
+ * 32 KiB at 8 lanes), the generic kernel above, with 4 rows per step for
+ * buffers of 8 KiB and more and 2 below (rows_per_step is then ignored);
+ * modes 0-2 take rows_per_step 2 or 4. DESIGN.md §4.1 has the measurements. */
 int photon_crc64_set_full_rows(int mode, int rows_per_step);
 
 /* Routed drop-in calls (photon_crc_set_device_dispatch) collect their result

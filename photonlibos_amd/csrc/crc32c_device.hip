@@ -519,7 +519,10 @@ int launch_batch64(const Batch64Args& a, uint64_t typical_len, hipStream_t strea
     if (dev < 0) return dev;
     int g = choose_lanes(typical_len);
     const uint32_t full = g_full64.load(std::memory_order_relaxed);
-    const int fu = (int)(full >> 4);
+    // rows per step: automatic mode 4 rows for buffers of 8 KiB and more (8
+    // KiB: 0.832 vs 0.823 at the power limit), 2 below (4 KiB: 0.809 vs 0.804;
+    // repo:profiles/r06n_power_crc64_rows_*.jsonl); else the knob's
+    const int fu = (full & 15u) == 3u ? (typical_len >= 8192 ? 4 : 2) : (int)(full >> 4);
     auto full_rows = [&](int gg) {  // the full-row kernel's mode for lane groups of gg, 0 = not eligible
         const int fx = (full & 15u) == 3u ? (gg <= 16 ? 2 : 0) : (int)(full & 15u);
         return fx && !a.iov && a.shift_init && a.nbytes % (2ull * 16ull * (uint64_t)gg * (uint64_t)fu) == 0 ? fx : 0;

@@ -18,7 +18,7 @@ Energy comes from amdsmi_get_energy_count (accumulator x resolution, uJ);
 without amdsmi the power sampler's mean power x time is used instead.
 Phases are separated by IDLE_S seconds of idle GPU. One JSON line per phase.
 
-  KERNELS=crc,rows,read,crc  STEADY_S=3  IDLE_S=2  [LANES=G]  python scripts/probe_power.py [--stamps]
+  KERNELS=crc,rows,read,crc  STEADY_S=3  IDLE_S=2  [LANES=G] [ROWS64=2|4]  python scripts/probe_power.py [--stamps]
   (crc@W: the product kernel on a grid capped at W workgroups, photon_crc_set_batch_grid;
    c3: CRC-32C on the same 4 GiB as 1 Mi x 4 KiB buffers; c3_64 / c2_64: CRC-64/ECMA on
    4 KiB / 64 KiB buffers with the generic batch kernel (c5_64: 8 KiB), c3_64full / c2_64full: with the
@@ -158,7 +158,12 @@ def launch(kernel, k):
         ck.read_stream(buf, nbytes, sink, sink.numel(), stream=st)
         rc = 0
     elif kernel[:5] in ("c3_64", "c5_64", "c2_64"):  # c5_64: 8 KiB buffers
-        ck.set_full_rows64(2 if kernel.endswith("full") else 0, 2)
+        if not kernel.endswith("full"):
+            ck.set_full_rows64(0, 2)
+        elif "ROWS64" in os.environ:  # the full-row kernel with that many rows per step
+            ck.set_full_rows64(2, int(os.environ["ROWS64"]))
+        else:  # the product's automatic choice
+            ck.set_full_rows64(3, 2)
         b = {"c3": 4096, "c5": 8192, "c2": 65536}[kernel[:2]]
         ck.batch64_strided(buf, b, b, nbytes // b, out64, stream=st)
         rc = 0

@@ -273,3 +273,24 @@ def test_full_row_kernel(torch_dev, oracle, mode, rows, g):
     finally:
         ck.set_full_rows64(3, 2)
         ck.set_lanes_per_buffer(0)
+
+
+@pytest.mark.parametrize("nbytes", [4096, 6144, 8192, 12288, 16384, 32768, 8192 + 512])
+def test_full_row_auto_shapes(torch_dev, oracle, nbytes):
+    # The automatic choice (round 6): uniform 4-8 KiB batches take 8 lanes,
+    # the full-row kernel 2 rows per step below 8 KiB and 4 from 8 KiB (a
+    # length that is not a multiple of the 4-row step pair -- 8.5 KiB --
+    # falls back to the generic kernel); every CRC against the oracle, with
+    # and without a seed, nothing written past the batch.
+    count = 1537
+    d = torch_dev.empty(nbytes * count + 64, dtype=torch_dev.uint8, device="cuda")
+    ck.fill_splitmix(d, nbytes, nbytes, count, 0x6A00 + nbytes)
+    host = d.cpu().numpy()
+    for seed in (0, 0x0123456789ABCDEF):
+        out = torch_dev.full((count + 1,), -1, dtype=torch_dev.int64, device="cuda")
+        ck.batch64_strided(d, nbytes, nbytes, count, out, seed=seed)
+        torch_dev.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64)
+        want = oracle.crc64ecma_strided(host, nbytes, nbytes, count, seed)
+        assert np.array_equal(got[:count], np.asarray(want, np.uint64)), (nbytes, seed)
+        assert int(got[count]) == 0xFFFFFFFFFFFFFFFF
