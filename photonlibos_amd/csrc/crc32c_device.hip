@@ -2553,7 +2553,9 @@ void svc_yield() {
 // The ring of a device's last kHeavyEvents heavy launches (HeavyLaunch),
 // kept only while device dispatch is on or once a service exists (a process
 // without routed calls pays nothing). Launches captured into a graph are not
-// marked.
+// marked, and a launch older than the last kHeavyEvents may still run
+// unmarked (many streams at once); a service started beside such a launch
+// only costs it CUs, for at most the service's life -- never a wrong CRC.
 constexpr int kHeavyEvents = 8;
 struct HeavyRing {
     std::mutex mu;
