@@ -22,6 +22,13 @@
 #ifndef PCRC_BATCH_LEAD
 #define PCRC_BATCH_LEAD false  // the same in the buffer batch (A/B: true)
 #endif
+// ... for the batch kernel's 2-row steps only (C3: 16 lanes, 16 rows per lane,
+// so row 15 was loaded on its own and waited for): 0.8578 vs 0.8567 in 3 of
+// 3 rounds; with 4-row steps (C2) it measured 0.2 points lower in the
+// driver's window, C4 +-0 (repo:profiles/r06p_ab_*_lead*.jsonl).
+#ifndef PCRC_BATCH_LEAD2
+#define PCRC_BATCH_LEAD2 true
+#endif
 // buf_body's row loop (A/B variants): 0 = one register set
 // copied cur <- nxt on the loop edge (the default); 1 = the compiler's unroll
 // by two (no copies; the next step's loads issued before this step's land:
@@ -846,6 +853,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
     // the copy as LDS-DMA -- no VGPRs held, a counted vmcnt before the barrier --
     // measured neutral, 4 rounds: repo:profiles/r05z_ab_dma_overlap_c3.jsonl.)
     constexpr bool kOverlap = MSG == 0 && G >= 32 && U <= 4 && PCRC_BATCH_OVERLAP && !PCRC_TABLE_BUILD;
+    constexpr bool kLead = PCRC_BATCH_LEAD || (U == 2 && PCRC_BATCH_LEAD2);  // lead rows + partial row preloaded
     if constexpr (!kOverlap) load_tables<G>(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
@@ -1040,8 +1048,8 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         uint32_t seed;
         item(wv, &p, &n, &seed);
         BufGeo g = buf_geo<G>(p, n, gl);
-        BufPre<U, PCRC_BATCH_LEAD> pre;
-        if (wv * GPW < args.count) buf_preload<G, U, PCRC_BATCH_LEAD>(g, gl, pre);  // wave-uniform
+        BufPre<U, kLead> pre;
+        if (wv * GPW < args.count) buf_preload<G, U, kLead>(g, gl, pre);  // wave-uniform
         if (PCRC_ABL & 4) {
             lds_barrier();
         } else if (img) {
@@ -1058,10 +1066,10 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
             if (!first) {
                 item(wv, &p, &n, &seed);
                 g = buf_geo<G>(p, n, gl);
-                buf_preload<G, U, PCRC_BATCH_LEAD>(g, gl, pre);
+                buf_preload<G, U, kLead>(g, gl, pre);
             }
             const uint32_t s = args.shift_init ? 0u : seed;
-            const uint32_t pc = buf_body<G, U, PCRC_BATCH_LEAD>(lds, g, pre, s, gl, la, !args.shift_init);
+            const uint32_t pc = buf_body<G, U, kLead>(lds, g, pre, s, gl, la, !args.shift_init);
             const uint32_t crc = buf_finish<G>(lds, g, pc, p, n, s, gl, la);
             const uint64_t bi = wv * GPW + grp;
             if (bi < args.count && gl == 0) args.out[bi] = crc ^ args.init_shift;  // init_shift is 0 unless shift_init
@@ -1075,7 +1083,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
         uint64_t n;
         uint32_t seed;
         item(wv, &p, &n, &seed);
-        const uint32_t crc = buffer_crc<G, U, PCRC_BATCH_LEAD>(lds, p, n, args.shift_init ? 0u : seed, gl, la,
+        const uint32_t crc = buffer_crc<G, U, kLead>(lds, p, n, args.shift_init ? 0u : seed, gl, la,
                                                                !args.shift_init);
         if (active && gl == 0) args.out[bi] = crc ^ args.init_shift;  // init_shift is 0 unless shift_init
     }
