@@ -29,6 +29,9 @@
 #ifndef PCRC_BATCH_LEAD2
 #define PCRC_BATCH_LEAD2 true
 #endif
+#ifndef PCRC_MSG_LEAD
+#define PCRC_MSG_LEAD 0  // A/B builds: 1 = lead rows preloaded in the message kernels (C5 -0.2, repo:profiles/r06p_ab_c5_msg_lead.jsonl)
+#endif
 // buf_body's row loop (A/B variants): 0 = one register set
 // copied cur <- nxt on the loop edge (the default); 1 = the compiler's unroll
 // by two (no copies; the next step's loads issued before this step's land:
@@ -854,6 +857,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
     // measured neutral, 4 rounds: repo:profiles/r05z_ab_dma_overlap_c3.jsonl.)
     constexpr bool kOverlap = MSG == 0 && G >= 32 && U <= 4 && PCRC_BATCH_OVERLAP && !PCRC_TABLE_BUILD;
     constexpr bool kLead = PCRC_BATCH_LEAD || (U == 2 && PCRC_BATCH_LEAD2);  // lead rows + partial row preloaded
+    constexpr bool kMsgLead = PCRC_MSG_LEAD != 0;  // the same in the message forms
     if constexpr (!kOverlap) load_tables<G>(lds, kc);
 
     constexpr int GPW = 64 / G;  // buffers per wavefront
@@ -902,7 +906,7 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                     // itself), so it has arrived when the next segment starts.
                     const photon_crc_iovec cur = nx;
                     nx = args.iov[sg + 1 < s1 ? sg + 1 : sg];
-                    acc = buffer_crc<G, U>(lds, static_cast<const uint8_t*>(cur.base), cur.len, acc, gl, la);
+                    acc = buffer_crc<G, U, kMsgLead>(lds, static_cast<const uint8_t*>(cur.base), cur.len, acc, gl, la);
                 }
             } else {
                 // Per-segment CRCs (seed 0) and the fold acc = acc * K ^ c,
@@ -987,10 +991,10 @@ __global__ __launch_bounds__(kBlock) void crc32c_batch_kernel(BatchArgs args, La
                     const uint8_t* p = static_cast<const uint8_t*>(cur.base);
                     const uint64_t n = cur.len;
                     const BufGeo g = buf_geo<G>(p, n, gl);
-                    BufPre<U> pre;
-                    buf_preload<G, U>(g, gl, pre);
+                    BufPre<U, kMsgLead> pre;
+                    buf_preload<G, U, kMsgLead>(g, gl, pre);
                     if (have) fold(cprev, nprev);
-                    const uint32_t pc = buf_body<G, U>(lds, g, pre, 0u, gl, la);
+                    const uint32_t pc = buf_body<G, U, kMsgLead>(lds, g, pre, 0u, gl, la);
                     const uint32_t c = buf_finish<G>(lds, g, pc, p, n, 0u, gl, la);
                     const uint32_t j = (uint32_t)((sg - s0) & (G - 1));
                     if (gl == j) pend = c;
