@@ -74,6 +74,9 @@ def test_bench_defaults():
     for n in (2, 4, 8):
         assert bench.parse(["--gpus", str(n)]).config == "c2"
     assert bench.CONFIGS["c4"]["count"] * 8 == 256 * 1024
+    # tuning arguments default to the product's choices (0 = not set)
+    assert a.rows == 0 and a.msg_rows == 0 and a.lanes == 0
+    assert bench.parse(["--rows", "4", "--msg-rows", "2"]).rows == 4
 
 
 def _run_bench(*argv, timeout=240):
