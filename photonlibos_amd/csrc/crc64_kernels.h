@@ -32,6 +32,15 @@
 #ifndef PCRC64_ROLL
 #define PCRC64_ROLL 1
 #endif
+// Table steps: 0 = the value rotated per lane (2 v_perm) so that lookup i
+// takes byte i, conflict-free; 1 = no rotation, lookup i takes byte
+// (i + q) % 4 of half i / 4 through a per-lane selector (4 fewer v_perm per
+// 16-byte block, 2-way bank conflicts: lanes l and l + 16 share a bank pair).
+// 1 measured slower, the LDS array being near its limit: C3 shape 0.790 vs
+// 0.805, C2 shape 0.806 vs 0.847 (repo:profiles/r06s_ab_crc64_half_local.jsonl).
+#ifndef PCRC64_HALF
+#define PCRC64_HALF 0
+#endif
 
 namespace pcrc {
 
@@ -105,6 +114,8 @@ struct LaneAddr64 {
     uint32_t rot_lo, rot_hi;   // v_perm selectors rotating a 64-bit value right by 8q bits
     uint32_t off[8];           // off_i = ((i+q)%8)*32 + (lane%4)*8 | 1<<16
     uint32_t r8;               // (lane%4)*8, for the byte-serial tail
+    uint32_t hoff[4];          // PCRC64_HALF: b_j*32 + (lane%4)*8 | 1<<16, b_j = (j + q) % 4
+    uint32_t hsel[2][4];       // PCRC64_HALF: {off.byte0, half.byte b_j, 0 | off.byte2, 0} (D | S)
 };
 
 __device__ __forceinline__ LaneAddr64 lane_addr64(uint32_t lane) {
@@ -122,6 +133,14 @@ __device__ __forceinline__ LaneAddr64 lane_addr64(uint32_t lane) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.off[i] = (((i + q) & 7u) << 5) | (r << 3) | (1u << 16);
     a.r8 = r << 3;
+    const uint32_t qh = (lane >> 2) & 3u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t b = (j + qh) & 3u;
+        a.hoff[j] = (b << 5) | (r << 3) | (1u << 16);
+        a.hsel[0][j] = 0x0C0C0000u | ((4u + b) << 8);
+        a.hsel[1][j] = 0x0C020000u | ((4u + b) << 8);
+    }
     return a;
 }
 
@@ -137,9 +156,25 @@ __device__ __forceinline__ uint2 look64(const uint32_t* lds, uint2 xr, const Lan
     return lds_u2(lds, __builtin_amdgcn_perm(half, a.off[I], sel));
 }
 
+// PCRC64_HALF: lookup i of the unrotated value, slice 4 (i / 4) + b_(i % 4)
+// (the second half's slices at +128 B: the instruction's offset field).
+template <int I, int TS>
+__device__ __forceinline__ uint2 look64h(const uint32_t* lds, uint2 x, const LaneAddr64& a) {
+    const uint32_t half = I < 4 ? x.x : x.y;
+    return lds_u2(lds, __builtin_amdgcn_perm(half, a.hoff[I & 3], a.hsel[TS][I & 3]) + (I < 4 ? 0u : 128u));
+}
+
 // Table product of x (8 lookups) XORed with e: 4 v_bitop3 per half.
 template <int TS>
 __device__ __forceinline__ uint2 step64(const uint32_t* lds, uint2 x, const LaneAddr64& a, uint2 e) {
+    if constexpr (PCRC64_HALF) {
+        const uint2 l0 = look64h<0, TS>(lds, x, a), l1 = look64h<1, TS>(lds, x, a);
+        const uint2 l2 = look64h<2, TS>(lds, x, a), l3 = look64h<3, TS>(lds, x, a);
+        const uint2 l4 = look64h<4, TS>(lds, x, a), l5 = look64h<5, TS>(lds, x, a);
+        const uint2 l6 = look64h<6, TS>(lds, x, a), l7 = look64h<7, TS>(lds, x, a);
+        return make_uint2(xor3(xor3(l0.x, l1.x, l2.x), xor3(l3.x, l4.x, l5.x), xor3(l6.x, l7.x, e.x)),
+                          xor3(xor3(l0.y, l1.y, l2.y), xor3(l3.y, l4.y, l5.y), xor3(l6.y, l7.y, e.y)));
+    }
     const uint2 xr = rot64(x, a);
     const uint2 l0 = look64<0, TS>(lds, xr, a), l1 = look64<1, TS>(lds, xr, a);
     const uint2 l2 = look64<2, TS>(lds, xr, a), l3 = look64<3, TS>(lds, xr, a);
