@@ -133,13 +133,15 @@ __device__ __forceinline__ LaneAddr64 lane_addr64(uint32_t lane) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.off[i] = (((i + q) & 7u) << 5) | (r << 3) | (1u << 16);
     a.r8 = r << 3;
-    const uint32_t qh = (lane >> 2) & 3u;
+    if constexpr (PCRC64_HALF) {
+        const uint32_t qh = (lane >> 2) & 3u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t b = (j + qh) & 3u;
-        a.hoff[j] = (b << 5) | (r << 3) | (1u << 16);
-        a.hsel[0][j] = 0x0C0C0000u | ((4u + b) << 8);
-        a.hsel[1][j] = 0x0C020000u | ((4u + b) << 8);
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t b = (j + qh) & 3u;
+            a.hoff[j] = (b << 5) | (r << 3) | (1u << 16);
+            a.hsel[0][j] = 0x0C0C0000u | ((4u + b) << 8);
+            a.hsel[1][j] = 0x0C020000u | ((4u + b) << 8);
+        }
     }
     return a;
 }
