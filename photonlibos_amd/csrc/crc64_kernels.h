@@ -41,6 +41,11 @@
 #ifndef PCRC64_HALF
 #define PCRC64_HALF 0
 #endif
+// Finish-table addresses (nib_mul64): 1 = nibble and position joined by an
+// OR (2 VALU per lookup), 0 = shift, mask and add (3; A/B builds).
+#ifndef PCRC64_NIB_OR
+#define PCRC64_NIB_OR 1
+#endif
 
 namespace pcrc {
 
@@ -375,8 +380,16 @@ __device__ __forceinline__ uint64_t nib_mul64(uint64_t x, const uint32_t* lds, u
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const uint32_t half = i < 8 ? (uint32_t)xr : (uint32_t)(xr >> 32);
+#if PCRC64_NIB_OR
+        // base is a multiple of 2 KiB and the position offset < 128: the
+        // nibble goes to bits 7-10 by one shift and (sh & 0x780) | pos in one
+        // v_bitop3 (truth table 0xEA), instead of shift, mask and add
+        const uint32_t sh = 4 * (i & 7) >= 7 ? half >> (4 * (i & 7) - 7) : half << (7 - 4 * (i & 7));
+        v[i] = lds_u2(lds, __builtin_amdgcn_bitop3_b32(sh, 0x780u, base + (((uint32_t)i + r) & 15u) * 8u, 0xEA));
+#else
         const uint32_t nib = (half >> (4 * (i & 7))) & 15u;
         v[i] = lds_u2(lds, base + nib * 128u + (((uint32_t)i + r) & 15u) * 8u);
+#endif
     }
     uint32_t lo = xor3(xor3(v[0].x, v[1].x, v[2].x), xor3(v[3].x, v[4].x, v[5].x), xor3(v[6].x, v[7].x, v[8].x));
     uint32_t hi = xor3(xor3(v[0].y, v[1].y, v[2].y), xor3(v[3].y, v[4].y, v[5].y), xor3(v[6].y, v[7].y, v[8].y));

@@ -1,0 +1,101 @@
+"""Does the payload's placement change a batch kernel's rate? (bench-only)
+
+One process, one library: the C3-shape batch (1 Mi x 4 KiB, CRC-64 full-row
+kernel by default, KIND=crc32 for CRC-32C) over several 4 GiB copies of the
+same bytes at different device addresses, alternating blocks of launches so
+that every copy sees the same power state. Prints one JSON line per copy:
+base address modulo 2 MiB / 1 GiB and the median launch rate.
+
+  ALLOCS=torch,hip,contig BLOCKS=6 PER=60 KIND=crc64|crc32 SHAPE=c3|c2 PRE_GIB=0 python scripts/probe_placement.py
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from photonlibos_amd import checksum as ck  # noqa: E402
+
+GIB = 1 << 30
+N, CNT = (65536, 1 << 16) if os.environ.get("SHAPE", "c3") == "c2" else (4096, 1 << 20)
+BLOCKS = int(os.environ.get("BLOCKS", "6"))
+PER = int(os.environ.get("PER", "60"))
+KIND = os.environ.get("KIND", "crc64")
+SKEW = int(os.environ.get("SKEW_KIB", "0")) << 10  # copy k starts k * SKEW past a 2 MiB boundary
+PRE = int(os.environ.get("PRE_GIB", "0"))  # GiB allocated (and held) before the first copy
+# how each copy is allocated: torch (caching allocator), hip (hipMalloc through
+# the library's runtime, photon_crc_device_alloc), contig (hipExtMallocWithFlags
+# hipDeviceMallocContiguous in that runtime)
+ALLOCS = os.environ.get("ALLOCS", "torch,torch,torch").split(",")
+COPIES = len(ALLOCS)
+
+st = torch.cuda.Stream()
+bufs, outs, keep = [], [], []
+if PRE:
+    keep.append(torch.empty(PRE << 30, dtype=torch.uint8, device="cuda"))
+hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime the library is linked to (already loaded)
+
+
+class Dev:
+    def __init__(self, p):
+        self.p = p
+
+    def data_ptr(self):
+        return self.p
+
+
+for k, how in enumerate(ALLOCS):
+    size = N * CNT + (4 << 20)
+    if how == "torch":
+        raw = torch.empty(size, dtype=torch.uint8, device="cuda")
+        base = raw.data_ptr()
+    else:
+        p = ctypes.c_void_p()
+        if how == "hip":
+            rc = ck.lib().photon_crc_device_alloc(ctypes.byref(p), ctypes.c_uint64(size))
+        else:
+            rc = hip.hipExtMallocWithFlags(ctypes.byref(p), ctypes.c_size_t(size), ctypes.c_uint(4))
+        assert rc == 0 and p.value, (how, rc)
+        raw, base = p, p.value
+    off = (-base) % (2 << 20) + k * SKEW
+    view = Dev(base + off)
+    ck.fill_splitmix(view, N, N, CNT, 0x5EED0003, stream=st)
+    keep.append(raw)
+    bufs.append(view)
+    outs.append(torch.zeros(CNT, dtype=torch.int64 if KIND == "crc64" else torch.int32, device="cuda"))
+torch.cuda.synchronize()
+
+
+def launch(k):
+    if KIND == "crc64":
+        ck.batch64_strided(bufs[k], N, N, CNT, outs[k], stream=st)
+    else:
+        ck.batch_strided(bufs[k], N, N, CNT, outs[k], stream=st)
+
+
+for k in range(COPIES):  # warm
+    for _ in range(10):
+        launch(k)
+st.synchronize()
+times = [[] for _ in range(COPIES)]
+for b in range(BLOCKS):
+    for k in range(COPIES):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(PER + 1)]
+        with torch.cuda.stream(st):
+            ev[0].record(st)
+            for i in range(PER):
+                launch(k)
+                ev[i + 1].record(st)
+        st.synchronize()
+        times[k] += [ev[i].elapsed_time(ev[i + 1]) for i in range(PER)]
+for k in range(COPIES):
+    same = bool(torch.equal(outs[k], outs[0]))
+    how = ALLOCS[k]
+    ms = float(np.median(times[k]))
+    print(json.dumps({"kind": KIND, "shape": os.environ.get("SHAPE", "c3"), "pre_gib": PRE, "copy": k, "alloc": how, "base_mod_2MiB": bufs[k].data_ptr() % (2 << 20),
+                      "base_mod_1GiB": bufs[k].data_ptr() % GIB, "base_hex": hex(bufs[k].data_ptr()),
+                      "median_ms": round(ms, 4), "frac_of_8TBps": round(N * CNT / (ms * 1e-3) / 8e12, 4),
+                      "same_crcs_as_copy0": same}), flush=True)
