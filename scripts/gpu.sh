@@ -53,9 +53,10 @@ run_one() {
       bash scripts/pmc_kernel.sh $1 $O/sq_$1 > /dev/null || { echo "sq $1 failed"; return 1; } ;;
     probe)
       local s=$1; shift
-      timeout -k 10 600 python -u scripts/$s "$@" > $O/probe_${s%.py}_$n.jsonl 2> $O/probe_${s%.py}_$n.err \
-        || { echo "probe $s failed"; tail -20 $O/probe_${s%.py}_$n.err; return 1; }
-      cut -c1-300 $O/probe_${s%.py}_$n.jsonl ;;
+      local pn; pn=$O/probe_${s%.py}_$(date +%s)_$n  # unique across gpu.sh invocations of one call
+      timeout -k 10 600 python -u scripts/$s "$@" > $pn.jsonl 2> $pn.err \
+        || { echo "probe $s failed"; tail -20 $pn.err; return 1; }
+      cut -c1-300 $pn.jsonl ;;
     ab)
       local lib=$1 rounds=$2; shift 2
       for r in $(seq 1 $rounds); do

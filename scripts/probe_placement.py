@@ -31,6 +31,26 @@ PRE = int(os.environ.get("PRE_GIB", "0"))  # GiB allocated (and held) before the
 # hipDeviceMallocContiguous in that runtime)
 ALLOCS = os.environ.get("ALLOCS", "torch,torch,torch").split(",")
 COPIES = len(ALLOCS)
+# engine settings compared on every copy, in the same process: VARIANTS is a
+# comma list of specs, each '+'-joined tokens: lN (lanes per buffer), rN
+# (generic-kernel rows per step), fMrN (CRC-64 full-row mode M, N rows), d
+# (the product default); LANES=8,16 is short for VARIANTS=l8,l16
+LANES = os.environ.get("VARIANTS") or ",".join("l" + x for x in os.environ.get("LANES", "0").split(","))
+LANES = LANES.split(",")
+
+
+def apply(spec):
+    ck.set_lanes_per_buffer(0)
+    ck.set_generic_rows(-1)
+    ck.set_full_rows64(3, 2)
+    for t in spec.split("+"):
+        if t.startswith("l"):
+            ck.set_lanes_per_buffer(int(t[1:]))
+        elif t.startswith("f"):
+            m, r = t[1:].split("r")
+            ck.set_full_rows64(int(m), int(r))
+        elif t.startswith("r"):
+            ck.set_generic_rows(int(t[1:]))
 
 st = torch.cuda.Stream()
 bufs, outs, keep = [], [], []
@@ -80,22 +100,27 @@ for k in range(COPIES):  # warm
     for _ in range(10):
         launch(k)
 st.synchronize()
-times = [[] for _ in range(COPIES)]
+times = {(k, g): [] for k in range(COPIES) for g in LANES}
+same = True
 for b in range(BLOCKS):
     for k in range(COPIES):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(PER + 1)]
-        with torch.cuda.stream(st):
-            ev[0].record(st)
-            for i in range(PER):
-                launch(k)
-                ev[i + 1].record(st)
-        st.synchronize()
-        times[k] += [ev[i].elapsed_time(ev[i + 1]) for i in range(PER)]
-for k in range(COPIES):
-    same = bool(torch.equal(outs[k], outs[0]))
+        for g in LANES:
+            apply(g)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(PER + 1)]
+            with torch.cuda.stream(st):
+                ev[0].record(st)
+                for i in range(PER):
+                    launch(k)
+                    ev[i + 1].record(st)
+            st.synchronize()
+            times[(k, g)] += [ev[i].elapsed_time(ev[i + 1]) for i in range(PER)]
+            same = same and bool(torch.equal(outs[k], outs[0]))
+apply("d")
+for (k, g), tl in times.items():
     how = ALLOCS[k]
-    ms = float(np.median(times[k]))
-    print(json.dumps({"kind": KIND, "shape": os.environ.get("SHAPE", "c3"), "pre_gib": PRE, "copy": k, "alloc": how, "base_mod_2MiB": bufs[k].data_ptr() % (2 << 20),
+    ms = float(np.median(tl))
+    print(json.dumps({"kind": KIND, "shape": os.environ.get("SHAPE", "c3"), "pre_gib": PRE, "copy": k, "alloc": how,
+                      "variant": g, "base_mod_2MiB": bufs[k].data_ptr() % (2 << 20),
                       "base_mod_1GiB": bufs[k].data_ptr() % GIB, "base_hex": hex(bufs[k].data_ptr()),
                       "median_ms": round(ms, 4), "frac_of_8TBps": round(N * CNT / (ms * 1e-3) / 8e12, 4),
-                      "same_crcs_as_copy0": same}), flush=True)
+                      "same_crcs_everywhere": same}), flush=True)
