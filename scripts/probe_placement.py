@@ -33,7 +33,8 @@ ALLOCS = os.environ.get("ALLOCS", "torch,torch,torch").split(",")
 COPIES = len(ALLOCS)
 # engine settings compared on every copy, in the same process: VARIANTS is a
 # comma list of specs, each '+'-joined tokens: lN (lanes per buffer), rN
-# (generic-kernel rows per step), fMrN (CRC-64 full-row mode M, N rows), d
+# (generic-kernel rows per step), fMrN (CRC-64 full-row mode M, N rows), gN
+# (workgroups of the persistent grid), d
 # (the product default); LANES=8,16 is short for VARIANTS=l8,l16
 LANES = os.environ.get("VARIANTS") or ",".join("l" + x for x in os.environ.get("LANES", "0").split(","))
 LANES = LANES.split(",")
@@ -43,6 +44,7 @@ def apply(spec):
     ck.set_lanes_per_buffer(0)
     ck.set_generic_rows(-1)
     ck.set_full_rows64(3, 2)
+    ck.lib().photon_crc_set_batch_grid(0)
     for t in spec.split("+"):
         if t.startswith("l"):
             ck.set_lanes_per_buffer(int(t[1:]))
@@ -51,6 +53,8 @@ def apply(spec):
             ck.set_full_rows64(int(m), int(r))
         elif t.startswith("r"):
             ck.set_generic_rows(int(t[1:]))
+        elif t.startswith("g"):
+            ck.lib().photon_crc_set_batch_grid(int(t[1:]))
 
 st = torch.cuda.Stream()
 bufs, outs, keep = [], [], []
