@@ -6,7 +6,7 @@ same bytes at different device addresses, alternating blocks of launches so
 that every copy sees the same power state. Prints one JSON line per copy:
 base address modulo 2 MiB / 1 GiB and the median launch rate.
 
-  ALLOCS=torch,hip,contig BLOCKS=6 PER=60 KIND=crc64|crc32 SHAPE=c3|c2 PRE_GIB=0 python scripts/probe_placement.py
+  ALLOCS=torch,hip,contig BLOCKS=6 PER=60 KIND=crc64|crc32 SHAPE=c3|c2|c5|c5_chain PRE_GIB=0 python scripts/probe_placement.py
 """
 import ctypes
 import json
@@ -20,7 +20,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from photonlibos_amd import checksum as ck  # noqa: E402
 
 GIB = 1 << 30
-N, CNT = (65536, 1 << 16) if os.environ.get("SHAPE", "c3") == "c2" else (4096, 1 << 20)
+SHAPE = os.environ.get("SHAPE", "c3")
+# c5 / c5_chain: 64 Ki messages x 8 scattered 8 KiB segments (bench.py's C5
+# layout: a random permutation of the pool's slots), CRC-32C only
+N, CNT = {"c2": (65536, 1 << 16), "c5": (8192, 1 << 19), "c5_chain": (8192, 1 << 19)}.get(SHAPE, (4096, 1 << 20))
+NSEG = 8
 BLOCKS = int(os.environ.get("BLOCKS", "6"))
 PER = int(os.environ.get("PER", "60"))
 KIND = os.environ.get("KIND", "crc64")
@@ -45,6 +49,8 @@ def apply(spec):
     ck.set_generic_rows(-1)
     ck.set_full_rows64(3, 2)
     ck.lib().photon_crc_set_batch_grid(0)
+    ck.set_msg_mode(0)
+    ck.set_msg_rows(2)
     for t in spec.split("+"):
         if t.startswith("l"):
             ck.set_lanes_per_buffer(int(t[1:]))
@@ -55,9 +61,13 @@ def apply(spec):
             ck.set_generic_rows(int(t[1:]))
         elif t.startswith("g"):
             ck.lib().photon_crc_set_batch_grid(int(t[1:]))
+        elif t.startswith("m"):  # mM: message form (0 auto, 1 one kernel, 2 segments + fold)
+            ck.set_msg_mode(int(t[1:]))
+        elif t.startswith("u"):  # uN: rows per step of the one-kernel message form
+            ck.set_msg_rows(int(t[1:]))
 
 st = torch.cuda.Stream()
-bufs, outs, keep = [], [], []
+bufs, outs, keep, msgs = [], [], [], []
 if PRE:
     keep.append(torch.empty(PRE << 30, dtype=torch.uint8, device="cuda"))
 hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime the library is linked to (already loaded)
@@ -90,11 +100,25 @@ for k, how in enumerate(ALLOCS):
     keep.append(raw)
     bufs.append(view)
     outs.append(torch.zeros(CNT, dtype=torch.int64 if KIND == "crc64" else torch.int32, device="cuda"))
+    if SHAPE.startswith("c5"):
+        perm = np.random.default_rng(0x5EED0005).permutation(CNT).astype(np.uint64)
+        iov = np.empty((CNT, 2), np.uint64)
+        iov[:, 0] = np.uint64(view.data_ptr()) + perm * np.uint64(N)
+        iov[:, 1] = N
+        msgs.append((torch.from_numpy(iov.view(np.int64)).cuda(),
+                     torch.zeros(CNT // NSEG, dtype=torch.int32, device="cuda"),
+                     torch.zeros(CNT, dtype=torch.int32, device="cuda") if SHAPE == "c5" else None))
 torch.cuda.synchronize()
 
 
+start = torch.from_numpy(np.arange(0, CNT + 1, NSEG, dtype=np.uint64).view(np.int64)).cuda()
+
+
 def launch(k):
-    if KIND == "crc64":
+    if SHAPE.startswith("c5"):
+        iov, mout, sout = msgs[k]
+        ck.batch_msg_n(iov, start, CNT // NSEG, CNT, sout, mout, stream=st)
+    elif KIND == "crc64":
         ck.batch64_strided(bufs[k], N, N, CNT, outs[k], stream=st)
     else:
         ck.batch_strided(bufs[k], N, N, CNT, outs[k], stream=st)
@@ -118,12 +142,15 @@ for b in range(BLOCKS):
                     ev[i + 1].record(st)
             st.synchronize()
             times[(k, g)] += [ev[i].elapsed_time(ev[i + 1]) for i in range(PER)]
-            same = same and bool(torch.equal(outs[k], outs[0]))
+            if SHAPE.startswith("c5"):
+                same = same and bool(torch.equal(msgs[k][1], msgs[0][1]))
+            else:
+                same = same and bool(torch.equal(outs[k], outs[0]))
 apply("d")
 for (k, g), tl in times.items():
     how = ALLOCS[k]
     ms = float(np.median(tl))
-    print(json.dumps({"kind": KIND, "shape": os.environ.get("SHAPE", "c3"), "pre_gib": PRE, "copy": k, "alloc": how,
+    print(json.dumps({"kind": KIND, "shape": SHAPE, "pre_gib": PRE, "copy": k, "alloc": how,
                       "variant": g, "base_mod_2MiB": bufs[k].data_ptr() % (2 << 20),
                       "base_mod_1GiB": bufs[k].data_ptr() % GIB, "base_hex": hex(bufs[k].data_ptr()),
                       "median_ms": round(ms, 4), "frac_of_8TBps": round(N * CNT / (ms * 1e-3) / 8e12, 4),
